@@ -1,0 +1,1090 @@
+/*
+ * dsp.h -- DSP / vector / math / LPC / FFT library of the MELPe engine.
+ *
+ * Restates, with the same fixed-point arithmetic, melpe/dsp_sub.c,
+ * melpe/mat_lib.c, melpe/math_lib.c, melpe/lpc_lib.c and melpe/fft_lib.c.
+ * Every routine runs on one lane (one channel) of a wavefront; the caller
+ * supplies all state explicitly (there are no statics: the reference's lazily
+ * computed tables live in g_der, see tables.h).  Heap scratch of the
+ * reference (v_get, melpe/mat_lib.c:578) becomes fixed-size locals.
+ */
+#ifndef MELPE_DSP_H
+#define MELPE_DSP_H
+
+#include "ops.h"
+#include "tables.h"
+
+namespace mlp {
+
+/* ------------------------------------------------------------------ */
+/* vectors: melpe/mat_lib.c                                           */
+/* ------------------------------------------------------------------ */
+
+MD void v_copy(int16_t *d, const int16_t *s, int n)	/* v_equ :136 */
+{
+	for (int i = 0; i < n; i++)
+		d[i] = s[i];
+}
+
+MD void v_copy32(int32_t *d, const int32_t *s, int n)	/* L_v_equ :237 */
+{
+	for (int i = 0; i < n; i++)
+		d[i] = s[i];
+}
+
+MD void v_zero(int16_t *d, int n)	/* v_zap :567 */
+{
+	for (int i = 0; i < n; i++)
+		d[i] = 0;
+}
+
+MD void v_set(int16_t *d, int16_t val, int n)	/* fill dsp_sub.c:87 */
+{
+	for (int i = 0; i < n; i++)
+		d[i] = val;
+}
+
+MD void v_add(int16_t *a, const int16_t *b, int n)	/* :87 */
+{
+	for (int i = 0; i < n; i++)
+		a[i] = add(a[i], b[i]);
+}
+
+MD void v_sub(int16_t *a, const int16_t *b, int n)	/* :520 */
+{
+	for (int i = 0; i < n; i++)
+		a[i] = sub(a[i], b[i]);
+}
+
+MD void v_equ_shr(int16_t *d, const int16_t *s, int16_t sc, int n)	/* :186 */
+{
+	for (int i = 0; i < n; i++)
+		d[i] = shr(s[i], sc);
+}
+
+MD void v_scale(int16_t *a, int16_t sc, int n)	/* :409 */
+{
+	for (int i = 0; i < n; i++)
+		a[i] = mult(a[i], sc);
+}
+
+MD void v_scale_shl(int16_t *a, int16_t sc, int n, int16_t sh)	/* :462 */
+{
+	for (int i = 0; i < n; i++)
+		a[i] = extract_h(L_shl(L_mult(a[i], sc), sh));
+}
+
+/* L_v_inner :293 -- sum of products, then shift to the output Q */
+MD Word32 L_v_inner(const int16_t *a, const int16_t *b, int n,
+		    int16_t qa, int16_t qb, int16_t qout)
+{
+	Word32 acc = 0;
+	for (int i = 0; i < n; i++)
+		acc = L_mac(acc, a[i], b[i]);
+	return L_shl(acc, sub(qout, add(add(qa, qb), 1)));
+}
+
+/* L_v_magsq :352 */
+MD Word32 L_v_magsq(const int16_t *a, int n, int16_t qa, int16_t qout)
+{
+	Word32 acc = 0;
+	for (int i = 0; i < n; i++)
+		acc = L_mac(acc, a[i], a[i]);
+	return L_shl(acc, sub(sub(qout, shl(qa, 1)), 1));
+}
+
+/* ------------------------------------------------------------------ */
+/* math: melpe/math_lib.c                                             */
+/* ------------------------------------------------------------------ */
+
+/* L_divider2 :105 -- signed 32/32 -> Q15 division through divide_s */
+MD Word16 L_divider2(Word32 num, Word32 den, int16_t nsh, int16_t dsh)
+{
+	bool neg = (num < 0) != (den < 0);
+	int16_t k = 0;
+	Word32 d = L_abs(L_shl(den, dsh));
+	Word32 nn = L_abs(L_shr(num, nsh));
+	while (d > (Word32) SW_MAX_) {
+		d = L_shr(d, 1);
+		k = add(k, 1);
+	}
+	nn = L_shr(nn, k);
+	Word16 q = divide_s(extract_l(nn), extract_l(d));
+	return neg ? negate(q) : q;
+}
+
+/* log10_fxp :169 */
+MD Word16 log10_fxp(Word16 x, Word16 Q)
+{
+	const int16_t *lt = TB(log_table);
+	Word16 sh = sub(7, Q);
+	if (!x)
+		return (Word16) -SW_MAX_;
+	Word16 i2 = shr(x, 7);
+	while (!i2 && x) {
+		x = shl(x, 1);
+		sh = sub(sh, 1);
+		i2 = shr(x, 7);
+	}
+	Word16 i1 = sub(i2, 1);
+	Word16 frac = shl((Word16) (x & 127), 8);
+	Word16 ic = mult(sub(lt[i2], lt[i1]), frac);
+	Word32 acc = L_shr(L_mult(lt[1], sh), 2);
+	Word16 t = add(shr(lt[i1], 1), extract_l(acc));
+	return add(t, shr(ic, 1));
+}
+
+/* L_log10_fxp :242 */
+MD Word16 L_log10_fxp(Word32 x, Word16 Q)
+{
+	const int16_t *lt = TB(log_table);
+	Word16 sh = sub(23, Q);
+	if (!x)
+		return (Word16) -SW_MAX_;
+	Word16 i2 = extract_l(L_shr(x, 23));
+	while (!i2 && x) {
+		x = L_shl(x, 1);
+		sh = sub(sh, 1);
+		i2 = extract_l(L_shr(x, 23));
+	}
+	Word16 i1 = sub(i2, 1);
+	Word32 frac = L_shl(x & (Word32) 0x7fffff, 8);
+	Word16 ic = extract_h(L_mpy_ls(frac, sub(lt[i2], lt[i1])));
+	Word32 acc = L_shr(L_mult(lt[1], sh), 3);
+	Word16 t = add(shr(lt[i1], 2), extract_l(acc));
+	return add(t, shr(ic, 2));
+}
+
+/* pow10_fxp :308 */
+MD Word16 pow10_fxp(Word16 x, Word16 Q)
+{
+	const int16_t *tab = TB(pow10_table);
+	const int16_t *tens = TB(pow10_tens_table);
+	const int16_t *qt = TB(pow10_q_table);
+	Word16 tm = shr(x, 12);
+	if (tm < -4)
+		return 0;
+	if (tm > 4)
+		return SW_MAX_;
+	Word16 i1 = shr((Word16) (x & 0x0ff0), 4);
+	Word16 i2 = add(i1, 1);
+	Word16 frac = shl((Word16) (x & 0x000f), 11);
+	Word16 ic = mult(sub(tab[i2], tab[i1]), frac);
+	Word16 m = add(tab[i1], ic);
+	Word16 ti = add(tm, 4);
+	Word32 y = L_mult(tens[ti], m);
+	if (tm >= 0) {
+		y = L_shr(y, sub(12, Q));
+		Word16 r = extract_l(y);
+		if (extract_h(y))
+			r = SW_MAX_;
+		return r;
+	}
+	return extract_l(L_shr(y, sub(add(qt[ti], 12), Q)));
+}
+
+MD Word16 sqrt_fxp(Word16 x, Word16 Q)	/* :432 */
+{
+	if (!x)
+		return 0;
+	return pow10_fxp(shr(log10_fxp(x, Q), 1), Q);
+}
+
+MD Word16 L_sqrt_fxp(Word32 x, Word16 Q)	/* :471 (no halving: as the reference) */
+{
+	if (!x)
+		return 0;
+	return pow10_fxp(L_log10_fxp(x, Q), Q);
+}
+
+MD Word16 L_pow_fxp(Word32 x, Word16 pw, Word16 qin, Word16 qout)	/* :517 */
+{
+	if (!x)
+		return 0;
+	Word16 t = L_log10_fxp(x, qin);
+	t = mult(pw, shl(t, 1));
+	return pow10_fxp(t, qout);
+}
+
+/* sin_fxp :556 / cos_fxp :643 -- quarter-wave table interpolation */
+MD Word16 sin_fxp(Word16 x)
+{
+	const int16_t *tab = TB(sin_table);
+	bool neg = x < 0;
+	Word16 tx = neg ? negate(x) : x;
+	if (tx > 16384)
+		tx = sub(SW_MAX_, tx);
+	Word16 i1 = shr(tx, 7);
+	if (i1 == 128)
+		return neg ? negate(tab[i1]) : tab[i1];
+	Word16 m = shl(sub(tx, shl(i1, 7)), 8);
+	Word16 y = add(tab[i1], mult(m, sub(tab[i1 + 1], tab[i1])));
+	return neg ? negate(y) : y;
+}
+
+MD Word16 cos_fxp(Word16 x)
+{
+	const int16_t *tab = TB(cos_table);
+	bool neg = false;
+	Word16 tx = x < 0 ? negate(x) : x;
+	if (tx > 16384) {
+		tx = sub(SW_MAX_, tx);
+		neg = true;
+	}
+	Word16 i1 = shr(tx, 7);
+	if (i1 == 128)
+		return 0;
+	Word16 m = shl(sub(tx, shl(i1, 7)), 8);
+	Word16 y = add(tab[i1], mult(m, sub(tab[i1 + 1], tab[i1])));
+	return neg ? negate(y) : y;
+}
+
+/* sqrt_Q15 :733 -- Taylor series square root of a Q15 value */
+MD Word16 sqrt_Q15(Word16 x)
+{
+	if (x == 0)
+		return 0;
+	Word32 A = L_deposit_h(x);
+	Word16 sh = norm_l(A);
+	A = L_shl(A, sh);
+	bool odd = (sh & 1) != 0;
+	sh = negate(shl(sh, -1));
+	A = L_shl(A, -1);
+	A = L_sub(A, L_deposit_h(0x4000));
+	Word16 x2 = extract_h(A);
+	A = L_add(A, L_deposit_h(0x4000));
+	A = L_add(A, L_deposit_h(0x4000));
+	Word32 t = L_mult(x2, x2);
+	t = -t;
+	A = L_add(A, L_shl(t, -1));
+	t = L_mult((Word16) L_shl(t, -16), (Word16) L_shl(t, -16));
+	Word16 x24 = extract_h(t);
+	A = L_sub(A, L_mult(x24, 0x5000));
+	A = L_add(A, L_mult(0x7000, mult(x24, x2)));
+	Word32 cube = L_mult(mult(x2, x2), x2);
+	A = L_add(A, L_shl(cube, -1));
+	A = L_add(A, L_shl(0x80, 8));
+	if (odd) {
+		A = L_mult((Word16) L_shl(A, -16), 0x5A82);
+		A = L_add(A, L_shl(0x80, 8));
+	}
+	A = L_shl(A, sh);
+	return extract_h(A);
+}
+
+MD Word16 add_shr(Word16 a, Word16 b)	/* :781 */
+{
+	return (Word16) L_shr(L_add(L_deposit_l(a), L_deposit_l(b)), 1);
+}
+
+/* ------------------------------------------------------------------ */
+/* filters and helpers: melpe/dsp_sub.c                               */
+/* ------------------------------------------------------------------ */
+
+/* envelope :62 -- rectify + 2nd-order smoother; out[-1], out[-2] are history */
+MD void envelope(const int16_t *in, int16_t prev_in, int16_t *out, int n)
+{
+	Word16 pa = abs_s(prev_in);
+	for (int i = 0; i < n; i++) {
+		Word16 ca = abs_s(in[i]);
+		Word32 acc = L_shr(L_deposit_h(sub(ca, pa)), 5);
+		acc = L_mac(acc, 31565, out[i - 1]);
+		acc = L_mac(acc, -15415, out[i - 2]);
+		out[i] = r_ound(L_shl(acc, 1));
+		pa = ca;
+	}
+}
+
+/* interp_array :113 */
+MD void interp_array(const int16_t *prev, const int16_t *curr, int16_t *out,
+		     int16_t f, int n)
+{
+	if (f == 0) {
+		v_copy(out, prev, n);
+	} else if (f == SW_MAX_) {
+		v_copy(out, curr, n);
+	} else {
+		Word16 f2 = sub(SW_MAX_, f);
+		for (int i = 0; i < n; i++)
+			out[i] = add(mult(f, curr[i]), mult(f2, prev[i]));
+	}
+}
+
+MD Word16 interp_scalar(Word16 prev, Word16 curr, Word16 f)	/* :697 */
+{
+	Word16 o;
+	interp_array(&prev, &curr, &o, f, 1);
+	return o;
+}
+
+MD Word16 median3(const int16_t *in)	/* :136 */
+{
+	Word16 lo = Min_(in[0], in[1]), hi = Max_(in[0], in[1]), t = in[2];
+	if (t < lo)
+		return lo;
+	if (t > hi)
+		return hi;
+	return t;
+}
+
+/* Bit packer state: pack_code :160 / unpack_code :485 write/read LSB first,
+ * wsize bits per byte. */
+struct BitCursor {
+	unsigned char *p;
+	int16_t bit;
+};
+
+MD void pack_code(Word16 code, BitCursor *c, int16_t nbits, int16_t wsize)
+{
+	for (int i = 0; i < nbits; i++) {
+		Word16 b = (Word16) (code & 1);
+		if (c->bit == 0)
+			*c->p = (unsigned char) b;
+		else
+			*c->p |= (unsigned char) shl(b, c->bit);
+		c->bit = add(c->bit, 1);
+		if (c->bit >= wsize) {
+			c->bit = 0;
+			c->p++;
+		}
+		code = shr(code, 1);
+	}
+}
+
+MD int16_t unpack_code(BitCursor *c, Word16 *code, int16_t nbits, int16_t wsize,
+		       uint16_t erase_mask)
+{
+	Word16 v = 0;
+	int16_t ret = (int16_t) (*c->p & erase_mask);
+	for (int i = 0; i < nbits; i++) {
+		Word16 bit = c->bit;
+		v |= shl(shr((Word16) ((Word16) *c->p & shl(1, bit)), bit), (Word16) i);
+		c->bit = add(c->bit, 1);
+		if (c->bit >= wsize) {
+			c->bit = 0;
+			c->p++;
+		}
+	}
+	*code = v;
+	if (c->bit != 0)
+		ret |= *c->p & erase_mask;
+	return ret;
+}
+
+/* peakiness :200 -- L2/L1 ratio of a residual, Q11 */
+MD Word16 peakiness(const int16_t *in, int n)
+{
+	int16_t tb[512];
+	Word16 sc = 4;
+	v_equ_shr(tb, in, sc, n);
+	Word32 e = L_v_magsq(tb, n, 0, 1);
+	if (e) {
+		sc = sub(sc, shr(norm_l(e), 1));
+		if (sc < 0)
+			sc = 0;
+	} else {
+		sc = 0;
+	}
+	Word32 sabs = 0;
+	for (int i = 0; i < n; i++)
+		sabs = L_add(sabs, L_deposit_l(abs_s(in[i])));
+	if (sc)
+		v_equ_shr(tb, in, sc, n);
+	if (sabs <= 0)
+		return 0;
+	e = sc ? L_v_magsq(tb, n, 0, 0) : L_v_magsq(in, n, 0, 0);
+	e = L_deposit_l(L_sqrt_fxp(e, 0));
+	Word16 pf = L_divider2(e, sabs, 0, 0);
+	if (pf > 20723)
+		return SW_MAX_;
+	Word16 s1 = add(sc, 5);
+	Word16 rn = sqrt_fxp(shl((Word16) n, 7), 7);
+	return extract_h(L_shl(L_mult(pf, rn), s1));
+}
+
+/* quant_u :259 -- uniform scalar quantiser, returns the index */
+MD void quant_u(int16_t *val, int16_t *idx, Word16 qmin, Word16 qmax,
+		Word16 nlev, Word16 nlev_q, bool dbl, Word16 scale)
+{
+	Word16 step = divide_s(sub(qmax, qmin), nlev_q);
+	int16_t i;
+	if (dbl) {
+		Word32 Lstep = L_deposit_l(step);
+		Word32 Lhalf = L_shr(Lstep, 1);
+		Word32 Lb = L_add(L_shl(L_deposit_l(qmin), scale), Lhalf);
+		Word32 Lin = L_shl(L_deposit_l(*val), scale);
+		for (i = 0; i < nlev; i++) {
+			if (Lin < Lb)
+				break;
+			Lb = L_add(Lb, Lstep);
+		}
+		*val = extract_l(L_shr(L_sub(Lb, Lhalf), scale));
+	} else {
+		step = shr(step, scale);
+		Word16 half = shr(step, 1);
+		Word16 b = add(qmin, half);
+		for (i = 0; i < nlev; i++) {
+			if (*val < b)
+				break;
+			b = add(b, step);
+		}
+		*val = sub(b, half);
+	}
+	*idx = i;
+}
+
+/* quant_u_dec :318 */
+MD Word16 quant_u_dec(Word16 idx, Word16 qmin, Word16 qmax, Word16 nlev_q, Word16 scale)
+{
+	Word16 step = divide_s(sub(qmax, qmin), nlev_q);
+	Word32 t = L_shr(L_mult(step, idx), 1);
+	t = L_add(L_shl(L_deposit_l(qmin), scale), t);
+	return extract_l(L_shr(t, scale));
+}
+
+/* rand_minstdgen :367 -- Park-Miller minimal standard generator computed
+ * with 16x16 products; *seed is the per-channel `next` (initially 1). */
+MD Word16 rand_minstdgen(uint32_t *seed)
+{
+	uint32_t nx = *seed;
+	uint16_t x0 = (uint16_t) extract_l((Word32) nx);
+	uint16_t x1 = (uint16_t) extract_h((Word32) nx);
+	uint32_t p, q, t1, t2, t3;
+	t1 = (uint32_t) 16807u * x1;
+	p = (uint32_t) L_shr((Word32) t1, 15);
+	t1 = (uint32_t) L_shl((Word32) (t1 & 0x00007fff), 16);
+	t2 = (uint32_t) 16807u * x0;
+	t3 = (uint32_t) L_sub(LW_MAX_, (Word32) t1);
+	if (t2 > t3) {
+		t1 = (uint32_t) L_sub((Word32) t1, (Word32) 0x7fffffff);
+		t1 = (uint32_t) L_sub((Word32) t1, 1);
+		q = (uint32_t) L_add((Word32) t1, (Word32) t2);
+		p = (uint32_t) L_add((Word32) p, 1);
+	} else {
+		q = (uint32_t) L_add((Word32) t1, (Word32) t2);
+	}
+	t3 = (uint32_t) L_sub(LW_MAX_, (Word32) p);
+	if (q > t3) {
+		t1 = (uint32_t) L_sub((Word32) p, (Word32) 0x7fffffff);
+		t1 = (uint32_t) L_add((Word32) t1, (Word32) q);
+	} else {
+		t1 = (uint32_t) L_add((Word32) p, (Word32) q);
+	}
+	*seed = t1;
+	return (Word16) (uint16_t) extract_h((Word32) t1);
+}
+
+MD void rand_num(int16_t *out, Word16 amp, int n, uint32_t *seed)	/* :343 */
+{
+	for (int i = 0; i < n; i++) {
+		Word16 t = sub(rand_minstdgen(seed), 16384);
+		out[i] = mult(amp, shl(t, 1));
+	}
+}
+
+MD void window(const int16_t *in, const int16_t *w, int16_t *out, int n)	/* :532 */
+{
+	for (int i = 0; i < n; i++)
+		out[i] = mult(w[i], in[i]);
+}
+
+MD void window_Q(const int16_t *in, const int16_t *w, int16_t *out, int n, Word16 qin)	/* :549 */
+{
+	Word16 sh = sub(15, qin);
+	for (int i = 0; i < n; i++)
+		out[i] = extract_h(L_shl(L_mult(w[i], in[i]), sh));
+}
+
+/* zerflt :569 / zerflt_Q :591 -- FIR over in[-order..n-1], run backwards so
+ * that in == out is allowed */
+MD void zerflt_Q(const int16_t *in, const int16_t *c, int16_t *out, int order,
+		 int n, Word16 qc)
+{
+	Word16 sc = sub(15, qc);
+	for (int i = n - 1; i >= 0; i--) {
+		Word32 acc = 0;
+		for (int j = 0; j <= order; j++)
+			acc = L_mac(acc, in[i - j], c[j]);
+		out[i] = r_ound(L_shl(acc, sc));
+	}
+}
+
+MD void zerflt(const int16_t *in, const int16_t *c, int16_t *out, int order, int n)
+{
+	zerflt_Q(in, c, out, order, n, 12);
+}
+
+/* iir_2nd_d :615 -- biquad with a double-precision (hi/lo) output memory */
+MD void iir_2nd_d(const int16_t *in, const int16_t *den, const int16_t *num,
+		  int16_t *out, int16_t *din, int16_t *dhi, int16_t *dlo, int n)
+{
+	for (int i = 0; i < n; i++) {
+		Word16 x = shr(in[i], 1);
+		Word32 acc = L_mult(dlo[0], den[1]);
+		acc = L_mac(acc, dlo[1], den[2]);
+		acc = L_shr(acc, 14);
+		acc = L_mac(acc, dhi[0], den[1]);
+		acc = L_mac(acc, dhi[1], den[2]);
+		acc = L_mac(acc, x, num[0]);
+		acc = L_mac(acc, din[0], num[1]);
+		acc = L_mac(acc, din[1], num[2]);
+		acc = L_shl(acc, 2);
+		din[1] = din[0];
+		din[0] = x;
+		dhi[1] = dhi[0];
+		dlo[1] = dlo[0];
+		dhi[0] = extract_h(acc);
+		dlo[0] = (Word16) (shr(extract_l(acc), 2) & 0x3FFF);
+		out[i] = r_ound(L_shl(acc, 1));
+	}
+}
+
+/* iir_2nd_s :660 -- biquad, single precision memories */
+MD void iir_2nd_s(const int16_t *in, const int16_t *den, const int16_t *num,
+		  int16_t *out, int16_t *din, int16_t *dout, int n)
+{
+	for (int i = 0; i < n; i++) {
+		Word16 x = in[i];
+		Word32 acc = L_mult(x, num[0]);
+		acc = L_mac(acc, din[0], num[1]);
+		acc = L_mac(acc, din[1], num[2]);
+		acc = L_mac(acc, dout[0], den[1]);
+		acc = L_mac(acc, dout[1], den[2]);
+		acc = L_shl(acc, 2);
+		din[1] = din[0];
+		din[0] = x;
+		Word16 y = r_ound(acc);
+		out[i] = y;
+		dout[1] = dout[0];
+		dout[0] = y;
+	}
+}
+
+/* ------------------------------------------------------------------ */
+/* LPC: melpe/lpc_lib.c                                               */
+/* ------------------------------------------------------------------ */
+
+/* lpc_acor :93 -- windowed, normalised autocorrelation with lag window */
+MD void lpc_acor(const int16_t *in, const int16_t *win, int16_t *r,
+		 Word16 hf_corr, int order, int n)
+{
+	const int16_t *lagw = TB(lagw_cof);
+	int16_t w[200];
+	Word16 nv, sf;
+	for (int i = 0; i < n; i++)
+		w[i] = mult(win[i], shr(in[i], 4));
+	Word32 e = L_v_magsq(w, n, 0, 1);
+	if (e) {
+		nv = sub(4, shr(norm_l(e), 1));
+		if (nv < 0)
+			nv = 0;
+	} else {
+		nv = 0;
+	}
+	for (int i = 0; i < n; i++)
+		w[i] = shr(mult(win[i], in[i]), nv);
+	e = L_v_magsq(w, n, 0, 1);
+	if (e > 0) {
+		nv = sub(norm_l(e), 1);
+		e = L_shl(e, nv);
+		e = L_add(e, L_mpy_ls(e, hf_corr));
+		Word16 t = norm_s(extract_h(e));
+		e = L_shl(e, t);
+		nv = add(nv, t);
+		r[0] = r_ound(e);
+		sf = divide_s(16382, r[0]);
+		e = L_shl(L_mpy_ls(e, sf), 1);
+		r[0] = r_ound(e);
+	} else {
+		nv = 0;
+		r[0] = SW_MAX_;
+		sf = 0;
+	}
+	for (int j = 1; j <= order; j++) {
+		Word32 acc = 0;
+		for (int i = j; i < n; i++)
+			acc = L_mac(acc, w[i], w[i - j]);
+		acc = L_shl(acc, nv);
+		acc = L_shl(L_mpy_ls(acc, sf), 1);
+		acc = L_mpy_ls(acc, lagw[j - 1]);
+		r[j] = r_ound(acc);
+	}
+}
+
+/* lpc_aejw :198 -- |A(e^jw)|^2 */
+MD Word32 lpc_aejw(const int16_t *lpc, Word16 omega, int order)
+{
+	if (order == 0)
+		return 524288L;
+	Word16 cs = cos_fxp(omega);
+	Word16 sn = negate(sin_fxp(omega));
+	Word16 a = lpc[order - 1];
+	Word16 re = shr(mult(cs, a), 3);
+	Word16 im = shr(mult(sn, a), 3);
+	for (int i = order - 2; i >= 0; i--) {
+		re = add(re, shr(lpc[i], 3));
+		Word16 t = im;
+		im = add(mult(cs, t), mult(sn, re));
+		re = sub(mult(cs, re), mult(sn, t));
+	}
+	re = add(re, 512);
+	Word32 m = L_add(L_mult(re, re), L_mult(im, im));
+	return m < 54 ? 54 : m;
+}
+
+MD void lpc_bwex(const int16_t *lpc, int16_t *aw, Word16 gamma, int order)	/* :271 */
+{
+	Word16 g = gamma;
+	for (int i = 0; i < order; i++) {
+		aw[i] = mult(lpc[i], g);
+		g = mult(g, gamma);
+	}
+}
+
+/* lpc_clmp :312 -- sort, then enforce a minimum LSF separation */
+MD void lpc_clmp(int16_t *lsp, Word16 delta, int order)
+{
+	bool unsorted = true;
+	for (int j = 0; unsorted && j < 10; j++) {
+		unsorted = false;
+		for (int i = 0; i < order - 1; i++)
+			if (lsp[i] > lsp[i + 1]) {
+				Word16 t = lsp[i + 1];
+				lsp[i + 1] = lsp[i];
+				lsp[i] = t;
+				unsorted = true;
+			}
+	}
+	if (unsorted)
+		return;
+	for (int j = 0; j < 10; j++) {
+		for (int i = 0; i < order - 1; i++) {
+			Word16 d = sub(lsp[i + 1], lsp[i]);
+			if (d >= delta)
+				continue;
+			Word16 s1, s2;
+			s1 = s2 = shr(sub(delta, d), 1);
+			if (i == 0 && lsp[i] < delta) {
+				s1 = shr(lsp[i], 1);
+			} else if (i > 0) {
+				Word16 t = sub(lsp[i], lsp[i - 1]);
+				if (t < delta)
+					s1 = 0;
+				else if (t < shl(delta, 1))
+					s1 = shr(sub(t, delta), 1);
+			}
+			if (i == order - 2 && lsp[i + 1] > sub(SW_MAX_, delta)) {
+				s2 = shr(sub(SW_MAX_, lsp[i + 1]), 1);
+			} else if (i < order - 2) {
+				Word16 t = sub(lsp[i + 2], lsp[i + 1]);
+				if (t < delta)
+					s2 = 0;
+				else if (t < shl(delta, 1))
+					s2 = shr(sub(t, delta), 1);
+			}
+			lsp[i] = sub(lsp[i], s1);
+			lsp[i + 1] = add(lsp[i + 1], s2);
+		}
+	}
+}
+
+/* lpc_refl2pred :531 */
+MD void lpc_refl2pred(const int16_t *refc, int16_t *lpc, int order)
+{
+	int16_t a1[16];
+	for (int i = 0; i < order; i++) {
+		lpc[i] = shift_r(refc[i], -3);
+		v_copy(a1, lpc, i);
+		for (int j = 0; j < i; j++)
+			lpc[j] = add(a1[j], mult(refc[i], a1[i - j - 1]));
+	}
+}
+
+/* lpc_schr :444 -- Schur recursion, returns the prediction error */
+MD Word16 lpc_schr(const int16_t *r, int16_t *lpc, int order)
+{
+	Word32 y1[16], y2[17];
+	int16_t refc[16];
+	refc[0] = divide_s(abs_s(r[1]), abs_s(r[0]));
+	if ((r[1] ^ r[0]) >= 0)
+		refc[0] = negate(refc[0]);
+	y2[0] = L_deposit_h(r[1]);
+	y2[1] = L_add(L_deposit_h(r[0]), L_mult(refc[0], r[1]));
+	for (int i = 1; i < order; i++) {
+		y1[0] = L_deposit_h(r[i + 1]);
+		Word32 acc = L_deposit_h(r[i + 1]);
+		for (int j = 0; j < i; j++) {
+			y1[j + 1] = L_add(y2[j], L_mpy_ls(acc, refc[j]));
+			acc = L_add(acc, L_mpy_ls(y2[j], refc[j]));
+		}
+		if (acc > y2[i]) {
+			v_zero(&refc[i], order - i);
+			break;
+		}
+		Word16 sh = norm_l(y2[i]);
+		Word16 t1 = abs_s(extract_h(L_shl(acc, sh)));
+		Word16 t2 = abs_s(extract_h(L_shl(y2[i], sh)));
+		refc[i] = divide_s(t1, t2);
+		if ((acc ^ y2[i]) >= 0)
+			refc[i] = negate(refc[i]);
+		y2[i + 1] = L_add(y2[i], L_mpy_ls(acc, refc[i]));
+		v_copy32(y2, y1, i + 1);
+	}
+	lpc_refl2pred(refc, lpc, order);
+	Word16 alpha = r[0];
+	for (int i = 0; i < order; i++)
+		alpha = mult(alpha, sub(SW_MAX_, mult(refc[i], refc[i])));
+	return alpha;
+}
+
+/* lsp_to_freq :626 -- root search of P/Q on a 257-point cosine grid */
+MD void lsp_to_freq(const int16_t *lsp, int16_t *freq, int order)
+{
+	const int16_t *lc = g_der.lsp_cos;
+	/* default_w = divide_s(ONE_Q11, order << 10), :654-655 */
+	Word16 dw = divide_s(2048, shl((Word16) order, 10));
+	Word16 dw0 = shr(dw, 1);
+	bool prev_less = true;
+	Word32 mag[3];
+	Word16 smag[3];
+	mag[0] = mag[1] = 0x7fffffff;
+	smag[0] = smag[1] = 0x7fff;
+	mag[2] = 0;
+	smag[2] = 0;
+	Word16 p2 = shr((Word16) order, 1);
+	Word16 count = 0;
+	for (int i = 0; i <= 256; i++) {
+		Word16 pc = (Word16) i;
+		Word32 acc = L_mult(lsp[p2], 8192);
+		for (int j = p2 - 1; j >= 0; j--) {
+			acc = L_add(acc, L_shr(L_mult(lsp[j], lc[pc]), 1));
+			pc = add(pc, (Word16) i);
+			if (pc > 511)
+				pc -= 512;
+		}
+		smag[2] = extract_h(acc);
+		mag[2] = L_abs(acc);
+		if (mag[2] < mag[1]) {
+			prev_less = true;
+		} else {
+			if (prev_less && (smag[0] ^ smag[2]) < 0) {
+				Word32 n1 = L_shr(L_sub(mag[0], mag[2]), 1);
+				Word32 d1 = L_add(L_sub(mag[0], L_shl(mag[1], 1)), mag[2]);
+				Word16 t = shr(L_divider2(n1, d1, 0, 0), 9);
+				t = add(shl(sub((Word16) i, 1), 6), t);
+				freq[count] = divide_s(t, shl(512, 5));
+				count = add(count, 1);
+			}
+			prev_less = false;
+		}
+		mag[0] = mag[1];
+		mag[1] = mag[2];
+		smag[0] = smag[1];
+		smag[1] = smag[2];
+	}
+	if (count != p2) {
+		freq[0] = dw0;
+		for (int i = 1; i < p2; i++)
+			freq[i] = add(freq[i - 1], dw);
+	}
+}
+
+/* lpc_pred2lsp :566 */
+MD void lpc_pred2lsp(const int16_t *lpc, int16_t *lsf, int order)
+{
+	Word32 Lp[6], Lq[6];
+	int16_t pc[6], qc[6], pf[6], qf[6];
+	Word16 p2 = shr((Word16) order, 1);
+	Lp[0] = Lq[0] = 67108864L;
+	for (int i = 1; i <= p2; i++) {
+		Word32 ai = L_shr(L_deposit_h(lpc[i - 1]), 2);
+		Word32 api = L_shr(L_deposit_h(lpc[order - i]), 2);
+		Lp[i] = L_add(L_sub(ai, api), Lp[i - 1]);
+		Lq[i] = L_sub(L_add(ai, api), Lq[i - 1]);
+	}
+	for (int i = 0; i <= p2; i++) {
+		pc[i] = r_ound(Lp[i]);
+		qc[i] = r_ound(Lq[i]);
+	}
+	lsp_to_freq(pc, pf, order);
+	lsp_to_freq(qc, qf, order);
+	for (int i = 0; i < p2; i++) {
+		lsf[2 * i] = qf[i];
+		lsf[2 * i + 1] = pf[i];
+	}
+}
+
+/* lpc_pred2refl :751 -- returns the residual energy, *refc = first refl. */
+MD Word16 lpc_pred2refl(const int16_t *lpc, int16_t *refc, int order)
+{
+	int16_t b[16], b1[16];
+	Word16 energy = SW_MAX_;
+	v_copy(b, lpc, order);
+	for (int i = order - 1; i >= 0; i--) {
+		if (b[i] >= 4096)
+			b[i] = 4095;
+		if (b[i] <= -4096)
+			b[i] = -4095;
+		Word32 acc = L_shl(L_sub(33554431L, L_mult(b[i], b[i])), 6);
+		energy = mult(energy, extract_h(acc));
+		Word16 sh = norm_l(acc);
+		Word16 e = extract_h(L_shl(acc, sh));
+		v_copy(b1, b, i);
+		for (int j = 0; j < i; j++) {
+			acc = L_mult(b[i], b1[i - j - 1]);
+			acc = L_sub(L_shl(L_deposit_l(b1[j]), 13), acc);
+			Word16 sgn = extract_h(acc);
+			acc = L_abs(acc);
+			Word16 s1 = norm_l(acc);
+			Word16 t = extract_h(L_shl(acc, s1));
+			if (t > e) {
+				t = shr(t, 1);
+				s1 = sub(s1, 1);
+			}
+			b[j] = divide_s(t, e);
+			s1 = sub(sub(s1, 3), sh);
+			b[j] = shr(b[j], s1);
+			if (sgn < 0)
+				b[j] = negate(b[j]);
+		}
+	}
+	*refc = shl(b[0], 3);
+	return energy;
+}
+
+/* lpc_lsp2pred :827 -- LSF (Q15) to predictor (Q12); clamps lsf in place */
+MD void lpc_lsp2pred(int16_t *lsf, int16_t *lpc, int order)
+{
+	Word32 f0[6], f1[6];
+	lpc_clmp(lsf, 0, order);
+	Word16 p2 = shr((Word16) order, 1);
+	f0[0] = f1[0] = 33554431L;
+	f0[1] = L_shr(L_deposit_h(negate(cos_fxp(lsf[0]))), 5);
+	f1[1] = L_shr(L_deposit_h(negate(cos_fxp(lsf[1]))), 5);
+	int k = 2;
+	for (int i = 2; i <= p2; i++) {
+		Word16 c0 = negate(cos_fxp(lsf[k++]));
+		Word16 c1 = negate(cos_fxp(lsf[k++]));
+		f0[i] = f0[i - 2];
+		f1[i] = f1[i - 2];
+		for (int j = i; j >= 2; j--) {
+			f0[j] = L_add(f0[j], L_add(L_shl(L_mpy_ls(f0[j - 1], c0), 1), f0[j - 2]));
+			f1[j] = L_add(f1[j], L_add(L_shl(L_mpy_ls(f1[j - 1], c1), 1), f1[j - 2]));
+		}
+		f0[1] = L_add(f0[1], L_shl(L_mpy_ls(f0[0], c0), 1));
+		f1[1] = L_add(f1[1], L_shl(L_mpy_ls(f1[0], c1), 1));
+	}
+	for (int i = p2 - 1; i >= 0; i--) {
+		f0[i + 1] = L_add(f0[i + 1], f0[i]);
+		f1[i + 1] = L_sub(f1[i + 1], f1[i]);
+		lpc[i] = extract_h(L_shl(L_add(f0[i + 1], f1[i + 1]), 2));
+		lpc[order - 1 - i] = extract_h(L_shl(L_sub(f0[i + 1], f1[i + 1]), 2));
+	}
+}
+
+/* lpc_syn :922 -- all-pole synthesis, y[-order..-1] is the memory */
+MD void lpc_syn(const int16_t *x, int16_t *y, const int16_t *a, int order, int n)
+{
+	for (int j = 0; j < n; j++) {
+		Word32 acc = L_shr(L_deposit_h(x[j]), 3);
+		for (int i = order; i > 0; i--)
+			acc = L_msu(acc, y[j - i], a[i - 1]);
+		y[j] = r_ound(L_shl(acc, 3));
+	}
+}
+
+/* ------------------------------------------------------------------ */
+/* FFT: melpe/fft_lib.c                                               */
+/* ------------------------------------------------------------------ */
+
+/* max |x| over d[0..n-1] through the saturating ops, as the reference */
+MD Word16 block_max(const int16_t *d, int n)
+{
+	Word16 m = 0;
+	for (int i = 0; i < n; i++) {
+		Word16 a = abs_s(d[i]);
+		if (sub(m, a) < 0)
+			m = a;
+	}
+	return m;
+}
+
+/* cfft :115 -- in-place radix-2 DIT complex FFT of nn points (2*nn shorts)
+ * with per-stage block floating point; returns the number of halvings. */
+MD Word16 cfft(int16_t *d0, Word16 nn)
+{
+	const int16_t *wrt = g_der.wr, *wit = g_der.wi;
+	int16_t *d = d0 - 1;	/* 1-based view, as the reference */
+	Word16 g = 0;
+	Word16 n = shl(nn, 1);
+	Word16 j = 1;
+	for (Word16 i = 1; i < n; i += 2) {
+		if (j > i) {
+			int16_t t = d[j];
+			d[j] = d[i];
+			d[i] = t;
+			t = d[j + 1];
+			d[j + 1] = d[i + 1];
+			d[i + 1] = t;
+		}
+		Word16 m = nn;
+		while (m >= 2 && j > m) {
+			j = sub(j, m);
+			m = shr(m, 1);
+		}
+		j = add(j, m);
+	}
+	if (block_max(d0, n) > 16383) {
+		g += 1;
+		for (int i = 0; i < n; i++)
+			d0[i] = shr(d0[i], 1);
+	}
+	for (int i = 0; i < n; i += 4) {
+		Word16 pr = d0[i], qr = d0[i + 2], pi = d0[i + 1], qi = d0[i + 3];
+		d0[i] = add(pr, qr);
+		d0[i + 2] = sub(pr, qr);
+		d0[i + 1] = add(pi, qi);
+		d0[i + 3] = sub(pi, qi);
+	}
+	if (block_max(d0, n) > 16383) {
+		g += 1;
+		for (int i = 0; i < n; i++)
+			d0[i] = shr(d0[i], 1);
+	}
+	for (int i = 0; i < n; i += 8) {
+		Word16 pr = d0[i], qr = d0[i + 4], pi = d0[i + 1], qi = d0[i + 5];
+		d0[i] = add(pr, qr);
+		d0[i + 4] = sub(pr, qr);
+		d0[i + 1] = add(pi, qi);
+		d0[i + 5] = sub(pi, qi);
+		pr = d0[i + 2];
+		qr = d0[i + 6];
+		pi = d0[i + 3];
+		qi = d0[i + 7];
+		d0[i + 2] = add(pr, qi);
+		d0[i + 6] = sub(pr, qi);
+		d0[i + 3] = sub(pi, qr);
+		d0[i + 7] = add(pi, qr);
+	}
+	Word16 mmax = 8;
+	Word16 istep_idx = shr(nn, 1);
+	while (n > mmax) {
+		Word16 mx = block_max(d0, n);
+		if (mx > 16383) {
+			g += 2;
+			for (int i = 0; i < n; i++)
+				d0[i] = shr(d0[i], 2);
+		} else if (mx > 8191) {
+			g += 1;
+			for (int i = 0; i < n; i++)
+				d0[i] = shr(d0[i], 1);
+		}
+		Word16 istep = shl(mmax, 1);
+		Word16 idx = 0;
+		istep_idx = shr(istep_idx, 1);
+		Word16 wr = SW_MAX_, wi = 0;
+		for (Word16 m = 1; m < mmax; m += 2) {
+			for (Word16 i = m; i <= n; i = add(i, istep)) {
+				Word16 jj = add(i, mmax);
+				Word32 tr = L_add(L_mult(wr, d[jj]), L_mult(wi, d[jj + 1]));
+				tr = L_add(tr, L_shl(0x80, 8));
+				tr = L_shl(L_shr(tr, 16), 16);
+				Word16 pr = d[i], qr = d[jj];
+				d[i] = extract_h(L_add(L_deposit_h(pr), tr));
+				d[jj] = extract_h(L_sub(L_deposit_h(pr), tr));
+				Word32 ti = L_sub(L_mult(wi, qr), L_mult(wr, d[jj + 1]));
+				ti = L_add(ti, L_shl(0x80, 8));
+				ti = L_shl(L_shr(ti, 16), 16);
+				Word16 pi = d[i + 1];
+				d[i + 1] = extract_h(L_sub(L_deposit_h(pi), ti));
+				d[jj + 1] = extract_h(L_add(L_deposit_h(pi), ti));
+			}
+			idx = add(idx, istep_idx);
+			wr = wrt[idx];
+			wi = wit[idx];
+		}
+		mmax = istep;
+	}
+	return g;
+}
+
+/* fft_npp :270 -- 256-point complex FFT, dir < 0 gives the inverse order */
+MD Word16 fft_npp(int16_t *d, Word16 dir)
+{
+	Word16 g = cfft(d, 256);
+	if (dir < 0) {
+		for (int n = 1; n < 128; n++) {
+			int16_t t = d[2 * n];
+			d[2 * n] = d[2 * (256 - n)];
+			d[2 * (256 - n)] = t;
+			t = d[2 * n + 1];
+			d[2 * n + 1] = d[2 * (256 - n) + 1];
+			d[2 * (256 - n) + 1] = t;
+		}
+	}
+	return g;
+}
+
+/* rfft :33 -- real FFT of n points through an n/2-point complex FFT;
+ * d must hold 2n shorts */
+MD void rfft(int16_t *d, Word16 n)
+{
+	const int16_t *wrt = g_der.wr, *wit = g_der.wi;
+	Word16 n2 = shr(n, 1);
+	cfft(d, n2);
+	if (block_max(d, n) > 16383)
+		for (int i = 0; i < n; i++)
+			d[i] = shr(d[i], 1);
+	for (int i = 2; i < n2; i += 2) {
+		Word16 r1 = add_shr(d[i], d[n - i]);
+		Word32 a = L_shl(L_sub(d[i + 1], d[n - i + 1]), 16);
+		Word16 r2 = add_shr(d[i + 1], d[n - i + 1]);
+		Word32 b = L_shl(L_sub(d[i], d[n - i]), 16);
+		d[i] = r1;
+		d[n - i] = r1;
+		d[2 * n - i + 1] = extract_h(L_shr(b, 1));
+		b = L_negate(b);
+		d[n + i + 1] = extract_h(L_shr(b, 1));
+		d[i + 1] = r2;
+		d[n - i + 1] = r2;
+		d[2 * n - i] = extract_h(L_shr(a, 1));
+		a = L_negate(a);
+		d[n + i] = extract_h(L_shr(a, 1));
+	}
+	d[n + n2] = 0;
+	d[n + n2 + 1] = 0;
+	Word16 r1 = add(d[0], d[1]);
+	Word16 i1 = sub(d[0], d[1]);
+	d[0] = r1;
+	d[1] = 0;
+	d[n] = i1;
+	d[n + 1] = 0;
+	int idx = 1;
+	Word16 wr = wrt[idx], wi = wit[idx];
+	for (int i = 2; i < n; i += 2) {
+		Word16 a1 = d[i], b1 = d[2 * n - i], a2 = d[i + 1], b2 = d[2 * n - i + 1];
+		Word32 t = L_deposit_h(a1);
+		t = L_add(t, L_mult(a2, wr));
+		t = L_add(t, L_shl(0x0080, 8));
+		t = L_shl(L_shr(t, 16), 16);
+		t = L_sub(t, L_mult(b2, wi));
+		t = L_add(t, L_shl(0x0080, 8));
+		d[i] = extract_h(t);
+		d[2 * n - i] = extract_h(t);
+		Word32 u = L_deposit_h(b1);
+		u = L_sub(u, L_mult(a2, wi));
+		u = L_add(u, L_shl(0x0080, 8));
+		u = L_shl(L_shr(u, 16), 16);
+		u = L_sub(u, L_mult(b2, wr));
+		u = L_add(u, L_shl(0x0080, 8));
+		d[i + 1] = extract_h(u);
+		d[2 * n - i + 1] = extract_h(L_negate(u));
+		idx += 1;
+		wr = wrt[idx];
+		wi = wit[idx];
+	}
+}
+
+}  // namespace mlp
+
+#endif

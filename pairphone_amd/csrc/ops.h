@@ -1,0 +1,295 @@
+/*
+ * ops.h -- saturating fixed-point basic operators, bit-exact with the
+ * reference's ETSI/TI-style library (melpe/mathhalf_i.h, melpe/mathdp31.c).
+ *
+ * Compiled for gfx950 (device code of the HIP kernels) and, for CPU-side
+ * testing only, for the host.  The definitions are closed forms that were
+ * checked against the reference's compiled operators (tests/test_basicops.py,
+ * exhaustive over the 16-bit domains, randomised over 32/40-bit ones):
+ *
+ *   add/sub/L_add            = clamp of the exact sum   (mathhalf_i.h:120,586,692)
+ *   L_sub                    = clamp, except L_sub(0, MIN32) = MIN32 (:719-730)
+ *   L_mult(a,b)              = sat(2ab)                 (:1387)
+ *   shl/shr/L_shl/L_shr      = saturating shift, right shifts capped (:781-1047)
+ *   norm_l(x)                = clz(x ^ x>>31) - 1       (:1256)
+ *   L40_*                    = int64 with a +-2^39 clamp (:1763-2168)
+ *
+ * On gfx950 the 32-bit saturating adds lower to v_add_i32 ... clamp.
+ */
+#ifndef MELPE_OPS_H
+#define MELPE_OPS_H
+
+#include <stdint.h>
+
+#if defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define MD __device__ __attribute__((always_inline)) inline
+#define MF __device__
+#define MDEV_CONST __device__
+#else
+#define MD static inline
+#define MF static
+#define MDEV_CONST
+#endif
+
+typedef int16_t Word16;
+typedef int32_t Word32;
+typedef int64_t Word40;
+
+#define SW_MAX_ 32767
+#define SW_MIN_ (-32768)
+#define LW_MAX_ ((int32_t) 0x7fffffff)
+#define LW_MIN_ ((int32_t) 0x80000000)
+#define MAX40_ ((int64_t) 1 << 39)
+#define MIN40_ (-((int64_t) 1 << 39))
+
+MD Word16 sat16(Word32 x)
+{
+	return (Word16) (x > SW_MAX_ ? SW_MAX_ : (x < SW_MIN_ ? SW_MIN_ : x));
+}
+
+MD Word32 sat_add32(Word32 a, Word32 b)
+{
+#if defined(__clang__)
+	return __builtin_elementwise_add_sat(a, b);
+#else
+	int64_t s = (int64_t) a + b;
+	return (Word32) (s > LW_MAX_ ? LW_MAX_ : (s < LW_MIN_ ? LW_MIN_ : s));
+#endif
+}
+
+MD Word32 sat_sub32(Word32 a, Word32 b)
+{
+#if defined(__clang__)
+	return __builtin_elementwise_sub_sat(a, b);
+#else
+	int64_t s = (int64_t) a - b;
+	return (Word32) (s > LW_MAX_ ? LW_MAX_ : (s < LW_MIN_ ? LW_MIN_ : s));
+#endif
+}
+
+MD Word16 add(Word16 a, Word16 b) { return sat16((Word32) a + b); }
+MD Word16 sub(Word16 a, Word16 b) { return sat16((Word32) a - b); }
+MD Word32 L_add(Word32 a, Word32 b) { return sat_add32(a, b); }
+
+MD Word32 L_sub(Word32 a, Word32 b)
+{
+	/* reference quirk: with a == 0 no overflow check is made and
+	 * 0 - MIN32 wraps to MIN32 (mathhalf_i.h:724-729) */
+	if (a == 0 && b == LW_MIN_)
+		return LW_MIN_;
+	return sat_sub32(a, b);
+}
+
+MD Word32 L_mult(Word16 a, Word16 b)
+{
+	Word32 p = (Word32) a * (Word32) b;
+	return sat_add32(p, p);
+}
+
+MD Word16 extract_h(Word32 x) { return (Word16) (x >> 16); }
+MD Word16 extract_l(Word32 x) { return (Word16) x; }
+MD Word32 L_deposit_h(Word16 a) { return (Word32) ((uint32_t) (int32_t) a << 16); }
+MD Word32 L_deposit_l(Word16 a) { return (Word32) a; }
+
+MD Word16 mult(Word16 a, Word16 b) { return extract_h(L_mult(a, b)); }
+MD Word32 L_mac(Word32 acc, Word16 a, Word16 b) { return sat_add32(acc, L_mult(a, b)); }
+/* L_mult never returns MIN32, so L_sub's quirk cannot trigger here */
+MD Word32 L_msu(Word32 acc, Word16 a, Word16 b) { return sat_sub32(acc, L_mult(a, b)); }
+MD Word16 r_ound(Word32 x) { return extract_h(sat_add32(x, 0x8000)); }
+MD Word16 msu_r(Word32 acc, Word16 a, Word16 b) { return r_ound(L_msu(acc, a, b)); }
+
+MD Word16 negate(Word16 a) { return a == SW_MIN_ ? (Word16) SW_MAX_ : (Word16) -a; }
+MD Word32 L_negate(Word32 a) { return a == LW_MIN_ ? LW_MAX_ : -a; }
+MD Word16 abs_s(Word16 a) { return a == SW_MIN_ ? (Word16) SW_MAX_ : (Word16) (a < 0 ? -a : a); }
+MD Word32 L_abs(Word32 a) { return a == LW_MIN_ ? LW_MAX_ : (a < 0 ? -a : a); }
+
+/* shl/shr: mathhalf_i.h:781-935 */
+MD Word16 shr(Word16 a, Word16 n);
+MD Word16 shl(Word16 a, Word16 n)
+{
+	if (n == 0 || a == 0)
+		return a;
+	if (n < 0) {
+		if (n <= -15)
+			return (Word16) (a < 0 ? -1 : 0);
+		return (Word16) (a >> (-n));
+	}
+	if (n >= 15)
+		return (Word16) (a > 0 ? SW_MAX_ : SW_MIN_);
+	{
+		Word32 v = (Word32) a * (1 << n);
+		if (v != (Word16) v)
+			return (Word16) (a > 0 ? SW_MAX_ : SW_MIN_);
+		return (Word16) v;
+	}
+}
+
+MD Word16 shr(Word16 a, Word16 n)
+{
+	if (n == 0 || a == 0)
+		return a;
+	if (n < 0) {
+		if (n <= -15)
+			return (Word16) (a > 0 ? SW_MAX_ : SW_MIN_);
+		return shl(a, (Word16) -n);
+	}
+	if (n >= 15)
+		return (Word16) (a < 0 ? -1 : 0);
+	return (Word16) (a >> n);
+}
+
+/* L_shl/L_shr: mathhalf_i.h:942-1047 */
+MD Word32 L_shl(Word32 a, Word16 n);
+MD Word32 L_shr(Word32 a, Word16 n)
+{
+	if (n == 0 || a == 0)
+		return a;
+	if (n < 0) {
+		if (n <= -31)
+			return a > 0 ? LW_MAX_ : LW_MIN_;
+		return L_shl(a, (Word16) -n);
+	}
+	if (n >= 31)
+		return a > 0 ? 0 : -1;
+	return a >> n;
+}
+
+MD Word32 L_shl(Word32 a, Word16 n)
+{
+	if (n == 0 || a == 0)
+		return a;
+	if (n < 0) {
+		if (n <= -31)
+			return a > 0 ? 0 : -1;
+		return a >> (-n);
+	}
+	if (n >= 31)
+		return a > 0 ? LW_MAX_ : LW_MIN_;
+	{
+		int64_t v = (int64_t) a * ((int64_t) 1 << n);
+		if (v > LW_MAX_)
+			return LW_MAX_;
+		if (v < LW_MIN_)
+			return LW_MIN_;
+		return (Word32) v;
+	}
+}
+
+/* shift_r / L_shift_r: mathhalf_i.h:1108-1230 */
+MD Word16 shift_r(Word16 a, Word16 n)
+{
+	if (n >= 0)
+		return shl(a, n);
+	if (n < -15)
+		return 0;
+	return add(shl(a, n), (Word16) (shl(a, (Word16) (n + 1)) & 1));
+}
+
+MD Word32 L_shift_r(Word32 a, Word16 n)
+{
+	if (n < -31)
+		return 0;
+	if (n < 0)
+		return L_add(L_shl(a, n), L_shl(a, (Word16) (n + 1)) & 1);
+	return L_shl(a, n);
+}
+
+MD Word16 norm_l(Word32 x)
+{
+	uint32_t u;
+	if (x == 0)
+		return 0;
+	u = (uint32_t) (x ^ (x >> 31));
+	if (u == 0)
+		return 31;
+#if defined(__HIP__)
+	return (Word16) (__clz((int) u) - 1);
+#else
+	return (Word16) (__builtin_clz(u) - 1);
+#endif
+}
+
+MD Word16 norm_s(Word16 a) { return norm_l(L_deposit_h(a)); }
+
+MD Word16 divide_s(Word16 num, Word16 den)
+{
+	if (num < 0 || den < 0 || num > den)
+		return 0;
+	if (num == den)
+		return SW_MAX_;
+	return (Word16) ((0x8000 * (Word32) num) / (Word32) den);
+}
+
+/* ---- 40-bit accumulator (mathhalf_i.h:1763-2168) ---- */
+MD Word40 clamp40(Word40 v) { return v > MAX40_ ? MAX40_ : (v < MIN40_ ? MIN40_ : v); }
+MD Word40 L40_add(Word40 acc, Word32 x) { return clamp40(acc + (Word40) x); }
+MD Word40 L40_sub(Word40 acc, Word32 x) { return clamp40(acc - (Word40) x); }
+MD Word40 L40_mac(Word40 acc, Word16 a, Word16 b) { return clamp40(acc + (Word40) a * (Word40) b * 2); }
+MD Word40 L40_msu(Word40 acc, Word16 a, Word16 b) { return clamp40(acc - (Word40) a * (Word40) b * 2); }
+MD Word40 L40_shr(Word40 acc, Word16 n);
+MD Word40 L40_shl(Word40 acc, Word16 n)
+{
+	if (n < 0)
+		return L40_shr(acc, (Word16) -n);
+	for (; n > 0; n--) {
+		acc *= 2;
+		if (acc > MAX40_)
+			return MAX40_;
+		if (acc < MIN40_)
+			return MIN40_;
+	}
+	return acc;
+}
+MD Word40 L40_shr(Word40 acc, Word16 n)
+{
+	if (n < 0)
+		return L40_shl(acc, (Word16) -n);
+	return acc >> (n > 62 ? 62 : n);	/* floor(acc/2) repeated */
+}
+MD Word40 L40_negate(Word40 acc)
+{
+	acc = -acc;
+	return acc > MAX40_ ? MAX40_ : acc;
+}
+MD Word16 norm32(Word40 acc)
+{
+	Word16 n = 0;
+	if (acc > 0) {
+		while (acc > (Word40) LW_MAX_) {
+			acc >>= 1;
+			n--;
+		}
+		while (acc < ((Word40) 1 << 30)) {
+			acc *= 2;
+			n++;
+		}
+	} else if (acc < 0) {
+		while (acc < (Word40) LW_MIN_) {
+			acc >>= 1;
+			n--;
+		}
+		while (acc >= -((Word40) 1 << 30)) {
+			acc *= 2;
+			n++;
+		}
+	}
+	return n;
+}
+MD Word32 L_sat32(Word40 acc)
+{
+	return (Word32) (acc > LW_MAX_ ? LW_MAX_ : (acc < LW_MIN_ ? LW_MIN_ : acc));
+}
+
+/* mathdp31.c:71-83 */
+MD Word32 L_mpy_ls(Word32 L_var2, Word16 var1)
+{
+	Word16 lo = (Word16) (shr(extract_l(L_var2), 1) & 0x7fff);
+	Word32 out = L_shr(L_mult(var1, lo), 15);
+	return L_mac(out, var1, extract_h(L_var2));
+}
+
+#define Max_(a, b) (((a) > (b)) ? (a) : (b))
+#define Min_(a, b) (((a) > (b)) ? (b) : (a))
+
+#endif

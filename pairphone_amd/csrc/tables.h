@@ -1,0 +1,34 @@
+/*
+ * tables.h -- constant tables of the codec as seen by the device code.
+ *
+ * g_tab holds the standard's codebooks and filter tables, extracted from the
+ * reference objects by oracle/dump_tables.py into
+ * pairphone_amd/data/melpe_tables.bin and uploaded once per device
+ * (hipMemcpyToSymbol).  g_der holds the tables the reference computes on first
+ * use (FFT twiddles melpe/fft_lib.c:285, the LSP cosine grid
+ * melpe/lpc_lib.c:640-657, the Fourier-magnitude weights melpe/vq_lib.c:512,
+ * the postfilter cross-fade window melpe/postfilt.c:73); an init kernel fills
+ * it with init_derived() (dsp.h).
+ */
+#ifndef MELPE_TABLES_H
+#define MELPE_TABLES_H
+
+#include "ops.h"
+#include "tables_gen.h"
+
+MDEV_CONST int16_t g_tab[MELPE_TABLE_WORDS];
+#define TB(name) ((const int16_t *) (g_tab + TOFF_##name))
+
+struct DerivedTables {
+	int16_t wr[257];	/* cos twiddles, + one dead slot read by cfft/rfft */
+	int16_t wi[257];	/* sin twiddles */
+	int16_t lsp_cos[512];	/* cos grid for lsp_to_freq */
+	int16_t w_fs[10];	/* Fourier-magnitude VQ weights, Q14 */
+	int16_t w_fs_inv[10];
+	int16_t pf_window[20];	/* postfilter gain cross-fade window */
+	int16_t pad[2];
+};
+
+MDEV_CONST DerivedTables g_der;
+
+#endif
