@@ -1,0 +1,37 @@
+/*
+ * melpe.h -- drop-in replacement for the reference codec's public header
+ * (reference melpe/melpe.h:1-19).  Same four symbols, same single-stream
+ * semantics, so PairPhone's tx.c / rx.c and melpe_enc.c / melpe_dec.c relink
+ * against libmelpe_amd.so unchanged.
+ *
+ *   melpe_n   melpe/melpe.c:63   denoise 180 samples in place (NPP only)
+ *   melpe_i   melpe/melpe.c:72   initialise the 1200 bps codec
+ *   melpe_a   melpe/melpe.c:91   540 samples -> 81 bits (11 bytes); sp is
+ *                                overwritten with the NPP output, as in the
+ *                                reference (melpe/melpe.c:94-96)
+ *   melpe_s   melpe/melpe.c:102  11 bytes -> 540 samples
+ *
+ * Differences that are deliberate and documented: the encoder and decoder
+ * keep separate parameter state (the reference shares melp_par/quant_par
+ * between them inside one process, melpe/global.c:28-37; standalone
+ * melpe/encoder.c and melpe/decoder.c semantics are reproduced exactly).
+ * The functions compute on the GPU; with no usable GPU they print an error
+ * and abort() -- there is no CPU fallback.
+ */
+#ifndef MELPE_AMD_MELPE_H
+#define MELPE_AMD_MELPE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+void melpe_n(short *sp);
+void melpe_i(void);
+void melpe_a(unsigned char *buf, short *sp);
+void melpe_s(short *sp, unsigned char *buf);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,88 @@
+/*
+ * melpe_batch.h -- batched C ABI of the MI355X MELPe-1200 engine.
+ *
+ * One engine = C independent channels resident on one GPU.  Each channel has
+ * its own encoder and decoder state, equal to a fresh reference process after
+ * melpe_engine_reset (the reference has exactly one instance per process:
+ * all its state lives in globals and function statics, melpe/global.c:20-53).
+ * Every call processes one superframe (540 samples <-> 11 bytes) of every
+ * active channel, exactly as melpe_a / melpe_s (melpe/melpe.c:91-107) would
+ * in that channel's own process.
+ *
+ * Buffers: PCM is channel-major, C x 540 int16 (sample s of channel c at
+ * [c*540 + s]); bitstreams are C x 11 bytes.  The *_host calls take host
+ * pointers and copy; the *_dev calls take device pointers (e.g. from torch)
+ * and enqueue on the given HIP stream without synchronising.  `active` is an
+ * optional C-byte mask (NULL = all channels): inactive channels are left
+ * untouched (state, PCM and bits), which gives ragged streams.
+ *
+ * All functions return 0 on success and a negative code on error;
+ * melpe_last_error() describes the last error of the calling thread.
+ */
+#ifndef MELPE_AMD_BATCH_H
+#define MELPE_AMD_BATCH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct melpe_engine melpe_engine;
+
+#define MELPE_SF_SAMPLES 540
+#define MELPE_SF_BYTES 11
+#define MELPE_FRAME_SAMPLES 180
+
+/* create an engine of `channels` channels on HIP device `device` */
+int melpe_engine_create(melpe_engine **out, int device, int channels);
+int melpe_engine_destroy(melpe_engine *e);
+int melpe_engine_channels(const melpe_engine *e);
+
+/* fresh-process state for the channels selected by `mask` (NULL = all);
+ * which: 1 = encoder (incl. NPP), 2 = decoder, 3 = both */
+int melpe_engine_reset(melpe_engine *e, const uint8_t *mask_host, int which);
+
+/* melpe_a on every active channel: sp (C x 540, in/out: overwritten with the
+ * NPP output), bits (C x 11, out) */
+int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp,
+		      const uint8_t *active);
+int melpe_encode_dev(melpe_engine *e, void *d_bits, void *d_sp,
+		     const void *d_active, void *hip_stream);
+
+/* melpe_s on every active channel: bits (C x 11, in), sp (C x 540, out) */
+int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
+		      const uint8_t *active);
+int melpe_decode_dev(melpe_engine *e, void *d_sp, const void *d_bits,
+		     const void *d_active, void *hip_stream);
+
+/* melpe_n on `frames` consecutive 180-sample frames of every active channel.
+ * sp is C x stride int16 (stride >= frames*180), in place.  A channel's first
+ * frame reads 256 samples (melpe/npp.c:178-179), so stride should be at
+ * least frames*180 + 76 with the look-ahead samples supplied. */
+int melpe_npp_host(melpe_engine *e, int16_t *sp, int frames, int stride,
+		   const uint8_t *active);
+int melpe_npp_dev(melpe_engine *e, void *d_sp, int frames, int stride,
+		  const void *d_active, void *hip_stream);
+
+/* deterministic integer test signal (pairphone_amd/csrc/synth.h) generated
+ * on the device: `samples` samples for each of C channels, continuing each
+ * channel's generator state (seeded by melpe_synth_seed). Output C x samples
+ * channel-major, device pointer. */
+int melpe_synth_seed(melpe_engine *e, uint32_t run_seed, uint32_t first_channel);
+int melpe_synth_dev(melpe_engine *e, void *d_sp, int samples, void *hip_stream);
+
+/* same generator on the host, one channel (for tests and tools) */
+int melpe_synth_host(uint32_t run_seed, uint32_t channel, int16_t *out, int samples);
+
+/* wall-clock of the last *_dev/_host call's kernel on the engine stream, ms,
+ * measured with HIP events (0 if unavailable) */
+double melpe_last_kernel_ms(const melpe_engine *e);
+
+const char *melpe_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

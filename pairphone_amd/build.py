@@ -1,0 +1,88 @@
+"""Build recipe of the engine (called by __graft_entry__.build()).
+
+1. When the reference is present (the dev container, never the GPU box):
+   compile it into oracle/_ref/ (oracle/Makefile) and refresh the table blob
+   (oracle/dump_tables.py).  Both are the checker side, not the product.
+2. Compile the HIP engine for gfx950 into pairphone_amd/libmelpe_amd.so
+   (hipcc; the tables are embedded with .incbin).
+3. Compile the host-emulation build of the same device sources
+   (build/libmelpe_hostemu.so, g++) used by the CPU-side tests to check the
+   kernel logic against the reference without a GPU.  The product library
+   never loads it.
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "pairphone_amd", "csrc")
+LIB = os.path.join(ROOT, "pairphone_amd", "libmelpe_amd.so")
+EMU = os.path.join(ROOT, "build", "libmelpe_hostemu.so")
+REF = "/root/reference/melpe"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _run(cmd, **kw):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True, **kw)
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _sources():
+    out = []
+    for d in (CSRC, os.path.join(ROOT, "include")):
+        for f in os.listdir(d):
+            if f.endswith((".h", ".hip", ".cpp")):
+                out.append(os.path.join(d, f))
+    out.append(os.path.join(ROOT, "pairphone_amd", "data", "melpe_tables.bin"))
+    return out
+
+
+def build_oracle():
+    if not os.path.isdir(REF):
+        print("reference not present: using prebuilt oracle/_ref and committed tables")
+        return
+    _run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "-j8"])
+    _run([sys.executable, os.path.join(ROOT, "oracle", "dump_tables.py")])
+
+
+def build_engine(force=False):
+    deps = _sources()
+    if not force and not _newer(LIB, deps):
+        return LIB
+    blob = os.path.join(ROOT, "pairphone_amd", "data", "melpe_tables.bin")
+    tmp = LIB + ".tmp"
+    _run([HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17", "-shared", "-fPIC",
+          "-Wno-unused-result", '-DMELPE_TABLES_BIN="%s"' % blob,
+          os.path.join(CSRC, "engine.hip"), "-o", tmp])
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_hostemu(force=False):
+    deps = _sources()
+    if not force and not _newer(EMU, deps):
+        return EMU
+    os.makedirs(os.path.dirname(EMU), exist_ok=True)
+    tmp = EMU + ".tmp"
+    _run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I" + CSRC,
+          os.path.join(CSRC, "hostemu.cpp"), "-o", tmp])
+    os.replace(tmp, EMU)
+    return EMU
+
+
+def build_all(force=False):
+    build_oracle()
+    build_engine(force)
+    if os.path.exists(os.path.join(CSRC, "hostemu.cpp")):
+        build_hostemu(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

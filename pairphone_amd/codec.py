@@ -1,0 +1,183 @@
+"""Host mirror of the engine's C ABI (include/melpe_batch.h, include/melpe.h).
+
+`Melpe` mirrors the reference's single-stream interface (melpe/melpe.h:10-14:
+melpe_n / melpe_i / melpe_a / melpe_s) with the same names, argument meaning
+and in-place side effect (melpe_a overwrites its input with the NPP output,
+melpe/melpe.c:94-96).  `MelpeEngine` is the batched engine: C channels per
+GPU, one superframe of every active channel per call.
+
+There is no CPU fallback: if libmelpe_amd.so cannot be loaded or no GPU is
+usable, these classes raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+SF_SAMPLES = 540
+SF_BYTES = 11
+FRAME_SAMPLES = 180
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmelpe_amd.so")
+_lib = None
+
+
+def load_library(path=None):
+    """Loads libmelpe_amd.so (the HIP build); raises if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError("libmelpe_amd.so not built (%s): run __graft_entry__.build()" % p)
+    lib = ctypes.CDLL(p)
+    vp, i32, u32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32
+    sig = {
+        "melpe_engine_create": (i32, [ctypes.POINTER(vp), i32, i32]),
+        "melpe_engine_destroy": (i32, [vp]),
+        "melpe_engine_channels": (i32, [vp]),
+        "melpe_engine_reset": (i32, [vp, vp, i32]),
+        "melpe_encode_host": (i32, [vp, vp, vp, vp]),
+        "melpe_encode_dev": (i32, [vp, vp, vp, vp, vp]),
+        "melpe_decode_host": (i32, [vp, vp, vp, vp]),
+        "melpe_decode_dev": (i32, [vp, vp, vp, vp, vp]),
+        "melpe_npp_host": (i32, [vp, vp, i32, i32, vp]),
+        "melpe_npp_dev": (i32, [vp, vp, i32, i32, vp, vp]),
+        "melpe_synth_seed": (i32, [vp, u32, u32]),
+        "melpe_synth_dev": (i32, [vp, vp, i32, vp]),
+        "melpe_synth_host": (i32, [u32, u32, vp, i32]),
+        "melpe_last_kernel_ms": (ctypes.c_double, [vp]),
+        "melpe_last_error": (ctypes.c_char_p, []),
+        "melpe_i": (None, []),
+        "melpe_a": (None, [vp, vp]),
+        "melpe_s": (None, [vp, vp]),
+        "melpe_n": (None, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError("libmelpe_amd: %s" % load_library().melpe_last_error().decode())
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def synth_signal(run_seed, channel, samples):
+    """Deterministic integer test signal of one channel (csrc/synth.h)."""
+    out = np.zeros(samples, dtype=np.int16)
+    _check(load_library().melpe_synth_host(run_seed, channel, _ptr(out), samples))
+    return out
+
+
+class MelpeEngine:
+    """C independent MELPe-1200 channels on one GPU (include/melpe_batch.h)."""
+
+    def __init__(self, channels, device=0):
+        self.lib = load_library()
+        self.h = ctypes.c_void_p()
+        _check(self.lib.melpe_engine_create(ctypes.byref(self.h), device, channels))
+        self.channels = channels
+
+    def close(self):
+        if self.h:
+            self.lib.melpe_engine_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, mask=None, which=3):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        _check(self.lib.melpe_engine_reset(self.h, _ptr(m), which))
+
+    def _mask(self, active):
+        if active is None:
+            return None
+        m = np.ascontiguousarray(active, dtype=np.uint8)
+        assert m.shape == (self.channels,)
+        return m
+
+    def encode(self, sp, active=None):
+        """melpe_a on every channel. sp: int16 [C, 540], overwritten with the
+        NPP output (as the reference).  Returns uint8 [C, 11]."""
+        assert sp.dtype == np.int16 and sp.shape == (self.channels, SF_SAMPLES)
+        assert sp.flags.c_contiguous
+        bits = np.zeros((self.channels, SF_BYTES), dtype=np.uint8)
+        m = self._mask(active)
+        _check(self.lib.melpe_encode_host(self.h, _ptr(bits), _ptr(sp), _ptr(m)))
+        return bits
+
+    def decode(self, bits, active=None):
+        """melpe_s on every channel. bits: uint8 [C, 11] -> int16 [C, 540]."""
+        bits = np.ascontiguousarray(bits, dtype=np.uint8)
+        assert bits.shape == (self.channels, SF_BYTES)
+        sp = np.zeros((self.channels, SF_SAMPLES), dtype=np.int16)
+        m = self._mask(active)
+        _check(self.lib.melpe_decode_host(self.h, _ptr(sp), _ptr(bits), _ptr(m)))
+        return sp
+
+    def npp(self, sp, frames, active=None):
+        """melpe_n on `frames` frames of every channel, in place.
+        sp: int16 [C, stride] with stride >= frames*180 (+76 look-ahead)."""
+        assert sp.dtype == np.int16 and sp.ndim == 2 and sp.flags.c_contiguous
+        m = self._mask(active)
+        _check(self.lib.melpe_npp_host(self.h, _ptr(sp), frames, sp.shape[1], _ptr(m)))
+        return sp
+
+    def encode_dev(self, d_bits, d_sp, d_active=None, stream=None):
+        _check(self.lib.melpe_encode_dev(self.h, d_bits, d_sp, d_active, stream))
+
+    def decode_dev(self, d_sp, d_bits, d_active=None, stream=None):
+        _check(self.lib.melpe_decode_dev(self.h, d_sp, d_bits, d_active, stream))
+
+    def synth_seed(self, run_seed, first_channel=0):
+        _check(self.lib.melpe_synth_seed(self.h, run_seed, first_channel))
+
+    def synth_dev(self, d_sp, samples, stream=None):
+        _check(self.lib.melpe_synth_dev(self.h, d_sp, samples, stream))
+
+    def last_kernel_ms(self):
+        return self.lib.melpe_last_kernel_ms(self.h)
+
+
+class Melpe:
+    """Single-stream drop-in mirror of melpe/melpe.h (process-global state,
+    exactly one instance, as the reference)."""
+
+    def __init__(self):
+        self.lib = load_library()
+
+    def melpe_i(self):
+        self.lib.melpe_i()
+
+    def melpe_a(self, sp):
+        """sp: int16[540], overwritten with the NPP output; returns 11 bytes."""
+        assert sp.dtype == np.int16 and sp.shape == (SF_SAMPLES,) and sp.flags.c_contiguous
+        buf = np.zeros(SF_BYTES, dtype=np.uint8)
+        self.lib.melpe_a(_ptr(buf), _ptr(sp))
+        return buf
+
+    def melpe_s(self, buf):
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        sp = np.zeros(SF_SAMPLES, dtype=np.int16)
+        self.lib.melpe_s(_ptr(sp), _ptr(buf))
+        return sp
+
+    def melpe_n(self, sp):
+        """denoise 180 samples in place; the first call reads 256 samples
+        (melpe/npp.c:178-179), so pass at least 256 valid samples."""
+        assert sp.dtype == np.int16 and sp.size >= 256 and sp.flags.c_contiguous
+        self.lib.melpe_n(_ptr(sp))
+        return sp

@@ -1,0 +1,73 @@
+/*
+ * hostemu.cpp -- host build of the engine's DEVICE sources, for CPU-side
+ * tests only (tests/test_hostemu.py).  It runs the very same per-channel
+ * code that the HIP kernels run (ops.h .. codec headers compiled with g++
+ * instead of hipcc), one channel after another, so the kernel logic can be
+ * checked against the reference oracle in a container without a GPU.
+ *
+ * NOT part of the product: libmelpe_amd.so never loads it, and nothing in
+ * pairphone_amd/ imports it.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+#include "state.h"
+#include "derived.h"
+
+using namespace mlp;
+
+struct emu_engine {
+	int channels;
+	std::vector<EncState> enc;
+	std::vector<DecState> dec;
+};
+
+static NppScratch g_npp_scratch;
+
+extern "C" {
+
+int emu_load_tables(const char *path)
+{
+	FILE *f = fopen(path, "rb");
+	if (!f)
+		return -1;
+	size_t n = fread(g_tab, sizeof(int16_t), MELPE_TABLE_WORDS, f);
+	fclose(f);
+	if (n != MELPE_TABLE_WORDS)
+		return -2;
+	derive_fft_twiddles(&g_der);
+	derive_lsp_cos(&g_der);
+	return 0;
+}
+
+emu_engine *emu_create(int channels)
+{
+	emu_engine *e = new emu_engine();
+	e->channels = channels;
+	e->enc.resize(channels);
+	e->dec.resize(channels);
+	for (int c = 0; c < channels; c++) {
+		enc_reset(&e->enc[c]);
+		dec_reset(&e->dec[c]);
+	}
+	return e;
+}
+
+void emu_destroy(emu_engine *e)
+{
+	delete e;
+}
+
+int emu_npp(emu_engine *e, int16_t *sp, int frames, int stride, int rate1200)
+{
+	for (int c = 0; c < e->channels; c++)
+		for (int f = 0; f < frames; f++) {
+			int16_t *x = sp + (size_t) c * stride + f * NPP_HOP;
+			npp_frame(&e->enc[c].npp, &g_npp_scratch, x, x, rate1200 != 0);
+		}
+	return 0;
+}
+
+}  // extern "C"
