@@ -1,0 +1,1084 @@
+/*
+ * analysis.h -- the MELPe analysis front end on one lane (= one channel):
+ * DC removal, bandpass voicing, integer/fractional pitch, pitch tracking and
+ * frame classification, LPC/LSF, gain, Fourier magnitudes, and the
+ * superframe smoothing (sc_ana).
+ *
+ * Restates melpe/melp_ana.c, melpe/melp_sub.c (analysis part),
+ * melpe/pit_lib.c, melpe/pitch.c, melpe/classify.c and melpe/fs_lib.c with
+ * the reference's statics held in EncState.  Function names follow the
+ * reference's; line numbers cite the reference file each one restates.
+ */
+#ifndef MELPE_ANALYSIS_H
+#define MELPE_ANALYSIS_H
+
+#include "state.h"
+
+namespace mlp {
+
+/* ------------------------------------------------------------------ */
+/* melpe/melp_sub.c                                                   */
+/* ------------------------------------------------------------------ */
+
+/* dc_rmv :211 -- 3 double-precision biquads (NEW_DC_FILTER) */
+MD void dc_rmv(const int16_t *in, int16_t *out, int16_t *din, int16_t *dhi,
+	       int16_t *dlo, int n)
+{
+	v_copy(out, in, n);
+	for (int s = 0; s < DC_ORD / 2; s++)
+		iir_2nd_d(out, TB(dc_den) + s * 3, TB(dc_num) + s * 3, out, din + s * 2,
+			  dhi + s * 2, dlo + s * 2, n);
+}
+
+/* remove_dc :261 */
+MD void remove_dc(const int16_t *in, int16_t *out, int16_t len)
+{
+	Word16 up = sub(15, norm_s(len));
+	Word16 pdown = shl(1, sub(up, 1));
+	Word32 sum = 0;
+	for (int i = 0; i < len; i++)
+		sum = L_add(sum, L_deposit_l(in[i]));
+	sum = L_shr(sum, up);
+	Word16 off = mult(extract_l(sum), divide_s(pdown, len));
+	off = shl(off, 1);
+	for (int i = 0; i < len; i++)
+		out[i] = sub(in[i], off);
+}
+
+/* gain_ana :311 -- pitch-adaptive RMS in dB (Q8) */
+MD Word16 gain_ana(const int16_t *sig, Word16 pitch, Word16 minlen, Word16 maxlen)
+{
+	int16_t tb[PITCHMAX * 2 + 8];
+	Word16 pq6 = shr(pitch, 1);
+	Word16 tmin = shl(minlen, 6);
+	Word16 fl = pq6;
+	while (fl < tmin)
+		fl = add(fl, pq6);
+	Word16 len = shr(add(fl, 32), 6);
+	if (len > maxlen)
+		len = shr(len, 1);
+	Word16 beg = negate(shr(len, 1));
+	Word16 sc = 3;
+	v_equ_shr(tb, &sig[beg], sc, len);
+	Word32 e = L_v_magsq(tb, len, 0, 1);
+	if (e) {
+		sc = sub(sc, shr(norm_l(e), 1));
+		if (sc < 0)
+			sc = 0;
+	} else {
+		sc = 0;
+	}
+	if (sc)
+		v_equ_shr(tb, &sig[beg], sc, len);
+	else
+		v_copy(tb, &sig[beg], len);
+	Word16 g, t1, t2;
+	e = L_v_magsq(tb, len, 0, 0);
+	if (sc) {
+		t1 = L_log10_fxp(e, 0);
+		t2 = L_log10_fxp(L_deposit_l(len), 0);
+		t1 = sub(t1, t2);
+		t2 = extract_l(L_shr(L_mult(sc, 1233), 1));
+		t1 = add(t1, t2);
+		g = shl(mult(20480, t1), 1);
+	} else {
+		t1 = (e == 0) ? (Word16) -4096 : L_log10_fxp(e, 0);
+		t2 = L_log10_fxp(L_deposit_l(len), 0);
+		t1 = sub(t1, t2);
+		g = shl(mult(20480, t1), 1);
+	}
+	return g < 0 ? 0 : g;
+}
+
+/* q_bpvc :555 -- returns uv_flag */
+MD int16_t q_bpvc(int16_t *bpvc, int16_t *idx, int nb)
+{
+	Word16 k = 0;
+	int16_t uv;
+	if (bpvc[0] > BPTHRESH_Q14) {
+		uv = 0;
+		bpvc[0] = 16384;
+		for (int i = 1; i < nb; i++) {
+			k = shl(k, 1);
+			if (bpvc[i] > BPTHRESH_Q14) {
+				bpvc[i] = 16384;
+				k |= 1;
+			} else {
+				bpvc[i] = 0;
+			}
+		}
+		if (k == 1) {	/* INVALID_BPVC */
+			bpvc[nb - 1] = 0;
+			k = 0;
+		}
+	} else {
+		uv = 1;
+		k = 0;
+		v_zero(bpvc, nb);
+	}
+	*idx = k;
+	return uv;
+}
+
+/* q_bpvc_dec :595 */
+MD void q_bpvc_dec(int16_t *bpvc, Word16 idx, int16_t uv, int nb)
+{
+	if (uv) {
+		idx = 0;
+		bpvc[0] = 0;
+	} else {
+		bpvc[0] = 16384;
+	}
+	if (idx == 1)
+		idx = 0;
+	for (int i = nb - 1; i > 0; i--) {
+		bpvc[i] = (idx & 1) ? 16384 : 0;
+		idx = shr(idx, 1);
+	}
+}
+
+/* ------------------------------------------------------------------ */
+/* melpe/pit_lib.c                                                    */
+/* ------------------------------------------------------------------ */
+
+/* f_pitch_scale :178 -- scale so the energy fits, returns the shift */
+MD Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
+{
+	Word16 sc = 0;
+	Word32 sum = 0, margin = LW_MAX_;
+	for (int i = 0; i < len; i++) {
+		Word32 t = L_mult(in[i], in[i]);
+		if (t <= margin) {
+			sum = L_add(sum, t);
+			margin = L_sub(margin, t);
+		} else {
+			margin = LW_MIN_;
+			break;
+		}
+	}
+	Word32 corr = sum;
+	if (margin == LW_MIN_) {
+		int16_t tb[PITCH_FR + 8];
+		sc = 5;
+		v_equ_shr(tb, in, sc, len);
+		corr = L_v_magsq(tb, len, 0, 1);
+	}
+	sc = sub(sc, shr(norm_l(corr), 1));
+	v_equ_shr(out, in, sc, len);
+	return sc;
+}
+
+/* find_pitch :240 -- normalised autocorrelation lag search, lags upper..lower */
+MD Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upper, Word16 len)
+{
+	Word16 ip = lower;
+	Word32 max_num = 0, max_den = 1;
+	bool even = true;
+	Word16 cb = negate(shr(add(len, upper), 1));
+	Word32 c00 = L_v_magsq(&sig[cb], len, 0, 1);
+	Word32 cTT = L_v_magsq(&sig[cb + upper], len, 0, 1);
+	for (Word16 i = upper; i >= lower; i--) {
+		Word32 corr = L_v_inner(&sig[cb], &sig[cb + i], len, 0, 0, 1);
+		Word16 s1a = norm_s(extract_h(c00));
+		Word16 s1b = norm_s(extract_h(cTT));
+		Word16 s = add(s1a, s1b);
+		Word16 s2 = shr(s, 1);
+		if (shl(s2, 1) != s)
+			s1a = sub(s1a, 1);
+		Word32 num;
+		if (corr > 0) {
+			Word16 sc = extract_h(L_shl(corr, s2));
+			num = extract_h(L_mult(sc, sc));
+		} else {
+			num = 0;
+		}
+		Word32 den = extract_h(L_mult(extract_h(L_shl(c00, s1a)),
+					      extract_h(L_shl(cTT, s1b))));
+		if (den < 1)
+			den = 1;
+		if (L_mult(extract_l(num), extract_l(max_den)) >
+		    L_mult(extract_l(max_num), extract_l(den))) {
+			max_den = den;
+			max_num = num;
+			ip = i;
+		}
+		if (even) {
+			even = false;
+			c00 = L_msu(c00, sig[cb], sig[cb]);
+			c00 = L_mac(c00, sig[cb + len], sig[cb + len]);
+			cb = add(cb, 1);
+		} else {
+			even = true;
+			cTT = L_msu(cTT, sig[cb + i - 1 + len], sig[cb + i - 1 + len]);
+			cTT = L_mac(cTT, sig[cb + i - 1], sig[cb + i - 1]);
+		}
+	}
+	*pcorr = shr(sqrt_fxp(divide_s(extract_l(max_num), extract_l(max_den)), 15), 1);
+	return ip;
+}
+
+/* frac_pch :340 -- fractional pitch refinement and its correlation */
+MD Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 range,
+		   Word16 pmin, Word16 pmax, Word16 pmin_q7, Word16 pmax_q7, Word16 lmin)
+{
+	Word16 len, cb, ip, corr;
+	if (range > 0) {
+		ip = shift_r(fpitch, -7);
+		Word16 lo = sub(ip, range), hi = add(ip, range);
+		if (hi > pmax)
+			hi = pmax;
+		if (lo < pmin)
+			lo = pmin;
+		Word16 q = add(shr(ip, 1), shr(ip, 2));
+		if (lo < q)
+			lo = q;
+		len = ip;
+		if (len < lmin)
+			len = lmin;
+		fpitch = shl(find_pitch(sig, &corr, lo, hi, len), 7);
+	}
+	ip = shift_r(fpitch, -7);
+	if (ip >= pmax)
+		ip = sub(pmax, 1);
+	len = ip;
+	if (len < lmin)
+		len = lmin;
+	cb = negate(shr(add(len, ip), 1));
+	Word32 msq = L_v_magsq(&sig[cb], len, 0, 1);
+	Word16 s1a = norm_s(extract_h(msq));
+	Word16 s1b = norm_s(extract_h(L_v_magsq(&sig[cb + ip - 1], (Word16) (len + 2), 0, 1)));
+	Word16 s = add(s1a, s1b);
+	Word16 s2 = shr(s, 1);
+	if (shl(s2, 1) != s)
+		s1a = sub(s1a, 1);
+	Word16 c00 = extract_h(L_shl(msq, s1a));
+	Word16 c0T = extract_h(L_shl(L_v_inner(&sig[cb], &sig[cb + ip], len, 0, 0, 1), s2));
+	Word16 c0T1 = extract_h(L_shl(L_v_inner(&sig[cb], &sig[cb + ip + 1], len, 0, 0, 1), s2));
+	Word16 c0Tm1 = extract_h(L_shl(L_v_inner(&sig[cb], &sig[cb + ip - 1], len, 0, 0, 1), s2));
+	if (c0Tm1 > c0T1) {
+		c0T1 = c0T;
+		c0T = c0Tm1;
+		ip = sub(ip, 1);
+	}
+	Word16 cTT1 = extract_h(L_shl(L_v_inner(&sig[cb + ip], &sig[cb + ip + 1], len, 0, 0, 1), s1b));
+	Word16 cTT = extract_h(L_shl(L_v_inner(&sig[cb + ip], &sig[cb + ip], len, 0, 0, 1), s1b));
+	Word16 cT1T1 = extract_h(L_shl(L_v_inner(&sig[cb + ip + 1], &sig[cb + ip + 1], len, 0, 0, 1), s1b));
+	Word32 den = L_add(L_mult(c0T1, sub(shr(cTT, 1), shr(cTT1, 1))),
+			   L_mult(c0T, sub(shr(cT1T1, 1), shr(cTT1, 1))));
+	Word32 num = L_sub(L_shr(L_mult(c0T1, cTT), 1), L_shr(L_mult(c0T, cTT1), 1));
+	Word16 frac;
+	Word32 aden = L_abs(den);
+	if (aden > 0) {
+		if (L_abs(L_shr(num, 2)) > aden) {
+			if ((num > 0 && den < 0) || (num < 0 && den > 0))
+				frac = -8192;
+			else
+				frac = 16384;
+		} else {
+			frac = L_divider2(num, den, 2, 0);
+		}
+	} else {
+		frac = 4096;
+	}
+	if (frac > 16384)
+		frac = 16384;
+	if (frac < -8192)
+		frac = -8192;
+	fpitch = add(shl(ip, 7), shr(frac, 6));
+	if (fpitch > pmax_q7) {
+		fpitch = pmax_q7;
+		frac = shl(sub(fpitch, shl(ip, 7)), 6);
+	}
+	if (fpitch < pmin_q7) {
+		fpitch = pmin_q7;
+		frac = shl(sub(fpitch, shl(ip, 7)), 6);
+	}
+	Word16 f1 = sub(8192, frac);
+	Word32 d1 = L_shr(L_mpy_ls(L_mult(cTT, f1), f1), 1);
+	Word32 d2 = L_mpy_ls(L_mult(cTT1, f1), frac);
+	Word32 d3 = L_shr(L_mpy_ls(L_mult(cT1T1, frac), frac), 1);
+	den = L_mpy_ls(L_add(L_add(d1, d2), d3), c00);
+	Word16 root = L_sqrt_fxp(den, 0);
+	Word32 t = L_mac(L_mult(c0T, f1), c0T1, frac);
+	corr = (t <= 0) ? (Word16) 0 : extract_h(t);
+	if (corr < root)
+		*pcorr = shr(divide_s(corr, root), 1);
+	else if (root <= 0)
+		*pcorr = 0;
+	else
+		*pcorr = 16384;
+	return fpitch;
+}
+
+/* double_ver :151 */
+MD void double_ver(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pmin, Word16 pmax,
+		   Word16 pmin_q7, Word16 pmax_q7, Word16 lmin)
+{
+	Word16 m = 1;
+	while (extract_l(L_shr(L_mult(pitch, m), 1)) < 3840)
+		m = add(m, 1);
+	if (m > 1) {
+		Word16 tp = extract_l(L_shr(L_mult(pitch, m), 1));
+		Word16 c;
+		frac_pch(sig, &c, tp, 0, pmin, pmax, pmin_q7, pmax_q7, lmin);
+		if (c < *pcorr)
+			*pcorr = c;
+	}
+}
+
+/* double_chk :84 -- pitch-halving check over multiples 8..2 */
+MD Word16 double_chk(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pdouble,
+		     Word16 pmin, Word16 pmax, Word16 pmin_q7, Word16 pmax_q7, Word16 lmin)
+{
+	pitch = frac_pch(sig, pcorr, pitch, 0, pmin, pmax, pmin_q7, pmax_q7, lmin);
+	Word16 thresh = extract_l(L_shr(L_mult(*pcorr, pdouble), 8));
+	for (Word16 m = 8; m >= 2; m--) {
+		Word16 t1 = 0;
+		Word16 t2 = shl(m, 11);
+		Word16 tp = pitch;
+		while (tp > t2) {
+			tp = shr(tp, 1);
+			t1 = add(t1, 1);
+		}
+		t2 = divide_s(tp, t2);
+		t1 = sub(4, t1);
+		tp = shr(t2, t1);
+		if (tp >= pmin_q7) {
+			Word16 c;
+			tp = frac_pch(sig, &c, tp, 0, pmin, pmax, pmin_q7, pmax_q7, lmin);
+			double_ver(sig, &c, tp, pmin, pmax, pmin_q7, pmax_q7, lmin);
+			if (c > thresh) {
+				pitch = frac_pch(sig, pcorr, tp, 0, pmin, pmax, pmin_q7, pmax_q7, lmin);
+				break;
+			}
+		}
+	}
+	double_ver(sig, pcorr, pitch, pmin, pmax, pmin_q7, pmax_q7, lmin);
+	return pitch;
+}
+
+/* p_avg_update :515 */
+MD Word16 p_avg_update(EncState *E, Word16 pitch, Word16 pcorr, Word16 pthresh)
+{
+	if (!E->pavg_started) {
+		v_set(E->good_pitch, DEFAULT_PITCH_Q7, NF);
+		E->pavg_started = 1;
+	}
+	if (pcorr > pthresh) {
+		v_copy(E->good_pitch, &E->good_pitch[1], NF - 1);
+		E->good_pitch[NF - 1] = pitch;
+	} else {
+		for (int i = 0; i < NF; i++)
+			E->good_pitch[i] = add(mult(31129, E->good_pitch[i]), 320);
+	}
+	return median3(E->good_pitch);
+}
+
+/* pitch_ana :571 -- final pitch from the lowpassed residual, with the
+ * speech fallback; pa_sigbuf is persistent (its tail 323..326 can be read
+ * stale by double_chk) */
+MD Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Word16 pest,
+		    Word16 pavg, Word16 *pcorr2)
+{
+	int16_t *sb = E->pa_sigbuf;
+	int16_t tdin[LPF_ORD], tdout[LPF_ORD];
+	Word16 pcorr, pitch, t, t2;
+	if (!E->pana_started) {
+		v_zero(E->lpres_delin, LPF_ORD);
+		v_zero(E->lpres_delout, LPF_ORD);
+		E->pana_started = 1;
+	}
+	v_copy(&sb[2], &resid[-PITCHMAX], PITCH_FR);
+	for (int s = 0; s < LPF_ORD / 2; s++) {
+		iir_2nd_s(&sb[2], TB(lpf_den) + s * 3, TB(lpf_num) + s * 3, &sb[2],
+			  &E->lpres_delin[s * 2], &E->lpres_delout[s * 2], FRAME);
+		for (int i = s * 2; i < s * 2 + 2; i++) {
+			tdin[i] = E->lpres_delin[i];
+			tdout[i] = E->lpres_delout[i];
+		}
+		iir_2nd_s(&sb[2 + FRAME], TB(lpf_den) + s * 3, TB(lpf_num) + s * 3, &sb[2 + FRAME],
+			  &E->lpres_delin[s * 2], &E->lpres_delout[s * 2], PITCH_FR - FRAME);
+		for (int i = s * 2; i < s * 2 + 2; i++) {
+			E->lpres_delin[i] = tdin[i];
+			E->lpres_delout[i] = tdout[i];
+		}
+	}
+	f_pitch_scale(&sb[2], &sb[2], PITCH_FR);
+	t = frac_pch(&sb[2 + PITCH_FR / 2], &pcorr, pest, 5, PITCHMIN, PITCHMAX,
+		     PITCHMIN_Q7, PITCHMAX_Q7, 160);
+	if (pcorr < 9831) {
+		v_copy(&sb[LPF_ORD], &speech[-PITCHMAX], PITCH_FR);
+		f_pitch_scale(&sb[2], &sb[2], PITCH_FR);
+		t = frac_pch(&sb[LPF_ORD + PITCH_FR / 2], &pcorr, pest, 0, PITCHMIN, PITCHMAX,
+			     PITCHMIN_Q7, PITCHMAX_Q7, 160);
+		if (pcorr < 9012) {
+			pitch = pavg;
+		} else {
+			t2 = (t > 12800) ? 89 : 115;
+			pitch = double_chk(&sb[LPF_ORD + PITCH_FR / 2], &pcorr, t, t2, PITCHMIN,
+					   PITCHMAX, PITCHMIN_Q7, PITCHMAX_Q7, 160);
+		}
+	} else {
+		t2 = (t > 12800) ? 64 : 96;
+		pitch = double_chk(&sb[LPF_ORD + PITCH_FR / 2], &pcorr, t, t2, PITCHMIN, PITCHMAX,
+				   PITCHMIN_Q7, PITCHMAX_Q7, 160);
+	}
+	if (pcorr < 9012)
+		pitch = pavg;
+	*pcorr2 = pcorr;
+	return pitch;
+}
+
+/* ------------------------------------------------------------------ */
+/* bpvc_ana, melpe/melp_sub.c:77 -- 5-band bandpass voicing           */
+/* ------------------------------------------------------------------ */
+MD void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
+		 Word16 *pitch)
+{
+	int16_t sb[BPF_ORD + PITCH_FR];
+	Word16 pcorr, t, sc;
+	const int16_t *bden = TB(bpf_den), *bnum = TB(bpf_num);
+	if (!E->bp_started) {
+		for (int i = 0; i < NUM_BANDS; i++) {
+			v_zero(E->bpfsp[i], PITCH_FR - FRAME);
+			v_zero(E->bpfdelin[i], BPF_ORD);
+			v_zero(E->bpfdelout[i], BPF_ORD);
+			v_zero(E->envdel[i], ENV_ORD);
+		}
+		v_zero(E->envdel2, NUM_BANDS);
+		E->bp_started = 1;
+	}
+	const int NEW = BPF_ORD + PITCH_FR - FRAME;	/* 147 */
+	v_copy(&sb[BPF_ORD], E->bpfsp[0], PITCH_FR - FRAME);
+	v_copy(&sb[NEW], &speech[PITCH_FR - FRAME - PITCHMAX], FRAME);
+	for (int s = 0; s < BPF_ORD / 2; s++)
+		iir_2nd_s(&sb[NEW], bden + s * 3, bnum + s * 3, &sb[NEW], &E->bpfdelin[0][s * 2],
+			  &E->bpfdelout[0][s * 2], FRAME);
+	v_copy(E->bpfsp[0], &sb[BPF_ORD + FRAME], PITCH_FR - FRAME);
+	f_pitch_scale(&sb[BPF_ORD], &sb[BPF_ORD], PITCH_FR);
+	*pitch = frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[0], fpitch[0], 5, PITCHMIN, PITCHMAX,
+			  PITCHMIN_Q7, PITCHMAX_Q7, 160);
+	for (int i = 1; i < 2; i++) {	/* NUM_PITCHES */
+		t = frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, fpitch[i], 5, PITCHMIN, PITCHMAX,
+			     PITCHMIN_Q7, PITCHMAX_Q7, 160);
+		if (pcorr > bpvc[0]) {
+			*pitch = t;
+			bpvc[0] = pcorr;
+		}
+	}
+	for (int i = 1; i < NUM_BANDS; i++) {
+		v_copy(&sb[BPF_ORD], E->bpfsp[i], PITCH_FR - FRAME);
+		v_copy(&sb[NEW], &speech[PITCH_FR - FRAME - PITCHMAX], FRAME);
+		for (int s = 0; s < BPF_ORD / 2; s++) {
+			int fi = i * (BPF_ORD / 2) * 3 + s * 3;
+			iir_2nd_s(&sb[NEW], bden + fi, bnum + fi, &sb[NEW], &E->bpfdelin[i][s * 2],
+				  &E->bpfdelout[i][s * 2], FRAME);
+		}
+		v_copy(E->bpfsp[i], &sb[BPF_ORD + FRAME], PITCH_FR - FRAME);
+		sc = f_pitch_scale(&sb[BPF_ORD], &sb[BPF_ORD], PITCH_FR);
+		frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[i], *pitch, 0, PITCHMIN, PITCHMAX,
+			 PITCHMIN_Q7, PITCHMAX_Q7, 160);
+		/* envelope: the history samples are re-scaled to this frame's scale */
+		t = shr(E->envdel2[i], sc);
+		E->envdel2[i] = shr(sb[BPF_ORD + FRAME - 1], (Word16) -sc);
+		v_equ_shr(&sb[BPF_ORD - ENV_ORD], E->envdel[i], sc, ENV_ORD);
+		envelope(&sb[BPF_ORD], t, &sb[BPF_ORD], PITCH_FR);
+		v_equ_shr(E->envdel[i], &sb[BPF_ORD + FRAME - ENV_ORD], (Word16) -sc, ENV_ORD);
+		f_pitch_scale(&sb[BPF_ORD], &sb[BPF_ORD], PITCH_FR);
+		frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, *pitch, 0, PITCHMIN, PITCHMAX,
+			 PITCHMIN_Q7, PITCHMAX_Q7, 160);
+		pcorr = sub(pcorr, 1638);
+		if (pcorr > bpvc[i])
+			bpvc[i] = pcorr;
+	}
+}
+
+/* ------------------------------------------------------------------ */
+/* melpe/pitch.c -- 8-candidate pitch tracker                          */
+/* ------------------------------------------------------------------ */
+
+/* ratio :591 / L_ratio :612 */
+MD Word16 ratio(Word16 x, Word16 y)
+{
+	Word16 d = abs_s(sub(x, y));
+	Word16 larger = (x > y) ? x : y;
+	return divide_s(d, larger);
+}
+
+MD Word16 L_ratio(Word16 x, Word32 y)
+{
+	Word32 lx = L_deposit_l(x);
+	Word32 d = L_sub(y, lx);
+	if (d < 0)
+		d = L_negate(d);
+	Word32 larger = (lx > y) ? lx : y;
+	return L_divider2(d, larger, 0, 0);
+}
+
+/* updateEn :633 */
+MD Word16 updateEn(Word16 prev, Word16 ifact, Word16 curr)
+{
+	Word16 t = sub(shr(curr, 1), shr(prev, 1));
+	if (t < negate(1024)) {
+		t = shr(log10_fxp(ifact, 15), 1);
+		return add(t, prev);
+	}
+	if (t > 3072) {
+		t = shr(log10_fxp(sub(SW_MAX_, ifact), 15), 1);
+		return add(t, curr);
+	}
+	t = shl(t, 2);
+	t = pow10_fxp(t, 5);
+	t = interp_scalar(t, 32, ifact);
+	t = shr(log10_fxp(t, 5), 1);
+	return add(prev, t);
+}
+
+/* lpfilt :100 */
+MD void lpfilt(const int16_t *in, int16_t *lp, int len)
+{
+	const int16_t *lpar = TB(lpar);
+	v_copy(lp, &lp[len], PIT_COR_LEN - len);
+	for (int i = 0; i < len; i++) {
+		Word32 s = L_shr(L_deposit_h(in[i]), 3);
+		for (int j = 0; j < 4; j++)
+			s = L_mac(s, lp[PIT_COR_LEN - len + i - j - 1], lpar[j]);
+		lp[PIT_COR_LEN - len + i] = r_ound(s);
+	}
+}
+
+/* ivfilt :138 -- 2nd-order inverse filter from 40-bit autocorrelations */
+MD void ivfilt(int16_t *iv, const int16_t *lp, int len)
+{
+	int16_t rc[3];
+	Word16 pc1, pc2;
+	v_copy(iv, &iv[len], PIT_COR_LEN - len);
+	Word40 acc = 0;
+	for (int i = 0; i < PIT_COR_LEN; i++)
+		acc = L40_mac(acc, lp[i], lp[i]);
+	Word16 sh = norm32(acc);
+	rc[0] = r_ound((Word32) L40_shl(acc, sh));
+	for (int i = 1; i < 3; i++) {
+		acc = 0;
+		for (int j = i; j < PIT_COR_LEN; j++)
+			acc = L40_mac(acc, lp[j], lp[j - i]);
+		rc[i] = r_ound((Word32) L40_shl(acc, sh));
+	}
+	if (rc[0] == 0) {
+		pc1 = pc2 = 0;
+	} else {
+		Word16 rc1 = divide_s(rc[1], rc[0]);
+		Word16 t1 = mult(rc1, rc[1]);
+		Word16 t2 = sub(rc[0], t1);
+		Word16 t3 = sub(rc[2], t1);
+		t1 = abs_s(t3);
+		if (t1 > t2) {
+			pc2 = -4096;
+		} else {
+			pc2 = divide_s(t1, t2);
+			if (t3 < 0)
+				pc2 = negate(pc2);
+			pc2 = shr(pc2, 3);
+		}
+		pc1 = mult(rc1, pc2);
+	}
+	for (int i = 0; i < len; i++) {
+		int k = PIT_COR_LEN - len + i;
+		Word32 t = L_shl(L_deposit_l(lp[k]), 13);
+		t = L_sub(t, L_mult(pc1, lp[k - 1]));
+		t = L_sub(t, L_mult(pc2, lp[k - 2]));
+		iv[k] = r_ound(L_shl(t, 3));
+	}
+}
+
+/* normalised 40-bit correlation step shared by corPeak and frac_cor:
+ * combines r0/rk normalisation and returns A/sqrt(r0 rk) in Q15 */
+MD Word16 cor_gain(Word32 *Lr0, Word16 *r0s, Word16 rks, Word32 Lrk, Word40 A, bool clip_neg)
+{
+	Word16 sh = add(*r0s, rks);
+	if (sh & 1) {
+		*Lr0 = L_shr(*Lr0, 1);
+		*r0s = sub(*r0s, 1);
+		sh = add(*r0s, rks);
+	}
+	sh = shr(sh, 1);
+	A = L40_shl(A, sh);
+	Word16 root = sqrt_Q15(mult(extract_h(*Lr0), extract_h(Lrk)));
+	Word16 t = extract_h((Word32) A);
+	if (clip_neg && t < 0)
+		t = 0;
+	return divide_s(t, root);
+}
+
+MD void norm40(Word40 *acc, Word16 *sh, Word32 *L)
+{
+	if (*acc == 0)
+		*acc = 1;
+	*sh = norm32(*acc);
+	*acc = L40_shl(*acc, *sh);
+	*L = (Word32) *acc;
+}
+
+/* corPeak :216 */
+MD void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
+{
+	int16_t pb[PIT_COR_LEN];
+	int16_t index[MAXPITCH + 1], gp[MAXPITCH + 1], peak[MAXPITCH + 1], corx[NODE];
+	const int PW = PIT_COR_LEN - MAXPITCH;	/* 73 */
+	remove_dc(in, pb, PIT_COR_LEN);
+	Word40 r0 = 0, rk = 0, A = 0;
+	Word16 r0s, rks;
+	Word32 Lr0, Lrk;
+	for (int i = 0; i < PW; i++)
+		r0 = L40_mac(r0, pb[i], pb[i]);
+	norm40(&r0, &r0s, &Lr0);
+	for (int i = MAXPITCH; i < PIT_COR_LEN; i++)
+		rk = L40_mac(rk, pb[i], pb[i]);
+	norm40(&rk, &rks, &Lrk);
+	for (int i = 0; i < PW; i++)
+		A = L40_mac(A, pb[i], pb[i + MAXPITCH]);
+	gp[MAXPITCH] = cor_gain(&Lr0, &r0s, rks, Lrk, A, true);
+	int lo = 0, hi = MAXPITCH;
+	for (int i = MAXPITCH - 1; i >= MINPITCH; i--) {
+		if (i % 2 == 0) {
+			r0 = L40_shr((Word40) Lr0, r0s);
+			r0 = L40_msu(r0, pb[lo], pb[lo]);
+			r0 = L40_mac(r0, pb[lo + PW], pb[lo + PW]);
+			norm40(&r0, &r0s, &Lr0);
+			lo++;
+		} else {
+			hi--;
+			rk = L40_shr((Word40) Lrk, rks);
+			rk = L40_mac(rk, pb[hi], pb[hi]);
+			rk = L40_msu(rk, pb[hi + PW], pb[hi + PW]);
+			norm40(&rk, &rks, &Lrk);
+		}
+		A = 0;
+		for (int j = lo; j < lo + PW; j++)
+			A = L40_mac(A, pb[j], pb[j + i]);
+		gp[i] = cor_gain(&Lr0, &r0s, rks, Lrk, A, true);
+	}
+	peak[MINPITCH] = (gp[MINPITCH + 1] < gp[MINPITCH]) ? gp[MINPITCH] : (int16_t) 0;
+	peak[MAXPITCH] = (gp[MAXPITCH] > gp[MAXPITCH - 1]) ? gp[MAXPITCH] : (int16_t) 0;
+	for (int i = MINPITCH + 1; i < MAXPITCH; i++)
+		peak[i] = (gp[i] > gp[i - 1] && gp[i] > gp[i + 1]) ? gp[i] : (int16_t) 0;
+	v_zero(index, MAXPITCH + 1);
+	for (int i = 0; i < NODE; i++) {
+		int best = MAXPITCH;
+		for (int j = MAXPITCH - 1; j >= MINPITCH; j--)
+			if (peak[j] > peak[best])
+				best = j;
+		index[best] = (int16_t) (i + 1);
+		corx[i] = peak[best];
+		peak[best] = 0;
+		if (i == 0)
+			cs->pitch = (int16_t) best;
+	}
+	cs->corx = corx[0];
+	int n = 0;
+	for (int i = MINPITCH; i <= MAXPITCH; i++)
+		if (index[i] != 0) {
+			pt->pit[n] = (int16_t) i;
+			pt->weight[n] = corx[index[i] - 1];
+			n++;
+		}
+	for (; n < NODE; n++) {
+		pt->pit[n] = 100;
+		pt->weight[n] = 0;
+	}
+	for (int i = 0; i < NODE - 1; i++)
+		for (int j = i + 1; j < NODE; j++) {
+			Word16 t1 = pt->pit[j], t2 = pt->pit[i], t = t2;
+			while (t < t1)
+				t = add(t, t2);
+			t2 = sub(t, shr(t2, 1));
+			if (t2 >= t1)
+				t = sub(t, pt->pit[i]);
+			t = abs_s(sub(pt->pit[j], t));
+			t2 = divide_s(t, pt->pit[j]);
+			if (t2 < 2621) {
+				t1 = mult(pt->weight[i], 6554);
+				t2 = sub(pt->weight[j], t1);
+				if (t2 < 0)
+					t2 = 0;
+				pt->weight[j] = t2;
+			}
+		}
+}
+
+/* pitchAuto :63 */
+MD void pitchAuto(EncState *E, const int16_t *in, PitTrack *pt, ClassParam *cs)
+{
+	if (!E->pauto_started) {
+		v_zero(E->lpbuf, PIT_COR_LEN);
+		v_zero(E->ivbuf, PIT_COR_LEN);
+		E->pauto_started = 1;
+	}
+	lpfilt(in, E->lpbuf, PIT_SUBFRAME);
+	ivfilt(E->ivbuf, E->lpbuf, PIT_SUBFRAME);
+	corPeak(E->ivbuf, pt, cs);
+}
+
+/* multiCheck :433 */
+MD Word16 multiCheck(Word16 f1, Word16 f2)
+{
+	if (f1 <= f2) {
+		Word16 t = f1;
+		f1 = f2;
+		f2 = t;
+	}
+	Word16 m = f2;
+	while (m <= f1)
+		m = add(m, f2);
+	if (sub(m, shr(f2, 1)) > f1)
+		m = sub(m, f2);
+	return ratio(f1, m);
+}
+
+/* trackPitch :471 */
+MD Word16 trackPitch(Word16 pitch, const PitTrack *pt)
+{
+	Word16 idx = -1, co = SW_MIN_;
+	for (int i = 0; i < NODE; i++) {
+		Word16 t = shl(pt->pit[i], 7);
+		if (ratio(t, pitch) < 6554 && pt->weight[i] > co) {
+			co = pt->weight[i];
+			idx = (Word16) i;
+		}
+	}
+	if (idx < 0) {
+		idx = 0;
+		Word16 best = abs_s(sub(shl(pt->pit[0], 7), pitch));
+		for (int i = 1; i < NODE; i++) {
+			Word16 t = abs_s(sub(shl(pt->pit[i], 7), pitch));
+			if (t < best) {
+				idx = (Word16) i;
+				best = t;
+			}
+		}
+	}
+	return idx;
+}
+
+/* pitLookahead :530 -- dynamic-programming look-ahead over the tracks */
+MD Word16 pitLookahead(PitTrack *pt, int num)
+{
+	for (int i = 0; i < NODE; i++) {
+		Word32 s = L_sub(LW_MAX_, L_deposit_h(pt[num].weight[i]));
+		pt[num].cost[i] = extract_h(L_mult(extract_h(s), 3200));
+	}
+	for (int i = num - 1; i >= 0; i--)
+		for (int j = 0; j < NODE; j++) {
+			Word16 k = trackPitch(shl(pt[i].pit[j], 7), &pt[i + 1]);
+			Word32 s = L_sub(LW_MAX_, L_deposit_h(pt[i].weight[j]));
+			Word32 c = L_mult(extract_h(s), 3200);
+			s = L_sub(L_deposit_h(pt[i].pit[j]), L_deposit_h(pt[i + 1].pit[k]));
+			c = L_add(c, L_shl(L_abs(s), 5));
+			c = L_add(c, L_deposit_h(pt[i + 1].cost[k]));
+			pt[i].cost[j] = extract_h(c);
+		}
+	Word32 best = L_deposit_h(pt[0].cost[0]);
+	int idx = 0;
+	for (int i = 1; i < NODE; i++)
+		if (L_deposit_h(pt[0].cost[i]) < best) {
+			best = L_deposit_h(pt[0].cost[i]);
+			idx = i;
+		}
+	return shl(pt[0].pit[idx], 7);
+}
+
+/* ------------------------------------------------------------------ */
+/* melpe/classify.c                                                    */
+/* ------------------------------------------------------------------ */
+
+/* zeroCrosCount :404 */
+MD Word16 zeroCrosCount(const int16_t *sp)
+{
+	int16_t d[PIT_SUBFRAME];
+	remove_dc(sp, d, PIT_SUBFRAME);
+	Word16 cnt = 0;
+	int ps = d[0] >= 0 ? 1 : -1;
+	for (int i = 1; i < PIT_SUBFRAME; i++) {
+		int cs = d[i] >= 0 ? 1 : -1;
+		if (ps + cs == 0)
+			cnt++;
+		ps = cs;
+	}
+	return divide_s(cnt, PIT_SUBFRAME);
+}
+
+/* bandEn :448 */
+MD Word16 bandEn(const int16_t *ac, int band)
+{
+	const int16_t *cf = band == 0 ? TB(enlpf_coef) : TB(enhpf_coef);
+	Word32 e = 0;
+	for (int i = 1; i < 17; i++)
+		e = L_add(e, L_deposit_l(mult(cf[i], ac[i])));
+	e = L_shl(e, 1);
+	e = L_add(e, L_deposit_l(mult(cf[0], ac[0])));
+	if (e < 16384)
+		return 0;
+	return log10_fxp(extract_l(L_shr(e, 4)), 10);
+}
+
+/* frac_cor :504 -- best normalised correlation within +-5 of pitch */
+MD Word16 frac_cor(const int16_t *in, Word16 pitch)
+{
+	Word16 lp = sub(pitch, 5), hp = add(pitch, 5);
+	if (lp < MINPITCH)
+		lp = MINPITCH;
+	if (hp > MAXPITCH)
+		hp = MAXPITCH;
+	Word40 r0 = 0, rk = 0, A = 0;
+	Word16 r0s, rks;
+	Word32 Lr0, Lrk;
+	for (int i = 0; i < PIT_COR_LEN - hp; i++)
+		r0 = L40_mac(r0, in[i], in[i]);
+	norm40(&r0, &r0s, &Lr0);
+	for (int i = hp; i < PIT_COR_LEN; i++)
+		rk = L40_mac(rk, in[i], in[i]);
+	norm40(&rk, &rks, &Lrk);
+	for (int i = 0; i < PIT_COR_LEN - hp; i++)
+		A = L40_mac(A, in[i], in[i + hp]);
+	Word16 maxgp = cor_gain(&Lr0, &r0s, rks, Lrk, A, true);
+	int lo = 0, hi = hp;
+	Word16 win = sub(PIT_COR_LEN, hp);
+	for (Word16 i = sub(hp, 1); i >= lp; i--) {
+		if (i % 2 == 0) {
+			r0 = L40_shr((Word40) Lr0, r0s);
+			r0 = L40_msu(r0, in[lo], in[lo]);
+			r0 = L40_mac(r0, in[lo + win], in[lo + win]);
+			norm40(&r0, &r0s, &Lr0);
+			lo++;
+		} else {
+			hi--;
+			rk = L40_shr((Word40) Lrk, rks);
+			rk = L40_mac(rk, in[hi], in[hi]);
+			rk = L40_msu(rk, in[hi + win], in[hi + win]);
+			norm40(&rk, &rks, &Lrk);
+		}
+		A = 0;
+		for (int j = lo; j < lo + win; j++)
+			A = L40_mac(A, in[j], in[j + i]);
+		Word16 g = cor_gain(&Lr0, &r0s, rks, Lrk, A, false);
+		if (g > maxgp)
+			maxgp = g;
+	}
+	return maxgp;
+}
+
+/* classify :92 -- silence/unvoiced/voiced/transition decision per 90-sample
+ * subframe; cs[-1] is the previous subframe's parameters */
+MD void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *ac)
+{
+	int16_t sa[BPF_ORD / 3 + PIT_COR_LEN], sbb[BPF_ORD / 3 + PIT_COR_LEN];
+	int16_t insp[PIT_SUBFRAME];
+	int16_t *si, *so;
+	int slen;
+	const bool first = !E->cls_started;
+	const int KEEP = PIT_COR_LEN - PIT_SUBFRAME;	/* 130 */
+	if (first) {
+		E->voicedEn = 10240;
+		E->silenceEn = 6144;
+		E->voicedCnt = 0;
+		v_zero(E->bpfdel, BPF_ORD + BPF_ORD / 3);
+		si = sa;
+		so = sbb;
+		slen = PIT_COR_LEN;
+		v_copy(&si[2], &in[(PIT_SUBFRAME - PIT_COR_LEN) / 2], slen);
+	} else {
+		si = sa + KEEP;
+		so = sbb + KEEP;
+		slen = PIT_SUBFRAME;
+		v_copy(&si[2], &in[(PIT_COR_LEN - PIT_SUBFRAME) / 2], slen);
+		v_copy(&so[2 - KEEP], E->back_sigbuf, KEEP);
+	}
+	const int16_t *pn = TB(bpf_num), *pd = TB(bpf_den) + 1;
+	for (int s = 0; s < BPF_ORD / 2; s++) {
+		v_copy(si, &E->bpfdel[2 * s], 2);
+		v_copy(so, &E->bpfdel[2 * s + 2], 2);
+		for (int j = 2; j < slen + 2; j++) {
+			Word32 t = L_mult(si[j], pn[0]);
+			t = L_mac(t, si[j - 1], pn[1]);
+			t = L_mac(t, si[j - 2], pn[2]);
+			t = L_mac(t, so[j - 1], pd[0]);
+			t = L_mac(t, so[j - 2], pd[1]);
+			so[j] = r_ound(L_shl(t, 2));
+		}
+		v_copy(&E->bpfdel[2 * s], &si[slen], 2);
+		int16_t *tp = si;
+		si = so;
+		so = tp;
+		pn += 3;
+		pd += 3;
+	}
+	if (first) {
+		E->cls_started = 1;
+		so = si;
+	} else {
+		so = si - KEEP;
+	}
+	v_copy(&E->bpfdel[BPF_ORD], &so[PIT_COR_LEN], 2);
+	v_copy(E->back_sigbuf, &so[2 + PIT_SUBFRAME], KEEP);
+
+	Word16 mx = 0, t1, t2, sh1 = 0;
+	Word32 L1, L2 = 0;
+	for (int i = 0; i < PIT_SUBFRAME; i++) {
+		t1 = abs_s(in[i]);
+		if (mx < t1)
+			mx = t1;
+		L2 = L_add(L2, t1);
+	}
+	if (mx == 0) {
+		L1 = 0;
+	} else if (mx <= 4884) {
+		L1 = L_v_magsq(in, PIT_SUBFRAME, 0, 0);
+		sh1 = 0;
+	} else {
+		v_equ_shr(insp, in, 3, PIT_SUBFRAME);
+		L1 = L_v_magsq(insp, PIT_SUBFRAME, 0, 0);
+		sh1 = 6;
+	}
+	while (L1 > SW_MAX_) {
+		L1 = L_shr(L1, 2);
+		sh1 = add(sh1, 2);
+	}
+	if (L1 == 0) {
+		cs->subEnergy = -20480;
+	} else {
+		t1 = shr(log10_fxp(extract_l(L1), 0), 1);
+		t2 = extract_l(L_shr(L_mult(617, sh1), 1));
+		cs->subEnergy = add(t1, t2);
+	}
+	cs->zeroCrosRate = zeroCrosCount(in);
+	if (L2 == 0) {
+		cs->peakiness = 2048;
+	} else {
+		sh1 = add(sh1, 15);
+		if (sh1 & 1) {
+			t1 = extract_l(L_shr(L1, 1));
+			sh1 = add(sh1, 1);
+		} else {
+			t1 = extract_l(L1);
+		}
+		sh1 = shr(sh1, 1);
+		t1 = sqrt_Q15(t1);
+		sh1 = sub(sh1, 8);
+		t2 = extract_l(L_shr(L2, sh1));
+		t1 = shr(t1, 7);
+		t1 = divide_s(t1, t2);
+		cs->peakiness = mult(19429, t1);
+	}
+	Word16 lhbd = sub(bandEn(ac, 0), bandEn(ac, 1));
+	Word16 lbc = frac_cor(&so[2], cs->pitch);
+	if (E->silenceEn > sub(E->voicedEn, 3072))
+		E->silenceEn = sub(E->voicedEn, 3072);
+	Word16 zcd = sub(cs->zeroCrosRate, cs[-1].zeroCrosRate);
+	Word16 sed = sub(cs->subEnergy, cs[-1].subEnergy);
+	const Word16 vEn = E->voicedEn, sEn = E->silenceEn;
+	int16_t cl;
+	if (cs->subEnergy < 6144) {
+		cl = SILENCE;
+	} else if (cs->subEnergy < interp_scalar(vEn, sEn, 21299)) {
+		if (cs->zeroCrosRate > 19661 && (cs->corx < 13107 || lbc < 16384))
+			cl = UNVOICED;
+		else if (lbc > 22938 || (lbc > 13107 && cs->corx > 22938))
+			cl = VOICED;
+		else if (zcd > 9830 || sed > 4096 || cs->peakiness > 3277)
+			cl = TRANSITION;
+		else if (cs->zeroCrosRate > 18022 || (lhbd < 2048 && cs->zeroCrosRate > 13107))
+			cl = UNVOICED;
+		else
+			cl = SILENCE;
+	} else if (zcd > 6554 || sed > 4096 || cs->peakiness > 3277) {
+		cl = (lbc > 22938 || cs->corx > 26214) ? VOICED : TRANSITION;
+	} else if (cs->zeroCrosRate < 6554) {
+		if (lbc > 16384 || (lbc > 9830 && cs->corx > 19661))
+			cl = VOICED;
+		else if (cs->subEnergy > interp_scalar(vEn, sEn, 9830))
+			cl = (cs->peakiness > 3072) ? TRANSITION : VOICED;
+		else
+			cl = SILENCE;
+	} else if (cs->zeroCrosRate < 16384) {
+		if (lbc > 18022 || (lbc > 9830 && cs->corx > 21299))
+			cl = VOICED;
+		else if (cs->subEnergy < interp_scalar(vEn, sEn, 19661) && lhbd > 4096)
+			cl = SILENCE;
+		else if (cs->peakiness > 2867)
+			cl = TRANSITION;
+		else
+			cl = UNVOICED;
+	} else if (cs->zeroCrosRate < 22938) {
+		if ((lbc > 19661 && cs->corx > 9830) || (lbc > 13107 && cs->corx > 22938))
+			cl = VOICED;
+		else if (cs->peakiness > 3072)
+			cl = TRANSITION;
+		else
+			cl = UNVOICED;
+	} else {
+		if ((lbc > 21299 && cs->corx > 9830) || (lbc > 14746 && cs->corx > 22938))
+			cl = VOICED;
+		else if (cs->peakiness > 4096)
+			cl = TRANSITION;
+		else
+			cl = UNVOICED;
+	}
+	cs->classy = cl;
+}
+
+/* ------------------------------------------------------------------ */
+/* find_harm, melpe/fs_lib.c:62 -- Fourier magnitudes of the residual */
+/* ------------------------------------------------------------------ */
+MD void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, int len)
+{
+	int16_t hb[1024];
+	Word32 Lm[NUM_HARM];
+	Word16 mx = 0;
+	for (int i = 0; i < len; i++) {
+		Word16 t = abs_s(in[i]);
+		if (t > mx)
+			mx = t;
+	}
+	Word16 sh = norm_s(mx);
+	v_set(fsmag, 8192, nh);
+	v_zero(hb, 1024);
+	for (int i = 0; i < len; i++)
+		hb[i] = shl(in[i], sh);
+	rfft(hb, 512);
+	Word16 fw = shr(divide_s(512, pitch), 2);
+	Word16 iw = shr(fw, 6);
+	Word16 i2 = shr(iw, 1);
+	Word16 t1 = shr(pitch, 9);
+	if (nh > t1)
+		nh = t1;
+	Word16 mfw = fw;
+	for (int k = 0; k < nh; k++) {
+		Word16 i0 = sub(shr(add(mfw, 32), 6), i2);
+		Word32 Lmax = 0;
+		for (int j = 0; j < iw; j++) {
+			Word16 b = add(i0, (Word16) j);
+			Word16 re = hb[2 * b], im = hb[2 * b + 1];
+			Word32 t = L_add(L_mult(re, re), L_mult(im, im));
+			Lmax = Max_(Lmax, t);
+		}
+		Lm[k] = Lmax;
+		mfw = add(mfw, fw);
+	}
+	Word40 avg = 1;
+	for (int k = 0; k < nh; k++)
+		avg = L40_add(avg, Lm[k]);
+	t1 = norm32(avg);
+	Word32 Lt = (Word32) L40_shl(avg, t1);
+	t1 = sub(31, t1);
+	Word16 t2 = divide_s(shl(nh, 10), extract_h(Lt));
+	sh = sub(30, t1);
+	for (int i = 0; i < nh; i++) {
+		t1 = extract_h(L_shl(Lm[i], sh));
+		t1 = extract_h(L_shl(L_mult(t1, t2), 2));
+		fsmag[i] = sqrt_Q15(t1);
+	}
+}
+
+}  // namespace mlp
+
+#endif

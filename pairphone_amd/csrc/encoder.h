@@ -1,0 +1,386 @@
+/*
+ * encoder.h -- one superframe of MELPe-1200 analysis + quantisation for one
+ * channel: melpe_a (melpe/melpe.c:91-99) = 3 x npp + analysis().
+ *
+ * analysis()  restates melpe/melp_ana.c:119-267
+ * melp_ana()  restates melpe/melp_ana.c:280-469
+ * sc_ana()    restates melpe/melp_ana.c:522-953
+ */
+#ifndef MELPE_ENCODER_H
+#define MELPE_ENCODER_H
+
+#include "quant.h"
+
+namespace mlp {
+
+/* melp_ana :280 -- analysis of one 180-sample frame; `speech` points at
+ * hpspeech[i*FRAME] (the window spans speech[0 .. FRAME_END+PITCHMAX]) */
+MD void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
+{
+	int16_t *sb = E->sigbuf;
+	int16_t ac[17], lpc[LPC_ORD + 1], tdin[LPF_ORD], tdout[LPF_ORD];
+	Word16 sub_pitch, t, dontcare, pcorr;
+	if (!E->ana_started) {
+		v_zero(E->lpfsp_delin, LPF_ORD);
+		v_zero(E->lpfsp_delout, LPF_ORD);
+		E->pitch_avg = DEFAULT_PITCH_Q7;
+		v_set(E->fpitch, DEFAULT_PITCH_Q7, 2);
+		E->ana_started = 1;
+	}
+	/* lowpass for the global pitch; the filter memory advances by FRAME only
+	 * (melp_ana.c:324-346) */
+	v_copy(&sb[LPF_ORD], &speech[PITCH_BEG], PITCH_FR);
+	for (int s = 0; s < LPF_ORD / 2; s++) {
+		for (int i = s * 2; i < s * 2 + 2; i++)
+			tdin[i] = sb[LPF_ORD + FRAME - 1 - i + s * 2];
+		iir_2nd_s(&sb[LPF_ORD], TB(lpf_den) + s * 3, TB(lpf_num) + s * 3, &sb[LPF_ORD],
+			  &E->lpfsp_delin[s * 2], &E->lpfsp_delout[s * 2], FRAME);
+		v_copy(&tdout[2 * s], &E->lpfsp_delout[2 * s], 2);
+		iir_2nd_s(&sb[LPF_ORD + FRAME], TB(lpf_den) + s * 3, TB(lpf_num) + s * 3,
+			  &sb[LPF_ORD + FRAME], &E->lpfsp_delin[s * 2], &E->lpfsp_delout[s * 2],
+			  PITCH_FR - FRAME);
+		v_copy(&E->lpfsp_delin[2 * s], &tdin[2 * s], 2);
+		v_copy(&E->lpfsp_delout[2 * s], &tdout[2 * s], 2);
+	}
+	f_pitch_scale(&sb[LPF_ORD], &sb[LPF_ORD], PITCH_FR);
+	E->fpitch[1] = find_pitch(&sb[LPF_ORD + PITCH_FR / 2], &dontcare, 2 * PITCHMIN,
+				  PITCHMAX, PITCHMAX);
+	E->fpitch[1] = shl(E->fpitch[1], 7);
+	bpvc_ana(E, &speech[FRAME_END], E->fpitch, par->bpvc, &sub_pitch);
+	par->jitter = (par->bpvc[0] < VJIT_Q14) ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;
+	lpc_acor(&speech[FRAME_END - LPC_FRAME / 2], TB(win_cof), ac, 4, 16, LPC_FRAME);
+	lpc[0] = 4096;
+	lpc_schr(ac, &lpc[1], LPC_ORD);
+	lpc_bwex(&lpc[1], &lpc[1], 32571, LPC_ORD);
+	lpc_pred2lsp(&lpc[1], par->lsf, LPC_ORD);
+	lpc_clmp(par->lsf, 409, LPC_ORD);
+	zerflt(&speech[PITCH_BEG], lpc, &sb[LPF_ORD], LPC_ORD, PITCH_FR);
+	t = peakiness(&sb[LPF_ORD + PITCHMAX / 2], PITCHMAX);
+	if (t > 5488)
+		par->bpvc[0] = 16384;
+	if (t > 6553) {
+		par->bpvc[1] = 16384;
+		par->bpvc[2] = 16384;
+	}
+	int ct = CUR_TRACK + subnum * PIT_SUBNUM;
+	for (int i = 0; i < PIT_SUBNUM; i++) {
+		pitchAuto(E, &speech[FRAME_END + i * PIT_SUBFRAME + PIT_COR_LEN / 2],
+			  &E->pitTrack[ct + i + 1], &E->classStat[ct + i + 1]);
+		classify(E, &speech[FRAME_END + i * PIT_SUBFRAME + PIT_SUBFRAME / 2],
+			 &E->classStat[ct + i + 1], ac);
+	}
+	par->pitch = pitch_ana(E, &speech[FRAME_END], &sb[LPF_ORD + PITCHMAX], sub_pitch,
+			       E->pitch_avg, &pcorr);
+	for (int i = 0; i < NUM_GAINFR; i++) {
+		if (par->bpvc[0] > BPTHRESH_Q14)
+			par->gain[i] = gain_ana(&speech[FRAME_BEG + (i + 1) * 90], sub_pitch, 120, 320);
+		else
+			par->gain[i] = gain_ana(&speech[FRAME_BEG + (i + 1) * 90], 15258, 0, 320);
+	}
+	t = (par->gain[NUM_GAINFR - 1] > 7680) ? pcorr : (Word16) 0;
+	E->pitch_avg = p_avg_update(E, par->pitch, t, VMIN_Q14);
+	par->uv_flag = (par->bpvc[0] > BPTHRESH_Q14) ? 0 : 1;
+	E->fpitch[0] = E->fpitch[1];
+}
+
+/* subenergyRelation1/2 :955/:980 (plain int arithmetic, as the reference) */
+MD bool subEnRel1(const ClassParam *cs, int c)
+{
+	int pg = cs[c - 2].subEnergy, lg = cs[c - 1].subEnergy, og = cs[c].subEnergy;
+	int ng = cs[c + 1].subEnergy, fg = cs[c + 2].subEnergy;
+	return ((lg - pg < 1024) && (og - lg < 1024) && (ng - og < 1024) &&
+		((pg - lg > 2458) || (lg - og > 2458) || (og - ng > 2458))) ||
+	       ((og - lg < 614) && (ng - og < 614) &&
+		(((lg - pg < 614) && ((pg - og > 1638) || (lg - ng > 1638))) ||
+		 ((fg - ng < 614) && ((lg - ng > 1638) || (og - fg > 1638)))));
+}
+
+MD bool subEnRel2(const ClassParam *cs, int c)
+{
+	int pg = cs[c - 2].subEnergy, lg = cs[c - 1].subEnergy, og = cs[c].subEnergy;
+	int ng = cs[c + 1].subEnergy, fg = cs[c + 2].subEnergy;
+	return ((lg - og < 614) && (og - ng < 614) &&
+		(((pg - lg < 614) && ((og - pg > 1638) || (ng - lg > 1638))) ||
+		 ((ng - fg < 614) && ((ng - lg > 1638) || (fg - og > 1638))))) ||
+	       ((pg - lg < 1024) && (lg - og < 1024) && (og - ng < 1024) &&
+		((lg - pg > 2458) || (og - lg > 2458) || (ng - og > 2458)));
+}
+
+/* the pitch-track correction shared by frames 0 and 1 of sc_ana when the
+ * tracks disagree (melp_ana.c:590-640 and 700-760) */
+MD void sc_track_fix(PitTrack *pt, int16_t *pitch, Word16 prev_pitch)
+{
+	Word16 i1 = trackPitch(prev_pitch, pt);
+	Word16 cand = shl(pt->pit[i1], 7);
+	Word16 i2 = trackPitch(*pitch, pt);
+	Word16 w12 = sub(pt->weight[i1], pt->weight[i2]);
+	if (multiCheck(*pitch, cand) < 2621) {
+		if ((*pitch > cand && w12 > -6554) || w12 > 6554)
+			*pitch = cand;
+	} else if (w12 > -3277) {
+		*pitch = cand;
+	}
+}
+
+/* sc_ana :522 -- superframe pitch smoothing and bpvc smoothing */
+MD void sc_ana(EncState *E, MelpParam *par)
+{
+	ClassParam *cs = E->classStat;
+	PitTrack *pt = E->pitTrack;
+	int16_t bpc[NUM_BANDS], sbp[NF + 1], uv[NF + 1];
+	Word16 cand, np, t1, t2, i1, i2, idx;
+	for (int i = 0; i < NF; i++) {
+		int c = i * PIT_SUBNUM + CUR_TRACK;
+		if (cs[c].classy == SILENCE && cs[c - 1].classy == SILENCE)
+			E->silenceEn = updateEn(E->silenceEn, 29491, cs[c].subEnergy);
+	}
+	uv[0] = E->sc_prev_uv;
+	uv[1] = par[0].uv_flag;
+	uv[2] = par[1].uv_flag;
+	uv[3] = par[2].uv_flag;
+	Word16 prev_pitch = E->sc_prev_pitch;
+
+	/* ---- frame 0 ---- */
+	int c = CUR_TRACK;
+	E->voicedCnt = uv[1] ? 0 : E->voicedCnt + 1;
+	if (!uv[1] && !uv[2] && !uv[3] && !subEnRel1(cs, c)) {
+		if (E->voicedCnt < 2 || subEnRel2(cs, c)) {
+			cand = pitLookahead(&pt[c], 3);
+			if (ratio(par[0].pitch, cand) > 4915) {
+				if (ratio(cand, par[1].pitch) < 4915)
+					par[0].pitch = cand;
+				else if (ratio(par[1].pitch, par[2].pitch) < 4915 &&
+					 ratio(par[0].pitch, par[1].pitch) > 4915)
+					par[0].pitch = par[1].pitch;
+				else if (ratio(par[0].pitch, par[1].pitch) > 4915)
+					par[0].pitch = cand;
+			}
+		} else if (!uv[0]) {
+			i1 = shr(sub(par[0].pitch, prev_pitch), 7);
+			i2 = shr(sub(par[1].pitch, par[0].pitch), 7);
+			if (abs_s(i1) > 5 && abs_s(i2) > 5 && i1 * i2 < 0) {
+				cand = pitLookahead(&pt[c], 3);
+				if (ratio(prev_pitch, cand) < 4915 || ratio(cand, par[1].pitch) < 6554)
+					par[0].pitch = cand;
+				else
+					par[0].pitch = add(shr(prev_pitch, 1), shr(par[1].pitch, 1));
+			} else if (ratio(par[0].pitch, prev_pitch) > 4915 &&
+				   (ratio(par[1].pitch, prev_pitch) < 4915 ||
+				    ratio(par[2].pitch, prev_pitch) < 4915)) {
+				sc_track_fix(&pt[c], &par[0].pitch, prev_pitch);
+			} else if (L_ratio(par[0].pitch, (Word32) (prev_pitch * 2)) < 2621 ||
+				   L_ratio(par[0].pitch, (Word32) (prev_pitch * 3)) < 2621) {
+				cand = pitLookahead(&pt[c], 4);
+				if (ratio(cand, prev_pitch) < 3277)
+					par[0].pitch = cand;
+			}
+		}
+	}
+	prev_pitch = shl(shr(par[0].pitch, 7), 7);
+
+	/* ---- frame 1 ---- */
+	c = CUR_TRACK + 2;
+	E->voicedCnt = uv[2] ? 0 : E->voicedCnt + 1;
+	if (!uv[2] && !subEnRel1(cs, c)) {
+		if (E->voicedCnt < 2 || subEnRel2(cs, c)) {
+			cand = pitLookahead(&pt[c], 3);
+			if (ratio(par[1].pitch, cand) > 4915) {
+				if (ratio(cand, par[2].pitch) < 4915) {
+					par[1].pitch = cand;
+				} else {
+					np = pitLookahead(&pt[c + 1], 3);
+					if (ratio(np, par[2].pitch) < 4915) {
+						if (ratio(cand, np) < 4915)
+							par[1].pitch = cand;
+						else if (ratio(par[1].pitch, np) > 4915)
+							par[1].pitch = np;
+					} else if (ratio(cand, np) < 4915) {
+						par[1].pitch = cand;
+					}
+				}
+			}
+		} else if (!uv[1]) {
+			i1 = shr(sub(par[1].pitch, prev_pitch), 7);
+			i2 = shr(sub(par[2].pitch, par[1].pitch), 7);
+			cand = pitLookahead(&pt[c], 3);
+			if (abs_s(i1) > 5 && abs_s(i2) > 5 && i1 * i2 < 0) {
+				if (ratio(prev_pitch, cand) < 4915 || ratio(cand, par[2].pitch) < 6554)
+					par[1].pitch = cand;
+				else
+					par[1].pitch = add(shr(prev_pitch, 1), shr(par[2].pitch, 1));
+			} else if (ratio(par[1].pitch, prev_pitch) > 4915 &&
+				   (ratio(par[2].pitch, prev_pitch) < 4915 ||
+				    ratio(cand, prev_pitch) < 4915)) {
+				if (ratio(cand, prev_pitch) < 4915)
+					par[1].pitch = cand;
+				else
+					sc_track_fix(&pt[c], &par[1].pitch, prev_pitch);
+			} else if (L_ratio(par[1].pitch, (Word32) (prev_pitch * 2)) < 2621 ||
+				   L_ratio(par[1].pitch, (Word32) (prev_pitch * 3)) < 2621) {
+				cand = pitLookahead(&pt[c], 4);
+				if (ratio(cand, prev_pitch) < 3277)
+					par[1].pitch = cand;
+			}
+		}
+	}
+	prev_pitch = shl(shr(par[1].pitch, 7), 7);
+
+	/* ---- frame 2 ---- */
+	c = CUR_TRACK + 4;
+	E->voicedCnt = uv[3] ? 0 : E->voicedCnt + 1;
+	if (!uv[3] && cs[c + 1].classy == VOICED && cs[c + 2].classy == VOICED &&
+	    !subEnRel1(cs, c)) {
+		if (E->voicedCnt < 2 || subEnRel2(cs, c)) {
+			cand = pitLookahead(&pt[c], 2);
+			if (ratio(par[2].pitch, cand) > 4915) {
+				np = pitLookahead(&pt[c + 1], 1);
+				if (ratio(np, cand) < 4915)
+					par[2].pitch = cand;
+				else if (ratio(par[2].pitch, np) >= 4915)
+					par[2].pitch = np;
+			}
+		} else if (!uv[2]) {
+			cand = pitLookahead(&pt[c], 2);
+			i1 = shr(sub(par[2].pitch, prev_pitch), 7);
+			i2 = shr(sub(cand, par[2].pitch), 7);
+			if (abs_s(i1) > 5 && abs_s(i2) > 5 && i1 * i2 < 0) {
+				if (ratio(prev_pitch, cand) < 4915) {
+					par[2].pitch = cand;
+				} else {
+					i1 = trackPitch(cand, &pt[c]);
+					i2 = trackPitch(par[2].pitch, &pt[c]);
+					Word16 w12 = sub(pt[c].weight[i1], pt[c].weight[i2]);
+					if (multiCheck(par[2].pitch, cand) < 2621) {
+						if ((par[2].pitch > cand && w12 > -6554) || w12 > 6554)
+							par[2].pitch = cand;
+					} else {
+						i1 = trackPitch(prev_pitch, &pt[c]);
+						cand = shl(pt[c].pit[i1], 7);
+						w12 = sub(pt[c].weight[i1], pt[c].weight[i2]);
+						if (multiCheck(par[2].pitch, cand) < 2621) {
+							if ((par[2].pitch > cand && w12 > -6554) || w12 > 6554)
+								par[2].pitch = cand;
+						} else {
+							par[2].pitch = add(shr(prev_pitch, 1), shr(cand, 1));
+						}
+					}
+				}
+			}
+		}
+	}
+
+	/* ---- bandpass voicing smoothing (melp_ana.c:855-925) ---- */
+	sbp[0] = E->sc_prev_sbp3;
+	for (int i = 0; i < NF; i++) {
+		v_copy(bpc, par[i].bpvc, NUM_BANDS);
+		if (q_bpvc(bpc, &idx, NUM_BANDS))
+			sbp[i + 1] = -1;
+		else
+			sbp[i + 1] = TB(inv_bp_index_map)[TB(bp_index_map)[idx]];
+	}
+	const int vEn = E->voicedEn;
+	for (int i = 1; i < NF; i++) {
+		c = CUR_TRACK + (i - 1) * 2;
+		if (sbp[i - 1] > 12 && sbp[i + 1] > 12) {
+			if (cs[c].subEnergy > vEn - 1024 ||
+			    (par[i - 1].bpvc[2] > 8192 && par[i - 1].bpvc[3] > 8192)) {
+				if (sbp[i] < 12)
+					sbp[i] = 12;
+			} else if (sbp[i] < 8) {
+				sbp[i] = 8;
+			}
+		} else if (sbp[i - 1] > 8 && sbp[i + 1] > 8) {
+			if (cs[c].subEnergy > vEn - 2048 ||
+			    (par[i - 1].bpvc[2] > 6554 && par[i - 1].bpvc[3] > 6554)) {
+				if (sbp[i] < 8)
+					sbp[i] = 8;
+			}
+		} else if (sbp[i - 1] < 8 && sbp[i + 1] < 8) {
+			if (cs[c].subEnergy < vEn - 1024 && par[i - 1].bpvc[3] < 11469) {
+				if (sbp[i] > 12)
+					sbp[i] = 12;
+			}
+		}
+	}
+	c = CUR_TRACK + 4;
+	if (cs[c].subEnergy > vEn - 614 && sbp[2] > 12 && par[1].bpvc[2] > 8192 &&
+	    par[1].bpvc[3] > 8192) {
+		if (sbp[3] < 12)
+			sbp[3] = 12;
+	} else if (cs[c].subEnergy > vEn - 1024 && sbp[2] > 8 && par[1].bpvc[2] > 7273 &&
+		   par[1].bpvc[3] > 7273) {
+		if (sbp[3] < 8)
+			sbp[3] = 8;
+	}
+	for (int i = 0; i < NF; i++) {
+		t1 = par[i].bpvc[0];
+		q_bpvc_dec(par[i].bpvc, sbp[i + 1], 0, NUM_BANDS);
+		par[i].bpvc[0] = t1;
+	}
+	E->sc_prev_sbp3 = sbp[3];
+	for (int i = 0; i < NF; i++) {
+		c = i * PIT_SUBNUM + CUR_TRACK;
+		if (E->voicedCnt > 2)
+			E->voicedEn = updateEn(E->voicedEn, 29491, cs[c].subEnergy);
+		if (E->voicedEn < cs[c].subEnergy)
+			E->voicedEn = cs[c].subEnergy;
+	}
+	for (int i = 0; i < TRACK_NUM - NF * PIT_SUBNUM; i++) {
+		cs[i] = cs[i + NF * PIT_SUBNUM];
+		pt[i] = pt[i + NF * PIT_SUBNUM];
+	}
+	E->sc_prev_uv = par[NF - 1].uv_flag;
+	E->sc_prev_pitch = shl(shr(par[NF - 1].pitch, 7), 7);
+	(void) t2;
+}
+
+/* analysis :119 -- 540 NPP-processed samples -> quantised params + chbuf */
+MD void analysis(EncState *E, const int16_t *sp_in)
+{
+	MelpParam *par = E->par;
+	int16_t lpc[LPC_ORD + 1];
+	for (int i = 0; i < NF; i++) {
+		dc_rmv(&sp_in[i * FRAME], &E->hpspeech[IN_BEG + i * FRAME], E->dcdelin,
+		       E->dcdelout_hi, E->dcdelout_lo, FRAME);
+		melp_ana(E, &E->hpspeech[i * FRAME], &par[i], i);
+	}
+	sc_ana(E, par);
+	lpc[0] = 4096;
+	lsf_vq(E, par);
+	pitch_vq(E, par);
+	gain_vq(E, par);
+	for (int i = 0; i < NF; i++)
+		quant_u(&par[i].jitter, &E->qpar.jit_index[i], 0, MAX_JITTER_Q15, 2, SW_MAX_,
+			true, 7);
+	quant_bp(E, par);
+	quant_jitter(E, par);
+	for (int i = 0; i < NF; i++) {
+		v_set(par[i].fs_mag, 8192, NUM_HARM);
+		if (!par[i].uv_flag) {
+			lpc_lsp2pred(par[i].lsf, &lpc[1], LPC_ORD);
+			zerflt(&E->hpspeech[i * FRAME + FRAME_END - LPC_FRAME / 2], lpc, E->sigbuf,
+			       LPC_ORD, LPC_FRAME);
+			window(E->sigbuf, TB(win_cof), E->sigbuf, LPC_FRAME);
+			find_harm(E->sigbuf, par[i].fs_mag, par[i].pitch, NUM_HARM, LPC_FRAME);
+		}
+	}
+	quant_fsmag(E, par);
+	for (int i = 0; i < NF; i++)
+		E->qpar.uv_flag[i] = par[i].uv_flag;
+	low_rate_chn_write(E);
+	v_copy(E->hpspeech, &E->hpspeech[NF * FRAME], IN_BEG);
+}
+
+/* melpe_a :91 -- sp (540) is denoised in place, then analysed; the 11-byte
+ * frame is left in E->chbuf */
+MD void encode_superframe(EncState *E, NppScratch *w, int16_t *sp)
+{
+	npp_frame(&E->npp, w, sp, sp);
+	npp_frame(&E->npp, w, sp + FRAME, sp + FRAME);
+	npp_frame(&E->npp, w, sp + 2 * FRAME, sp + 2 * FRAME);
+	analysis(E, sp);
+}
+
+}  // namespace mlp
+
+#endif

@@ -13,8 +13,7 @@
 #include <string.h>
 #include <vector>
 
-#include "state.h"
-#include "derived.h"
+#include "codec.h"
 
 using namespace mlp;
 
@@ -37,8 +36,7 @@ int emu_load_tables(const char *path)
 	fclose(f);
 	if (n != MELPE_TABLE_WORDS)
 		return -2;
-	derive_fft_twiddles(&g_der);
-	derive_lsp_cos(&g_der);
+	derive_all(&g_der);
 	return 0;
 }
 
@@ -68,6 +66,45 @@ int emu_npp(emu_engine *e, int16_t *sp, int frames, int stride, int rate1200)
 			npp_frame(&e->enc[c].npp, &g_npp_scratch, x, x, rate1200 != 0);
 		}
 	return 0;
+}
+
+/* melpe_a on every channel: sp (C x 540) in/out, bits (C x 11) out */
+int emu_encode(emu_engine *e, unsigned char *bits, int16_t *sp)
+{
+	for (int c = 0; c < e->channels; c++) {
+		encode_superframe(&e->enc[c], &g_npp_scratch, sp + (size_t) c * BLOCK);
+		for (int k = 0; k < 11; k++)
+			bits[c * 11 + k] = e->enc[c].chbuf[k];
+	}
+	return 0;
+}
+
+/* per-superframe debug view of channel c: melp_par (3 x 30 int16) and
+ * quant_par (30 int16), in the layout oracle/ref_tool.c dumps */
+int emu_enc_params(emu_engine *e, int c, int16_t *out)
+{
+	const EncState *E = &e->enc[c];
+	memcpy(out, E->par, sizeof(E->par));
+	const QuantParam *q = &E->qpar;
+	int16_t *w = out + 90;
+	int k = 0;
+	w[k++] = q->pitch_index;
+	for (int i = 0; i < NF; i++)
+		for (int j = 0; j < MAX_LSF_STAGE; j++)
+			w[k++] = q->lsf_index[i][j];
+	for (int i = 0; i < NUM_GAINFR; i++)
+		w[k++] = q->gain_index[i];
+	for (int i = 0; i < NF; i++)
+		w[k++] = q->jit_index[i];
+	for (int i = 0; i < NF; i++)
+		w[k++] = q->bpvc_index[i];
+	w[k++] = q->fs_index;
+	for (int i = 0; i < NF; i++)
+		w[k++] = q->uv_flag[i];
+	for (int i = 0; i < MSVQ_STAGES; i++)
+		w[k++] = q->msvq_index[i];
+	w[k++] = q->fsvq_index;
+	return k;
 }
 
 }  // extern "C"

@@ -1,0 +1,796 @@
+/*
+ * quant.h -- 1200 bps quantisers and the 81-bit channel packing, encoder
+ * side: restates melpe/qnt12.c (pitch_vq, gain_vq, lsf_vq, quant_bp,
+ * quant_jitter, quant_fsmag), melpe/vq_lib.c (vq_lspw, vq_enc, vq_fsw),
+ * melpe/melp_chn.c (low_rate_chn_write, parity) and melpe/fec_code.c
+ * (low_rate_fec_code).  The sequential candidate-list updates of the
+ * reference (wvq1 slot replacement, InsertCand) are kept in order, so ties
+ * resolve exactly as there.
+ */
+#ifndef MELPE_QUANT_H
+#define MELPE_QUANT_H
+
+#include "analysis.h"
+
+namespace mlp {
+
+#define PITCH_VQ_CAND 16
+#define LSP_VQ_CAND 8
+#define LSP_VQ_STAGES 4
+#define LSP_INP_CAND 5
+
+/* vq_lspw, melpe/vq_lib.c:70 -- |A(e^jw)|^-0.3 weights */
+MD void vq_lspw(int16_t *w, const int16_t *lsp, const int16_t *lpc, int order)
+{
+	for (int i = 0; i < order; i++)
+		w[i] = L_pow_fxp(lpc_aejw(lpc, lsp[i], order), -9830, 19, 11);
+	w[8] = mult(w[8], 20971);
+	w[9] = mult(w[9], 5242);
+}
+
+/* vq_enc, melpe/vq_lib.c:474 -- full search, first minimum wins */
+MD Word32 vq_enc(const int16_t *cb, const int16_t *u, int levels, int order, int16_t *uhat,
+		 int16_t *index)
+{
+	int16_t best = 0;
+	Word32 dmin = LW_MAX_;
+	const int16_t *p = cb;
+	for (int i = 0; i < levels; i++) {
+		Word32 d = 0;
+		for (int j = 0; j < order; j++) {
+			Word16 t = sub(u[j], *p++);
+			d = L_mac(d, t, t);
+		}
+		if (d < dmin) {
+			dmin = d;
+			best = (int16_t) i;
+		}
+	}
+	*index = best;
+	v_copy(uhat, &cb[order * best], order);
+	return dmin;
+}
+
+/* vq_fsw, melpe/vq_lib.c:512 -- Fourier-magnitude weights (init time) */
+MD void vq_fsw(int16_t *wfs, int nh, Word16 pitch)
+{
+	Word16 w0 = divide_s(16384, pitch);
+	for (int i = 0; i < nh; i++) {
+		Word16 t = shl(add((Word16) i, 1), 11);
+		t = extract_h(L_shl(L_mult(w0, t), 1));
+		t = mult(t, t);
+		Word32 L = L_add(268435456L, L_mult(22937, t));
+		t = L_pow_fxp(L, 22609, 28, 13);
+		t = mult(19200, t);
+		wfs[i] = divide_s(3744, add(1600, t));
+	}
+}
+
+/* ------------------------------------------------------------------ */
+/* pitch VQ, melpe/qnt12.c:75-353                                      */
+/* ------------------------------------------------------------------ */
+
+/* wvq1 :221 -- keeps `cand` best entries; a new entry replaces the slot
+ * holding the current maximum, exactly as the reference's linear rescan */
+MD void wvq1(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int dim, int cbsize,
+	     int16_t *index, Word32 *dist, int cand)
+{
+	for (int j = 0; j < cand; j++)
+		dist[j] = LW_MAX_;
+	Word32 maxd = LW_MAX_;
+	int maxi = 0;
+	for (int i = 0; i < cbsize; i++) {
+		Word32 err = 0;
+		for (int j = 0; j < dim; j++)
+			if (wt[j] > 0) {
+				Word16 t = sub(tgt[j], cb[j]);
+				err = L_add(err, L_shr(L_mult(t, t), 2));
+				if (err >= maxd)
+					break;
+			}
+		if (err < maxd) {
+			index[maxi] = (int16_t) i;
+			dist[maxi] = err;
+			maxd = 0;
+			for (int j = 0; j < cand; j++)
+				if (dist[j] > maxd) {
+					maxd = dist[j];
+					maxi = j;
+				}
+		}
+		cb += dim;
+	}
+}
+
+/* wvq2 :302 */
+MD int16_t wvq2(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int dim,
+		const int16_t *index, const Word32 *dist, int cand)
+{
+	Word32 mn = LW_MAX_;
+	int16_t ind = 0;
+	for (int i = 0; i < cand; i++) {
+		Word32 err = dist[i];
+		for (int j = 0; j < dim; j++)
+			if (wt[j] > 0) {
+				Word16 t = sub(tgt[j], cb[j]);
+				err = L_add(err, L_shr(L_mult(t, t), 2));
+				if (err >= mn)
+					break;
+			}
+		if (err < mn) {
+			mn = err;
+			ind = index[i];
+		}
+		cb += dim;
+	}
+	return ind;
+}
+
+/* pitch_vq :75 */
+MD void pitch_vq(EncState *E, MelpParam *par)
+{
+	QuantParam *q = &E->qpar;
+	int16_t tgt[NF], deltp[NF], deltw[NF], wt[NF];
+	int16_t dcb[PITCH_VQ_CAND * NF], il[PITCH_VQ_CAND];
+	Word32 dl[PITCH_VQ_CAND];
+	for (int i = 0; i < NF; i++)
+		tgt[i] = log10_fxp(par[i].pitch, 7);
+	int cnt = 0;
+	for (int i = 0; i < NF; i++) {
+		if (par[i].uv_flag) {
+			wt[i] = 0;
+		} else {
+			wt[i] = 1;
+			cnt++;
+		}
+	}
+	for (int i = 0; i < NF; i++) {
+		if (E->pvq_prev_uv_flag || par[i].uv_flag) {
+			deltp[i] = 0;
+			deltw[i] = 0;
+		} else {
+			deltp[i] = sub(tgt[i], E->pvq_prev_pitch);
+			deltw[i] = 1;
+		}
+		E->pvq_prev_pitch = tgt[i];
+		E->pvq_prev_uv_flag = par[i].uv_flag;
+	}
+	if (cnt == 0) {
+		for (int i = 0; i < NF; i++)
+			par[i].pitch = 50;	/* UV_PITCH (Q0, as the reference) */
+		E->pvq_prev_qpitch = LOG_UV_PITCH_Q12;
+	} else if (cnt == 1) {
+		for (int i = 0; i < NF; i++) {
+			if (!par[i].uv_flag) {
+				quant_u(&tgt[i], &q->pitch_index, 5329, 9028, 98, 25088, true, 7);
+				par[i].pitch = quant_u_dec(q->pitch_index, 5329, 9028, 25088, 7);
+			} else {
+				par[i].pitch = LOG_UV_PITCH_Q12;
+			}
+		}
+		E->pvq_prev_qpitch = par[NF - 1].pitch;
+		for (int i = 0; i < NF; i++)
+			par[i].pitch = pow10_fxp(par[i].pitch, 7);
+	} else {
+		const int16_t *cb;
+		int size;
+		if (cnt == NF) {
+			cb = TB(pitch_vq_cb_vvv);
+			size = 2048;
+		} else {
+			cb = TB(pitch_vq_cb_uvv);
+			size = 512;
+		}
+		wvq1(tgt, wt, cb, NF, size, il, dl, PITCH_VQ_CAND);
+		Word16 k = 0;
+		for (int i = 0; i < PITCH_VQ_CAND; i++) {
+			Word16 t2 = extract_l(L_shr(L_mult(il[i], NF), 1));
+			dcb[k] = sub(cb[t2], E->pvq_prev_qpitch);
+			v_copy(&dcb[k + 1], &cb[t2 + 1], NF - 1);
+			v_sub(&dcb[k + 1], &cb[t2], NF - 1);
+			k = add(k, NF);
+		}
+		int16_t pi = wvq2(deltp, deltw, dcb, NF, il, dl, PITCH_VQ_CAND);
+		if (par[NF - 1].uv_flag)
+			E->pvq_prev_qpitch = LOG_UV_PITCH_Q12;
+		else
+			E->pvq_prev_qpitch = cb[pi * NF + NF - 1];
+		for (int i = 0; i < NF; i++)
+			par[i].pitch = par[i].uv_flag ? (int16_t) UV_PITCH_Q7
+						      : pow10_fxp(cb[pi * NF + i], 7);
+		q->pitch_index = pi;
+	}
+}
+
+/* gain_vq :368 -- 1024 x 6 full search with the reference's early skip */
+MD void gain_vq(EncState *E, MelpParam *par)
+{
+	const int16_t *cb = TB(gain_vq_cb);
+	int16_t tg[NF * NUM_GAINFR];
+	for (int i = 0; i < NF; i++)
+		v_copy(&tg[i * NUM_GAINFR], par[i].gain, NUM_GAINFR);
+	Word32 minErr = LW_MAX_;
+	int16_t idx = 0;
+	Word16 b = 0;
+	for (int i = 0; i < 1024; i++) {
+		Word16 t = sub(tg[0], cb[b]);
+		Word32 err = L_add(0, L_shr(L_mult(t, t), 3));
+		if (err < minErr) {
+			for (int j = 1; j < NF * NUM_GAINFR; j++) {
+				t = sub(tg[j], cb[b + j]);
+				err = L_add(err, L_shr(L_mult(t, t), 3));
+			}
+			if (err < minErr) {
+				minErr = err;
+				idx = (int16_t) i;
+			}
+		}
+		b = add(b, NF * NUM_GAINFR);
+	}
+	b = extract_l(L_shr(L_mult(idx, NF * NUM_GAINFR), 1));
+	for (int i = 0; i < NF; i++) {
+		v_copy(par[i].gain, &cb[b], NUM_GAINFR);
+		b = add(b, NUM_GAINFR);
+	}
+	E->qpar.gain_index[0] = idx;
+}
+
+/* quant_bp :447 */
+MD void quant_bp(EncState *E, MelpParam *par)
+{
+	for (int i = 0; i < NF; i++) {
+		par[i].uv_flag = q_bpvc(par[i].bpvc, &E->qpar.bpvc_index[i], NUM_BANDS);
+		E->qpar.bpvc_index[i] = TB(bp_index_map)[E->qpar.bpvc_index[i]];
+	}
+}
+
+/* ------------------------------------------------------------------ */
+/* LSF MSVQ, melpe/qnt12.c:482-1138                                    */
+/* ------------------------------------------------------------------ */
+
+/* WeightedMSE :669 -- early exit after half the dimensions */
+MD Word16 WeightedMSE(int n, const int16_t *w, const int16_t *x, const int16_t *tgt,
+		      Word16 max_dmin)
+{
+	Word32 d = 0;
+	Word16 half = shr((Word16) n, 1);
+	for (int i = 0; i < half; i++) {
+		Word16 t = sub(x[i], tgt[i]);
+		d = L_mac(d, w[i], mult(t, t));
+	}
+	if (r_ound(d) >= max_dmin)
+		return SW_MAX_;
+	for (int i = half; i < n; i++) {
+		Word16 t = sub(x[i], tgt[i]);
+		d = L_mac(d, w[i], mult(t, t));
+	}
+	return r_ound(d);
+}
+
+/* InsertCand :735 -- ordered insert into the M-best list */
+MD Word16 InsertCand(int c1, int s1, int16_t *dMin, Word16 dist, int16_t entry,
+		     int16_t (*nextIndex)[LSP_VQ_STAGES], int16_t (*index)[LSP_VQ_STAGES])
+{
+	int i = 0;
+	while (i < LSP_VQ_CAND && dist > dMin[i])
+		i++;
+	for (int j = LSP_VQ_CAND - 1; j > i; j--) {
+		dMin[j] = dMin[j - 1];
+		v_copy(nextIndex[j], nextIndex[j - 1], s1 + 1);
+	}
+	dMin[i] = dist;
+	v_copy(nextIndex[i], index[c1], s1);
+	nextIndex[i][s1] = entry;
+	return dMin[LSP_VQ_CAND - 1];
+}
+
+/* lspVQ :482 -- M-best multistage search; qout receives the ncPrev best
+ * reconstructions (dim each), cb_index their stage indices (tos each) */
+MD void lspVQ(const int16_t *target, const int16_t *weight, int16_t *qout, const int16_t *cb,
+	      int tos, const int16_t *cb_size, int16_t *cb_index, int dim, bool flag)
+{
+	int16_t index[LSP_VQ_CAND][LSP_VQ_STAGES], nextIndex[LSP_VQ_CAND][LSP_VQ_STAGES];
+	int16_t cand[LSP_VQ_CAND][2 * LPC_ORD], ct[2 * LPC_ORD], dMin[LSP_VQ_CAND];
+	for (int i = 0; i < LSP_VQ_CAND; i++) {
+		v_zero(cand[i], dim);
+		v_zero(index[i], LSP_VQ_STAGES);
+		v_zero(nextIndex[i], LSP_VQ_STAGES);
+	}
+	int ncPrev = 1;
+	const int16_t *cbp = cb;
+	Word16 off = 0;
+	for (int s1 = 0; s1 < tos; s1++) {
+		v_set(dMin, SW_MAX_, LSP_VQ_CAND);
+		Word16 maxd = SW_MAX_;
+		for (int c1 = 0; c1 < ncPrev; c1++) {
+			off = 0;
+			v_copy(ct, target, dim);
+			v_sub(ct, cand[c1], dim);
+			for (int e = 0; e < cb_size[s1]; e++) {
+				Word16 d = WeightedMSE(dim, weight, cbp + off, ct, maxd);
+				if (d < maxd)
+					maxd = InsertCand(c1, s1, dMin, d, (int16_t) e, nextIndex, index);
+				off = add(off, (Word16) dim);
+			}
+		}
+		if (!flag && s1 == tos - 1) {
+			ncPrev = 1;
+		} else {
+			Word16 t1 = extract_l(L_shr(L_mult((Word16) ncPrev, cb_size[s1]), 1));
+			Word16 t2 = (s1 == tos - 1) ? LSP_INP_CAND : LSP_VQ_CAND;
+			ncPrev = t1 < t2 ? t1 : t2;
+		}
+		for (int c1 = 0; c1 < ncPrev; c1++) {
+			v_zero(cand[c1], dim);
+			const int16_t *p2 = cb;
+			v_copy(index[c1], nextIndex[c1], s1 + 1);
+			for (int i = 0; i <= s1; i++) {
+				Word16 o = extract_l(L_shr(L_mult(index[c1][i], (Word16) dim), 1));
+				v_add(cand[c1], p2 + o, dim);
+				p2 += extract_l(L_shr(L_mult(cb_size[i], (Word16) dim), 1));
+			}
+		}
+		cbp += off;
+	}
+	for (int i = 0; i < ncPrev; i++) {
+		v_copy(&cb_index[i * tos], index[i], tos);
+		v_copy(&qout[i * dim], cand[i], dim);
+	}
+}
+
+/* lspStable :805 (the reference also prints a warning when unstable) */
+MD bool lspStable(int16_t *lsp, int order)
+{
+	if (lsp[0] < 52)
+		lsp[0] = 52;
+	for (int i = 0; i < order - 1; i++) {
+		Word16 t = add(lsp[i], 205);
+		if (lsp[i + 1] < t)
+			lsp[i + 1] = t;
+	}
+	if (lsp[order - 1] > 32702)
+		lsp[order - 1] = 32702;
+	return !(lsp[order - 1] < lsp[order - 2]);
+}
+
+MD void lspSort(int16_t *lsp, int order)	/* :865 */
+{
+	for (int j = 1; j < order; j++) {
+		int16_t t = lsp[j];
+		int i = j - 1;
+		while (i >= 0 && lsp[i] > t) {
+			lsp[i + 1] = lsp[i];
+			i--;
+		}
+		lsp[i + 1] = t;
+	}
+}
+
+/* interpolation-error term of lsf_vq (qnt12.c:1019-1063): weighted square of
+ * a Q15-scaled 32-bit difference through its normalised mantissa */
+MD Word32 lsf_werr(Word32 acc, Word16 w)
+{
+	Word16 t1 = norm_l(acc);
+	Word16 t2 = extract_h(L_shl(acc, t1));
+	if (t2 == SW_MIN_)
+		t2 = -32767;
+	t2 = mult(t2, t2);
+	Word32 r = L_mult(t2, w);
+	t1 = shl(sub(1, t1), 1);
+	return L_shl(r, sub(t1, 3));
+}
+
+/* lsf_vq :895 */
+MD void lsf_vq(EncState *E, MelpParam *par)
+{
+	QuantParam *q = &E->qpar;
+	const int16_t melp_cb_size[4] = {256, 64, 32, 32};
+	const int16_t res_cb_size[4] = {256, 64, 64, 64};
+	const int16_t uv_cb_size[1] = {512};
+	const int16_t *cb_uv = TB(lsp_uv_9), *cb_v = TB(lsp_v_256x64x32x32);
+	int16_t lpc[LPC_ORD], wgt[NF][LPC_ORD], mwgt[2 * LPC_ORD];
+	int16_t best0[LPC_ORD], best1[LPC_ORD], res[2 * LPC_ORD];
+	int16_t lcand[LSP_INP_CAND][LPC_ORD], lidx[LSP_INP_CAND * LSP_VQ_STAGES];
+	int16_t il0[LPC_ORD], il1[LPC_ORD];
+	int16_t *lsp[NF];
+	if (!E->lsf_started) {
+		Word16 t2 = shl(LPC_ORD, 10), t1 = 819;
+		for (int i = 0; i < LPC_ORD; i++) {
+			E->qplsp[i] = divide_s(t1, t2);
+			t1 = add(t1, 819);
+		}
+		E->lsf_started = 1;
+	}
+	for (int i = 0; i < NF; i++) {
+		lsp[i] = par[i].lsf;
+		lpc_lsp2pred(lsp[i], lpc, LPC_ORD);
+		vq_lspw(wgt[i], lsp[i], lpc, LPC_ORD);
+	}
+	Word16 uvc = 0;
+	for (int i = 0; i < NF; i++) {
+		uvc = shl(uvc, 1);
+		if (par[i].uv_flag) {
+			uvc |= 1;
+			if (i == 0)
+				v_scale(wgt[0], 6554, LPC_ORD);
+			else if (i == 1)
+				v_scale(wgt[1], 6554, LPC_ORD);
+		}
+	}
+	if (uvc == 7 || uvc == 6 || uvc == 5 || uvc == 3) {
+		/* at most one voiced frame: each frame on its own */
+		for (int i = 0; i < NF; i++) {
+			bool uv = (uvc >> (NF - 1 - i)) & 1;
+			if (uv)
+				lspVQ(lsp[i], wgt[i], lsp[i], cb_uv, 1, uv_cb_size, q->lsf_index[i],
+				      LPC_ORD, false);
+			else
+				lspVQ(lsp[i], wgt[i], lsp[i], cb_v, 4, melp_cb_size, q->lsf_index[i],
+				      LPC_ORD, false);
+		}
+	} else {
+		int tos;
+		if (uvc == 1) {
+			tos = 1;
+			lspVQ(lsp[2], wgt[2], lcand[0], cb_uv, tos, uv_cb_size, lidx, LPC_ORD, true);
+		} else {
+			tos = 4;
+			lspVQ(lsp[2], wgt[2], lcand[0], cb_v, tos, melp_cb_size, lidx, LPC_ORD, true);
+		}
+		Word32 minErr = LW_MAX_;
+		int cand = 0;
+		int16_t inp = 0;
+		const int16_t *ic = TB(inpCoef);
+		for (int k = 0; k < LSP_INP_CAND; k++)
+			for (int i = 0; i < 16; i++) {
+				Word32 err = 0;
+				for (int j = 0; j < LPC_ORD; j++) {
+					Word16 f = ic[i * 20 + j];
+					Word32 acc = L_mult(f, E->qplsp[j]);
+					acc = L_mac(acc, sub(16384, f), lcand[k][j]);
+					il0[j] = extract_h(L_shl(acc, 1));
+					acc = L_sub(acc, L_shl(L_deposit_l(lsp[0][j]), 15));
+					f = ic[i * 20 + j + LPC_ORD];
+					Word32 bcc = L_mult(f, E->qplsp[j]);
+					bcc = L_mac(bcc, sub(16384, f), lcand[k][j]);
+					il1[j] = extract_h(L_shl(bcc, 1));
+					bcc = L_sub(bcc, L_shl(L_deposit_l(lsp[1][j]), 15));
+					err = L_add(err, lsf_werr(acc, wgt[0][j]));
+					err = L_add(err, lsf_werr(bcc, wgt[1][j]));
+					acc = L_shl(L_deposit_l(lsp[2][j]), 15);
+					acc = L_sub(acc, L_shl(L_deposit_l(lcand[k][j]), 15));
+					err = L_add(err, lsf_werr(acc, wgt[2][j]));
+				}
+				if (err < minErr) {
+					minErr = err;
+					cand = k;
+					inp = (int16_t) i;
+					v_copy(best0, il0, LPC_ORD);
+					v_copy(best1, il1, LPC_ORD);
+				}
+			}
+		v_copy(lsp[2], lcand[cand], LPC_ORD);
+		v_copy(q->lsf_index[0], &lidx[cand * tos], tos);
+		q->lsf_index[1][0] = inp;
+		for (int i = 0; i < LPC_ORD; i++) {
+			res[i] = shl(sub(lsp[0][i], best0[i]), 2);
+			res[i + LPC_ORD] = shl(sub(lsp[1][i], best1[i]), 2);
+		}
+		v_copy(mwgt, wgt[0], LPC_ORD);
+		v_copy(mwgt + LPC_ORD, wgt[1], LPC_ORD);
+		lspVQ(res, mwgt, res, TB(res256x64x64x64), uvc == 1 ? 4 : 2, res_cb_size,
+		      q->lsf_index[2], 2 * LPC_ORD, false);
+		for (int i = 0; i < LPC_ORD; i++) {
+			lsp[0][i] = add(shr(res[i], 2), best0[i]);
+			lsp[1][i] = add(shr(res[i + LPC_ORD], 2), best1[i]);
+		}
+	}
+	lspStable(lsp[0], LPC_ORD);
+	lspStable(lsp[1], LPC_ORD);
+	if (!lspStable(lsp[2], LPC_ORD))
+		lspSort(lsp[2], LPC_ORD);
+	v_copy(E->qplsp, lsp[2], LPC_ORD);
+}
+
+/* quant_jitter :1198 */
+MD void quant_jitter(EncState *E, MelpParam *par)
+{
+	Word16 uvc = 0;
+	int16_t jit[NF];
+	for (int i = 0; i < NF; i++) {
+		uvc = shl(uvc, 1);
+		uvc |= par[i].uv_flag;
+		jit[i] = par[i].jitter;
+	}
+	bool flag = false;
+	switch (uvc) {
+	case 6:
+		flag = jit[2] == MAX_JITTER_Q15;
+		break;
+	case 5:
+	case 4:
+	case 1:
+		flag = jit[1] == MAX_JITTER_Q15;
+		break;
+	case 3:
+		flag = jit[0] == MAX_JITTER_Q15;
+		break;
+	case 0: {
+		int c = 0;
+		for (int i = 0; i < NF; i++)
+			if (jit[i] == MAX_JITTER_Q15)
+				c++;
+		flag = c >= 2;
+		break;
+	}
+	default:
+		break;
+	}
+	for (int i = 0; i < NF; i++)
+		jit[i] = par[i].uv_flag ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;
+	if (flag && uvc == 0)
+		jit[0] = jit[1] = jit[2] = MAX_JITTER_Q15;
+	for (int i = 0; i < NF; i++)
+		par[i].jitter = jit[i];
+	E->qpar.jit_index[0] = flag;
+}
+
+/* quant_fsmag :1277 */
+MD void quant_fsmag(EncState *E, MelpParam *par)
+{
+	int16_t qmag[NUM_HARM];
+	int cnt = 0, last = -1;
+	for (int i = 0; i < NF; i++) {
+		if (par[i].uv_flag) {
+			v_set(par[i].fs_mag, 8192, NUM_HARM);
+		} else {
+			window_Q(par[i].fs_mag, g_der.w_fs, par[i].fs_mag, NUM_HARM, 14);
+			last = i;
+			cnt++;
+		}
+	}
+	if (cnt > 0)
+		vq_enc(TB(fsvq_cb), par[last].fs_mag, 256, NUM_HARM, qmag, &E->qpar.fs_index);
+	if (cnt > 1) {
+		if (E->fsm_prev_uv || par[0].uv_flag) {
+			for (int i = 0; i <= last; i++)
+				if (!par[i].uv_flag)
+					v_copy(par[i].fs_mag, qmag, NUM_HARM);
+		} else if (par[1].uv_flag) {
+			v_copy(par[0].fs_mag, E->fsm_prev_fsmag, NUM_HARM);
+			v_copy(par[last].fs_mag, qmag, NUM_HARM);
+		} else if (par[2].uv_flag) {
+			v_copy(par[1].fs_mag, qmag, NUM_HARM);
+			for (int i = 0; i < NUM_HARM; i++)
+				par[0].fs_mag[i] = add(shr(qmag[i], 1), shr(E->fsm_prev_fsmag[i], 1));
+		} else {
+			v_copy(par[2].fs_mag, qmag, NUM_HARM);
+			for (int i = 0; i < NUM_HARM; i++) {
+				Word16 p = E->fsm_prev_fsmag[i], v = qmag[i];
+				par[0].fs_mag[i] = add(mult(p, 21845), mult(v, 10923));
+				par[1].fs_mag[i] = add(mult(p, 10923), mult(v, 21845));
+			}
+		}
+	} else if (cnt == 1) {
+		v_copy(par[last].fs_mag, qmag, NUM_HARM);
+	}
+	E->fsm_prev_uv = par[NF - 1].uv_flag;
+	if (E->fsm_prev_uv)
+		v_set(E->fsm_prev_fsmag, 8192, NUM_HARM);
+	else
+		v_copy(E->fsm_prev_fsmag, par[NF - 1].fs_mag, NUM_HARM);
+}
+
+/* ------------------------------------------------------------------ */
+/* FEC + channel write, melpe/fec_code.c, melpe/melp_chn.c             */
+/* ------------------------------------------------------------------ */
+
+MD Word16 binprod(const int16_t *x, const int16_t *y, int n)	/* fec_code.c binprod_int */
+{
+	Word16 v = 0;
+	for (int i = 0; i < n; i++)
+		v ^= x[i] & y[i];
+	return v;
+}
+
+/* vgetbits: dest[n-1..0] <- bits bit_pos..bit_pos-n+1 of source */
+MD void vgetbits(int16_t *dest, Word16 src, Word16 bit_pos, Word16 n)
+{
+	if (n >= 0 && bit_pos >= sub(n, 1)) {
+		src = shr(src, (Word16) (bit_pos - n + 1));
+		for (int i = sub(n, 1); i >= 0; i--) {
+			dest[i] = (int16_t) (src & 1);
+			src = shr(src, 1);
+		}
+	}
+}
+
+/* vsetbits: bits bit_pos.. of *dest <- source[0..n-1] */
+MD void vsetbits(int16_t *dest, Word16 bit_pos, Word16 n, const int16_t *src)
+{
+	if (n >= 0 && bit_pos >= n - 1)
+		for (int i = 0, j = bit_pos; i < n; i++, j--) {
+			*dest &= ~(1 << j);
+			*dest |= src[i] << j;
+		}
+}
+
+MD void sbc_enc(int16_t *x, int n, int k, const int16_t *pmat)
+{
+	for (int i = k; i < n; i++, pmat += k)
+		x[i] = binprod(x, pmat, k);
+}
+
+MD void crc4_enc(int16_t *bit, int nbits)
+{
+	int16_t d[4] = {0, 0, 0, 0};
+	int ll = nbits + 4;
+	for (int i = 1; i <= nbits; i++) {
+		int16_t x = (int16_t) (d[3] ^ bit[ll - i]);
+		d[3] = d[2];
+		d[2] = d[1];
+		d[1] = (int16_t) (x ^ d[0]);
+		d[0] = x;
+	}
+	v_copy(bit, d, 4);
+}
+
+/* low_rate_fec_code :955 -- protects all-unvoiced superframes */
+MD void low_rate_fec_code(QuantParam *q)
+{
+	if (!(q->uv_flag[0] && q->uv_flag[1] && q->uv_flag[2]))
+		return;
+	int16_t c84[8], c74[7], c13[13];
+	const int16_t *p84 = TB(pmat84), *p74 = TB(pmat74);
+	vgetbits(c84, q->gain_index[0], 9, 4);
+	sbc_enc(c84, 8, 4, p84);
+	vsetbits(&q->fs_index, 7, 4, &c84[4]);
+	vgetbits(c84, q->gain_index[0], 5, 4);
+	sbc_enc(c84, 8, 4, p84);
+	vsetbits(&q->fs_index, 3, 4, &c84[4]);
+	vgetbits(c74, q->gain_index[0], 1, 2);
+	c74[2] = c74[3] = 0;
+	sbc_enc(c74, 7, 4, p74);
+	vsetbits(&q->bpvc_index[0], 1, 2, &c74[4]);
+	vsetbits(&q->jit_index[0], 0, 1, &c74[6]);
+	for (int f = 0; f < NF; f++) {
+		vgetbits(&c13[4], q->lsf_index[f][0], 8, 9);
+		crc4_enc(c13, 9);
+		vsetbits(&q->lsf_index[f][1], 3, 4, &c13[0]);
+	}
+}
+
+MD Word16 parity(Word16 x, int len)	/* melp_chn.c:1367 */
+{
+	Word16 p = 0;
+	for (int i = 0; i < len; i++) {
+		p ^= x & 1;
+		x >>= 1;
+	}
+	return p;
+}
+
+/* low_rate_chn_write :262 -- 81-bit superframe into chbuf (11 bytes) */
+MD void low_rate_chn_write(EncState *E)
+{
+	QuantParam *q = &E->qpar;
+	unsigned char bb[81];
+	BitCursor bc = {bb, 0};
+	low_rate_fec_code(q);
+	E->sync_bit = sub(1, E->sync_bit);
+	pack_code(E->sync_bit, &bc, 1, 1);
+	int cnt = 0;
+	for (int i = 0; i < NF; i++)
+		if (!q->uv_flag[i])
+			cnt++;
+	Word16 uv_index = 0, bp1 = 0, bp2 = 0, lsp_prot = 0;
+	if (cnt <= 1) {
+		if (!q->uv_flag[0])
+			bp2 = 3;
+		else if (!q->uv_flag[1])
+			bp2 = 2;
+		else if (!q->uv_flag[2])
+			bp2 = 1;
+		if (bp2 == 0)
+			q->pitch_index = 0;	/* UV_PIND */
+		else
+			q->pitch_index = TB(low_rate_pitch_enc)[bp2 * 99 + q->pitch_index];
+	} else if (cnt == 2) {
+		if (q->uv_flag[0]) {
+			uv_index = 4;
+			bp1 = 3;
+		} else if (q->uv_flag[1]) {
+			uv_index = 2;
+			bp1 = 2;
+		} else if (q->uv_flag[2]) {
+			uv_index = 1;
+			bp1 = 1;
+			lsp_prot = 7;
+		}
+	} else {
+		uv_index = (int16_t) (q->pitch_index / 512);
+		q->pitch_index = sub(q->pitch_index, (int16_t) (uv_index * 512));
+		uv_index = TB(vvv_index_map)[uv_index];
+	}
+	pack_code(uv_index, &bc, 3, 1);
+	pack_code(parity(uv_index, 3), &bc, 1, 1);
+	pack_code(q->pitch_index, &bc, 9, 1);
+	const int16_t u1 = q->uv_flag[0], u2 = q->uv_flag[1], cu = q->uv_flag[2];
+	int16_t (*L)[MAX_LSF_STAGE] = q->lsf_index;
+	if (u1 == 1 && u2 == 1 && cu == 1) {
+		pack_code(L[0][0], &bc, 9, 1);
+		pack_code(L[1][0], &bc, 9, 1);
+		pack_code(L[2][0], &bc, 9, 1);
+		pack_code(L[0][1], &bc, 4, 1);
+		pack_code(L[1][1], &bc, 4, 1);
+		pack_code(L[2][1], &bc, 4, 1);
+		pack_code(lsp_prot, &bc, 3, 1);
+	} else if (u1 == 1 && u2 == 1 && cu != 1) {
+		pack_code(L[0][0], &bc, 9, 1);
+		pack_code(L[1][0], &bc, 9, 1);
+		pack_code(L[2][0], &bc, 8, 1);
+		pack_code(L[2][1], &bc, 6, 1);
+		pack_code(L[2][2], &bc, 5, 1);
+		pack_code(L[2][3], &bc, 5, 1);
+	} else if (u1 == 1 && u2 != 1 && cu == 1) {
+		pack_code(L[0][0], &bc, 9, 1);
+		pack_code(L[1][0], &bc, 8, 1);
+		pack_code(L[1][1], &bc, 6, 1);
+		pack_code(L[1][2], &bc, 5, 1);
+		pack_code(L[1][3], &bc, 5, 1);
+		pack_code(L[2][0], &bc, 9, 1);
+	} else if (u1 != 1 && u2 == 1 && cu == 1) {
+		pack_code(L[0][0], &bc, 8, 1);
+		pack_code(L[0][1], &bc, 6, 1);
+		pack_code(L[0][2], &bc, 5, 1);
+		pack_code(L[0][3], &bc, 5, 1);
+		pack_code(L[1][0], &bc, 9, 1);
+		pack_code(L[2][0], &bc, 9, 1);
+	} else {
+		const bool vvu = (u1 != 1 && u2 != 1 && cu == 1);
+		if (vvu) {
+			pack_code(L[0][0], &bc, 9, 1);
+		} else {
+			pack_code(L[0][0], &bc, 8, 1);
+			pack_code(L[0][1], &bc, 6, 1);
+			pack_code(L[0][2], &bc, 5, 1);
+			pack_code(L[0][3], &bc, 5, 1);
+		}
+		pack_code(L[1][0], &bc, 4, 1);
+		if (vvu) {
+			pack_code(L[2][0], &bc, 8, 1);
+			pack_code(L[2][1], &bc, 6, 1);
+			pack_code(L[2][2], &bc, 6, 1);
+			pack_code(L[2][3], &bc, 6, 1);
+			pack_code(lsp_prot, &bc, 3, 1);
+		} else {
+			pack_code(L[2][0], &bc, 8, 1);
+			pack_code(L[2][1], &bc, 6, 1);
+		}
+	}
+	pack_code(q->gain_index[0], &bc, 10, 1);
+	for (int i = 0; i < NF; i++)
+		if (!q->uv_flag[i])
+			pack_code(q->bpvc_index[i], &bc, 2, 1);
+	if (cnt == 2) {
+		pack_code(bp1, &bc, 2, 1);
+	} else if (cnt == 1) {
+		pack_code(bp2, &bc, 2, 1);
+		pack_code(bp1, &bc, 2, 1);
+	} else if (cnt == 0) {
+		pack_code(q->bpvc_index[0], &bc, 2, 1);
+		pack_code(bp2, &bc, 2, 1);
+		pack_code(bp1, &bc, 2, 1);
+	}
+	pack_code(q->fs_index, &bc, 8, 1);
+	pack_code(q->jit_index[0], &bc, 1, 1);
+	/* chbuf: LSB first, chwordsize = 8 (melpe.c:79); the reference's
+	 * "|= 0x8000" on a byte (melp_chn.c:439) is a no-op */
+	BitCursor cc = {E->chbuf, 0};
+	for (int i = 0; i < 81; i++)
+		pack_code(bb[i], &cc, 1, 8);
+}
+
+}  // namespace mlp
+
+#endif

@@ -4,7 +4,8 @@
  * The reference keeps one codec instance per process in globals
  * (melpe/global.c:20-53) and ~90 function statics.
  * Here every one of them is a field of EncState / DecState, one instance per
- * channel in HBM; *_reset() gives the state of a fresh process.
+ * channel in HBM; enc_reset()/dec_reset() give the state of a fresh process
+ * (static initialisers + melp_ana_init / melp_syn_init, melpe/melpe.c:72-88).
  */
 #ifndef MELPE_STATE_H
 #define MELPE_STATE_H
@@ -13,17 +14,162 @@
 
 namespace mlp {
 
+/* codec geometry (melpe/sc1200.h:60-140) */
+#define FRAME 180
+#define NF 3
+#define BLOCK 540
+#define LPC_ORD 10
+#define NUM_HARM 10
+#define NUM_BANDS 5
+#define NUM_GAINFR 2
+#define PITCHMIN 20
+#define PITCHMAX 160
+#define PITCHMIN_Q7 2560
+#define PITCHMAX_Q7 20480
+#define PITCH_FR 321
+#define FRAME_BEG 70
+#define FRAME_END 250
+#define PITCH_BEG 90
+#define IN_BEG 360
+#define LPC_FRAME 200
+#define LPF_ORD 6
+#define DC_ORD 6
+#define BPF_ORD 6
+#define ENV_ORD 2
+#define PIT_COR_LEN 220
+#define PIT_SUBNUM 2
+#define PIT_SUBFRAME 90
+#define NODE 8
+#define TRACK_NUM 9
+#define CUR_TRACK 2
+#define MAXPITCH 147
+#define MINPITCH 20
+#define MAX_LSF_STAGE 4
+#define MSVQ_STAGES 4
+#define SIG_LENGTH (LPF_ORD + PITCH_FR)
+#define UV_PITCH_Q7 6400
+#define DEFAULT_PITCH_Q7 6400
+#define LOG_UV_PITCH_Q12 6963
+#define MAX_JITTER_Q15 8192
+#define BPTHRESH_Q14 9830
+#define VJIT_Q14 8192
+#define VMIN_Q14 13107
+#define VOICED 0
+#define UNVOICED 1
+#define TRANSITION 0
+#define SILENCE 3
+
+struct MelpParam {	/* struct melp_param, melpe/sc1200.h:233 */
+	int16_t pitch;	/* Q7 */
+	int16_t lsf[LPC_ORD];	/* Q15 */
+	int16_t gain[NUM_GAINFR];	/* Q8 */
+	int16_t jitter;	/* Q15 */
+	int16_t bpvc[NUM_BANDS];	/* Q14 */
+	int16_t uv_flag;
+	int16_t fs_mag[NUM_HARM];	/* Q13 */
+};
+
+struct QuantParam {	/* struct quant_param, melpe/sc1200.h:244 (no pointers) */
+	int16_t pitch_index;
+	int16_t lsf_index[NF][MAX_LSF_STAGE];
+	int16_t gain_index[NUM_GAINFR];
+	int16_t jit_index[NF];
+	int16_t bpvc_index[NF];
+	int16_t fs_index;
+	int16_t uv_flag[NF];
+	int16_t msvq_index[MSVQ_STAGES];
+	int16_t fsvq_index;
+};
+
+struct ClassParam {	/* classParam, melpe/cprv.h:40 */
+	int16_t classy, subEnergy, zeroCrosRate, peakiness, corx, pitch;
+};
+
+struct PitTrack {	/* pitTrackParam, melpe/cprv.h:34 */
+	int16_t pit[NODE], weight[NODE], cost[NODE];
+};
+
 struct EncState {
 	NppState npp;
+	/* melpe/global.c */
+	int16_t hpspeech[IN_BEG + BLOCK];
+	int16_t dcdelin[DC_ORD], dcdelout_hi[DC_ORD], dcdelout_lo[DC_ORD];
+	MelpParam par[NF];
+	QuantParam qpar;
+	int16_t voicedEn, silenceEn;
+	int32_t voicedCnt;
+	/* melpe/melp_ana.c */
+	int16_t sigbuf[SIG_LENGTH];
+	ClassParam classStat[TRACK_NUM];
+	PitTrack pitTrack[TRACK_NUM];
+	int16_t ana_started;
+	int16_t lpfsp_delin[LPF_ORD], lpfsp_delout[LPF_ORD];
+	int16_t pitch_avg, fpitch[2];
+	int16_t sc_prev_sbp3, sc_prev_uv, sc_prev_pitch;
+	/* melpe/classify.c */
+	int16_t cls_started;
+	int16_t bpfdel[BPF_ORD + BPF_ORD / 3];
+	int16_t back_sigbuf[PIT_COR_LEN - PIT_SUBFRAME];
+	/* melpe/pitch.c */
+	int16_t pauto_started;
+	int16_t lpbuf[PIT_COR_LEN], ivbuf[PIT_COR_LEN];
+	/* melpe/melp_sub.c (bpvc_ana) */
+	int16_t bp_started;
+	int16_t bpfsp[NUM_BANDS][PITCH_FR - FRAME];
+	int16_t bpfdelin[NUM_BANDS][BPF_ORD], bpfdelout[NUM_BANDS][BPF_ORD];
+	int16_t envdel[NUM_BANDS][ENV_ORD], envdel2[NUM_BANDS];
+	/* melpe/pit_lib.c */
+	int16_t pavg_started, good_pitch[NF];
+	int16_t pana_started;
+	int16_t lpres_delin[LPF_ORD], lpres_delout[LPF_ORD];
+	int16_t pa_sigbuf[SIG_LENGTH];
+	/* melpe/qnt12.c */
+	int16_t pvq_prev_uv_flag, pvq_prev_pitch, pvq_prev_qpitch;
+	int16_t lsf_started, qplsp[LPC_ORD];
+	int16_t fsm_prev_uv, fsm_prev_fsmag[NUM_HARM];
+	/* melpe/melp_chn.c */
+	int16_t sync_bit;
+	int16_t pad_;
+	uint8_t chbuf[12];
 };
 
 struct DecState {
 	int16_t dummy;
 };
 
+/* melp_ana_init, melpe/melp_ana.c:475-506 (the part melpe_i re-runs) */
+MD void enc_melpe_i(EncState *e)
+{
+	for (int i = 0; i < IN_BEG + BLOCK; i++)
+		e->hpspeech[i] = 0;
+	for (int i = 0; i < TRACK_NUM; i++) {
+		for (int k = 0; k < NODE; k++) {
+			e->pitTrack[i].pit[k] = 50;
+			e->pitTrack[i].weight[k] = SW_MAX_;
+		}
+		e->classStat[i].classy = UNVOICED;
+		e->classStat[i].subEnergy = 5734;
+		e->classStat[i].zeroCrosRate = 16384;
+		e->classStat[i].peakiness = 2048;
+		e->classStat[i].corx = 6554;
+	}
+}
+
+/* fresh-process state: zero .bss, the reference's static initialisers, then
+ * melpe_i() */
 MD void enc_reset(EncState *e)
 {
+	int16_t *p = (int16_t *) e;
+	for (unsigned i = 0; i < sizeof(EncState) / 2; i++)
+		p[i] = 0;
 	npp_reset(&e->npp);
+	e->sc_prev_uv = UNVOICED;	/* melp_ana.c:525-527 */
+	e->sc_prev_pitch = 6400;
+	e->pvq_prev_uv_flag = 1;	/* qnt12.c:78-80 */
+	e->pvq_prev_pitch = LOG_UV_PITCH_Q12;
+	e->pvq_prev_qpitch = LOG_UV_PITCH_Q12;
+	e->fsm_prev_uv = 1;	/* qnt12.c:1279 */
+	enc_melpe_i(e);
 }
 
 MD void dec_reset(DecState *d)
