@@ -119,6 +119,12 @@ class MelpeEngine:
         _check(self.lib.melpe_encode_host(self.h, _ptr(bits), _ptr(sp), _ptr(m)))
         return bits
 
+    def _raw_encode(self, sp, bits, active):
+        """encode with caller-provided output bits (kept for inactive lanes)"""
+        m = self._mask(active)
+        _check(self.lib.melpe_encode_host(self.h, _ptr(bits), _ptr(sp), _ptr(m)))
+        return bits
+
     def decode(self, bits, active=None):
         """melpe_s on every channel. bits: uint8 [C, 11] -> int16 [C, 540]."""
         bits = np.ascontiguousarray(bits, dtype=np.uint8)

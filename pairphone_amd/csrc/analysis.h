@@ -31,7 +31,7 @@ MD void dc_rmv(const int16_t *in, int16_t *out, int16_t *din, int16_t *dhi,
 }
 
 /* remove_dc :261 */
-MD void remove_dc(const int16_t *in, int16_t *out, int16_t len)
+MN void remove_dc(const int16_t *in, int16_t *out, int16_t len)
 {
 	Word16 up = sub(15, norm_s(len));
 	Word16 pdown = shl(1, sub(up, 1));
@@ -46,7 +46,7 @@ MD void remove_dc(const int16_t *in, int16_t *out, int16_t len)
 }
 
 /* gain_ana :311 -- pitch-adaptive RMS in dB (Q8) */
-MD Word16 gain_ana(const int16_t *sig, Word16 pitch, Word16 minlen, Word16 maxlen)
+MN Word16 gain_ana(const int16_t *sig, Word16 pitch, Word16 minlen, Word16 maxlen)
 {
 	int16_t tb[PITCHMAX * 2 + 8];
 	Word16 pq6 = shr(pitch, 1);
@@ -142,7 +142,7 @@ MD void q_bpvc_dec(int16_t *bpvc, Word16 idx, int16_t uv, int nb)
 /* ------------------------------------------------------------------ */
 
 /* f_pitch_scale :178 -- scale so the energy fits, returns the shift */
-MD Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
+MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 {
 	Word16 sc = 0;
 	Word32 sum = 0, margin = LW_MAX_;
@@ -169,7 +169,7 @@ MD Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 }
 
 /* find_pitch :240 -- normalised autocorrelation lag search, lags upper..lower */
-MD Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upper, Word16 len)
+MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upper, Word16 len)
 {
 	Word16 ip = lower;
 	Word32 max_num = 0, max_den = 1;
@@ -218,7 +218,7 @@ MD Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 }
 
 /* frac_pch :340 -- fractional pitch refinement and its correlation */
-MD Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 range,
+MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 range,
 		   Word16 pmin, Word16 pmax, Word16 pmin_q7, Word16 pmax_q7, Word16 lmin)
 {
 	Word16 len, cb, ip, corr;
@@ -311,7 +311,7 @@ MD Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 }
 
 /* double_ver :151 */
-MD void double_ver(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pmin, Word16 pmax,
+MN void double_ver(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pmin, Word16 pmax,
 		   Word16 pmin_q7, Word16 pmax_q7, Word16 lmin)
 {
 	Word16 m = 1;
@@ -327,7 +327,7 @@ MD void double_ver(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pmin,
 }
 
 /* double_chk :84 -- pitch-halving check over multiples 8..2 */
-MD Word16 double_chk(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pdouble,
+MN Word16 double_chk(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pdouble,
 		     Word16 pmin, Word16 pmax, Word16 pmin_q7, Word16 pmax_q7, Word16 lmin)
 {
 	pitch = frac_pch(sig, pcorr, pitch, 0, pmin, pmax, pmin_q7, pmax_q7, lmin);
@@ -377,7 +377,7 @@ MD Word16 p_avg_update(EncState *E, Word16 pitch, Word16 pcorr, Word16 pthresh)
 /* pitch_ana :571 -- final pitch from the lowpassed residual, with the
  * speech fallback; pa_sigbuf is persistent (its tail 323..326 can be read
  * stale by double_chk) */
-MD Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Word16 pest,
+MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Word16 pest,
 		    Word16 pavg, Word16 *pcorr2)
 {
 	int16_t *sb = E->pa_sigbuf;
@@ -432,7 +432,7 @@ MD Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 /* ------------------------------------------------------------------ */
 /* bpvc_ana, melpe/melp_sub.c:77 -- 5-band bandpass voicing           */
 /* ------------------------------------------------------------------ */
-MD void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
+MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
 		 Word16 *pitch)
 {
 	int16_t sb[BPF_ORD + PITCH_FR];
@@ -516,7 +516,7 @@ MD Word16 L_ratio(Word16 x, Word32 y)
 }
 
 /* updateEn :633 */
-MD Word16 updateEn(Word16 prev, Word16 ifact, Word16 curr)
+MN Word16 updateEn(Word16 prev, Word16 ifact, Word16 curr)
 {
 	Word16 t = sub(shr(curr, 1), shr(prev, 1));
 	if (t < negate(1024)) {
@@ -535,7 +535,7 @@ MD Word16 updateEn(Word16 prev, Word16 ifact, Word16 curr)
 }
 
 /* lpfilt :100 */
-MD void lpfilt(const int16_t *in, int16_t *lp, int len)
+MN void lpfilt(const int16_t *in, int16_t *lp, int len)
 {
 	const int16_t *lpar = TB(lpar);
 	v_copy(lp, &lp[len], PIT_COR_LEN - len);
@@ -548,7 +548,7 @@ MD void lpfilt(const int16_t *in, int16_t *lp, int len)
 }
 
 /* ivfilt :138 -- 2nd-order inverse filter from 40-bit autocorrelations */
-MD void ivfilt(int16_t *iv, const int16_t *lp, int len)
+MN void ivfilt(int16_t *iv, const int16_t *lp, int len)
 {
 	int16_t rc[3];
 	Word16 pc1, pc2;
@@ -593,7 +593,7 @@ MD void ivfilt(int16_t *iv, const int16_t *lp, int len)
 
 /* normalised 40-bit correlation step shared by corPeak and frac_cor:
  * combines r0/rk normalisation and returns A/sqrt(r0 rk) in Q15 */
-MD Word16 cor_gain(Word32 *Lr0, Word16 *r0s, Word16 rks, Word32 Lrk, Word40 A, bool clip_neg)
+MN Word16 cor_gain(Word32 *Lr0, Word16 *r0s, Word16 rks, Word32 Lrk, Word40 A, bool clip_neg)
 {
 	Word16 sh = add(*r0s, rks);
 	if (sh & 1) {
@@ -620,7 +620,7 @@ MD void norm40(Word40 *acc, Word16 *sh, Word32 *L)
 }
 
 /* corPeak :216 */
-MD void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
+MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 {
 	int16_t pb[PIT_COR_LEN];
 	int16_t index[MAXPITCH + 1], gp[MAXPITCH + 1], peak[MAXPITCH + 1], corx[NODE];
@@ -707,7 +707,7 @@ MD void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 }
 
 /* pitchAuto :63 */
-MD void pitchAuto(EncState *E, const int16_t *in, PitTrack *pt, ClassParam *cs)
+MN void pitchAuto(EncState *E, const int16_t *in, PitTrack *pt, ClassParam *cs)
 {
 	if (!E->pauto_started) {
 		v_zero(E->lpbuf, PIT_COR_LEN);
@@ -736,7 +736,7 @@ MD Word16 multiCheck(Word16 f1, Word16 f2)
 }
 
 /* trackPitch :471 */
-MD Word16 trackPitch(Word16 pitch, const PitTrack *pt)
+MN Word16 trackPitch(Word16 pitch, const PitTrack *pt)
 {
 	Word16 idx = -1, co = SW_MIN_;
 	for (int i = 0; i < NODE; i++) {
@@ -761,7 +761,7 @@ MD Word16 trackPitch(Word16 pitch, const PitTrack *pt)
 }
 
 /* pitLookahead :530 -- dynamic-programming look-ahead over the tracks */
-MD Word16 pitLookahead(PitTrack *pt, int num)
+MN Word16 pitLookahead(PitTrack *pt, int num)
 {
 	for (int i = 0; i < NODE; i++) {
 		Word32 s = L_sub(LW_MAX_, L_deposit_h(pt[num].weight[i]));
@@ -792,7 +792,7 @@ MD Word16 pitLookahead(PitTrack *pt, int num)
 /* ------------------------------------------------------------------ */
 
 /* zeroCrosCount :404 */
-MD Word16 zeroCrosCount(const int16_t *sp)
+MN Word16 zeroCrosCount(const int16_t *sp)
 {
 	int16_t d[PIT_SUBFRAME];
 	remove_dc(sp, d, PIT_SUBFRAME);
@@ -808,7 +808,7 @@ MD Word16 zeroCrosCount(const int16_t *sp)
 }
 
 /* bandEn :448 */
-MD Word16 bandEn(const int16_t *ac, int band)
+MN Word16 bandEn(const int16_t *ac, int band)
 {
 	const int16_t *cf = band == 0 ? TB(enlpf_coef) : TB(enhpf_coef);
 	Word32 e = 0;
@@ -822,7 +822,7 @@ MD Word16 bandEn(const int16_t *ac, int band)
 }
 
 /* frac_cor :504 -- best normalised correlation within +-5 of pitch */
-MD Word16 frac_cor(const int16_t *in, Word16 pitch)
+MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 {
 	Word16 lp = sub(pitch, 5), hp = add(pitch, 5);
 	if (lp < MINPITCH)
@@ -869,7 +869,7 @@ MD Word16 frac_cor(const int16_t *in, Word16 pitch)
 
 /* classify :92 -- silence/unvoiced/voiced/transition decision per 90-sample
  * subframe; cs[-1] is the previous subframe's parameters */
-MD void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *ac)
+MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *ac)
 {
 	int16_t sa[BPF_ORD / 3 + PIT_COR_LEN], sbb[BPF_ORD / 3 + PIT_COR_LEN];
 	int16_t insp[PIT_SUBFRAME];
@@ -1029,7 +1029,7 @@ MD void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *
 /* ------------------------------------------------------------------ */
 /* find_harm, melpe/fs_lib.c:62 -- Fourier magnitudes of the residual */
 /* ------------------------------------------------------------------ */
-MD void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, int len)
+MN void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, int len)
 {
 	int16_t hb[1024];
 	Word32 Lm[NUM_HARM];

@@ -75,7 +75,7 @@ MD void v_scale_shl(int16_t *a, int16_t sc, int n, int16_t sh)	/* :462 */
 }
 
 /* L_v_inner :293 -- sum of products, then shift to the output Q */
-MD Word32 L_v_inner(const int16_t *a, const int16_t *b, int n,
+MN Word32 L_v_inner(const int16_t *a, const int16_t *b, int n,
 		    int16_t qa, int16_t qb, int16_t qout)
 {
 	Word32 acc = 0;
@@ -85,7 +85,7 @@ MD Word32 L_v_inner(const int16_t *a, const int16_t *b, int n,
 }
 
 /* L_v_magsq :352 */
-MD Word32 L_v_magsq(const int16_t *a, int n, int16_t qa, int16_t qout)
+MN Word32 L_v_magsq(const int16_t *a, int n, int16_t qa, int16_t qout)
 {
 	Word32 acc = 0;
 	for (int i = 0; i < n; i++)
@@ -98,7 +98,7 @@ MD Word32 L_v_magsq(const int16_t *a, int n, int16_t qa, int16_t qout)
 /* ------------------------------------------------------------------ */
 
 /* L_divider2 :105 -- signed 32/32 -> Q15 division through divide_s */
-MD Word16 L_divider2(Word32 num, Word32 den, int16_t nsh, int16_t dsh)
+MN Word16 L_divider2(Word32 num, Word32 den, int16_t nsh, int16_t dsh)
 {
 	bool neg = (num < 0) != (den < 0);
 	int16_t k = 0;
@@ -114,7 +114,7 @@ MD Word16 L_divider2(Word32 num, Word32 den, int16_t nsh, int16_t dsh)
 }
 
 /* log10_fxp :169 */
-MD Word16 log10_fxp(Word16 x, Word16 Q)
+MN Word16 log10_fxp(Word16 x, Word16 Q)
 {
 	const int16_t *lt = TB(log_table);
 	Word16 sh = sub(7, Q);
@@ -135,7 +135,7 @@ MD Word16 log10_fxp(Word16 x, Word16 Q)
 }
 
 /* L_log10_fxp :242 */
-MD Word16 L_log10_fxp(Word32 x, Word16 Q)
+MN Word16 L_log10_fxp(Word32 x, Word16 Q)
 {
 	const int16_t *lt = TB(log_table);
 	Word16 sh = sub(23, Q);
@@ -156,7 +156,7 @@ MD Word16 L_log10_fxp(Word32 x, Word16 Q)
 }
 
 /* pow10_fxp :308 */
-MD Word16 pow10_fxp(Word16 x, Word16 Q)
+MN Word16 pow10_fxp(Word16 x, Word16 Q)
 {
 	const int16_t *tab = TB(pow10_table);
 	const int16_t *tens = TB(pow10_tens_table);
@@ -240,7 +240,7 @@ MD Word16 cos_fxp(Word16 x)
 }
 
 /* sqrt_Q15 :733 -- Taylor series square root of a Q15 value */
-MD Word16 sqrt_Q15(Word16 x)
+MN Word16 sqrt_Q15(Word16 x)
 {
 	if (x == 0)
 		return 0;
@@ -282,7 +282,7 @@ MD Word16 add_shr(Word16 a, Word16 b)	/* :781 */
 /* ------------------------------------------------------------------ */
 
 /* envelope :62 -- rectify + 2nd-order smoother; out[-1], out[-2] are history */
-MD void envelope(const int16_t *in, int16_t prev_in, int16_t *out, int n)
+MN void envelope(const int16_t *in, int16_t prev_in, int16_t *out, int n)
 {
 	Word16 pa = abs_s(prev_in);
 	for (int i = 0; i < n; i++) {
@@ -372,7 +372,7 @@ MD int16_t unpack_code(BitCursor *c, Word16 *code, int16_t nbits, int16_t wsize,
 }
 
 /* peakiness :200 -- L2/L1 ratio of a residual, Q11 */
-MD Word16 peakiness(const int16_t *in, int n)
+MN Word16 peakiness(const int16_t *in, int n)
 {
 	int16_t tb[512];
 	Word16 sc = 4;
@@ -403,7 +403,7 @@ MD Word16 peakiness(const int16_t *in, int n)
 }
 
 /* quant_u :259 -- uniform scalar quantiser, returns the index */
-MD void quant_u(int16_t *val, int16_t *idx, Word16 qmin, Word16 qmax,
+MN void quant_u(int16_t *val, int16_t *idx, Word16 qmin, Word16 qmax,
 		Word16 nlev, Word16 nlev_q, bool dbl, Word16 scale)
 {
 	Word16 step = divide_s(sub(qmax, qmin), nlev_q);
@@ -497,7 +497,7 @@ MD void window_Q(const int16_t *in, const int16_t *w, int16_t *out, int n, Word1
 
 /* zerflt :569 / zerflt_Q :591 -- FIR over in[-order..n-1], run backwards so
  * that in == out is allowed */
-MD void zerflt_Q(const int16_t *in, const int16_t *c, int16_t *out, int order,
+MN void zerflt_Q(const int16_t *in, const int16_t *c, int16_t *out, int order,
 		 int n, Word16 qc)
 {
 	Word16 sc = sub(15, qc);
@@ -515,7 +515,7 @@ MD void zerflt(const int16_t *in, const int16_t *c, int16_t *out, int order, int
 }
 
 /* iir_2nd_d :615 -- biquad with a double-precision (hi/lo) output memory */
-MD void iir_2nd_d(const int16_t *in, const int16_t *den, const int16_t *num,
+MN void iir_2nd_d(const int16_t *in, const int16_t *den, const int16_t *num,
 		  int16_t *out, int16_t *din, int16_t *dhi, int16_t *dlo, int n)
 {
 	for (int i = 0; i < n; i++) {
@@ -540,7 +540,7 @@ MD void iir_2nd_d(const int16_t *in, const int16_t *den, const int16_t *num,
 }
 
 /* iir_2nd_s :660 -- biquad, single precision memories */
-MD void iir_2nd_s(const int16_t *in, const int16_t *den, const int16_t *num,
+MN void iir_2nd_s(const int16_t *in, const int16_t *den, const int16_t *num,
 		  int16_t *out, int16_t *din, int16_t *dout, int n)
 {
 	for (int i = 0; i < n; i++) {
@@ -565,7 +565,7 @@ MD void iir_2nd_s(const int16_t *in, const int16_t *den, const int16_t *num,
 /* ------------------------------------------------------------------ */
 
 /* lpc_acor :93 -- windowed, normalised autocorrelation with lag window */
-MD void lpc_acor(const int16_t *in, const int16_t *win, int16_t *r,
+MN void lpc_acor(const int16_t *in, const int16_t *win, int16_t *r,
 		 Word16 hf_corr, int order, int n)
 {
 	const int16_t *lagw = TB(lagw_cof);
@@ -612,7 +612,7 @@ MD void lpc_acor(const int16_t *in, const int16_t *win, int16_t *r,
 }
 
 /* lpc_aejw :198 -- |A(e^jw)|^2 */
-MD Word32 lpc_aejw(const int16_t *lpc, Word16 omega, int order)
+MN Word32 lpc_aejw(const int16_t *lpc, Word16 omega, int order)
 {
 	if (order == 0)
 		return 524288L;
@@ -642,7 +642,7 @@ MD void lpc_bwex(const int16_t *lpc, int16_t *aw, Word16 gamma, int order)	/* :2
 }
 
 /* lpc_clmp :312 -- sort, then enforce a minimum LSF separation */
-MD void lpc_clmp(int16_t *lsp, Word16 delta, int order)
+MN void lpc_clmp(int16_t *lsp, Word16 delta, int order)
 {
 	bool unsorted = true;
 	for (int j = 0; unsorted && j < 10; j++) {
@@ -701,7 +701,7 @@ MD void lpc_refl2pred(const int16_t *refc, int16_t *lpc, int order)
 }
 
 /* lpc_schr :444 -- Schur recursion, returns the prediction error */
-MD Word16 lpc_schr(const int16_t *r, int16_t *lpc, int order)
+MN Word16 lpc_schr(const int16_t *r, int16_t *lpc, int order)
 {
 	Word32 y1[16], y2[17];
 	int16_t refc[16];
@@ -738,7 +738,7 @@ MD Word16 lpc_schr(const int16_t *r, int16_t *lpc, int order)
 }
 
 /* lsp_to_freq :626 -- root search of P/Q on a 257-point cosine grid */
-MD void lsp_to_freq(const int16_t *lsp, int16_t *freq, int order)
+MN void lsp_to_freq(const int16_t *lsp, int16_t *freq, int order)
 {
 	const int16_t *lc = g_der.lsp_cos;
 	/* default_w = divide_s(ONE_Q11, order << 10), :654-655 */
@@ -790,7 +790,7 @@ MD void lsp_to_freq(const int16_t *lsp, int16_t *freq, int order)
 }
 
 /* lpc_pred2lsp :566 */
-MD void lpc_pred2lsp(const int16_t *lpc, int16_t *lsf, int order)
+MN void lpc_pred2lsp(const int16_t *lpc, int16_t *lsf, int order)
 {
 	Word32 Lp[6], Lq[6];
 	int16_t pc[6], qc[6], pf[6], qf[6];
@@ -815,7 +815,7 @@ MD void lpc_pred2lsp(const int16_t *lpc, int16_t *lsf, int order)
 }
 
 /* lpc_pred2refl :751 -- returns the residual energy, *refc = first refl. */
-MD Word16 lpc_pred2refl(const int16_t *lpc, int16_t *refc, int order)
+MN Word16 lpc_pred2refl(const int16_t *lpc, int16_t *refc, int order)
 {
 	int16_t b[16], b1[16];
 	Word16 energy = SW_MAX_;
@@ -853,7 +853,7 @@ MD Word16 lpc_pred2refl(const int16_t *lpc, int16_t *refc, int order)
 }
 
 /* lpc_lsp2pred :827 -- LSF (Q15) to predictor (Q12); clamps lsf in place */
-MD void lpc_lsp2pred(int16_t *lsf, int16_t *lpc, int order)
+MN void lpc_lsp2pred(int16_t *lsf, int16_t *lpc, int order)
 {
 	Word32 f0[6], f1[6];
 	lpc_clmp(lsf, 0, order);
@@ -911,7 +911,7 @@ MD Word16 block_max(const int16_t *d, int n)
 
 /* cfft :115 -- in-place radix-2 DIT complex FFT of nn points (2*nn shorts)
  * with per-stage block floating point; returns the number of halvings. */
-MD Word16 cfft(int16_t *d0, Word16 nn)
+MN Word16 cfft(int16_t *d0, Word16 nn)
 {
 	const int16_t *wrt = g_der.wr, *wit = g_der.wi;
 	int16_t *d = d0 - 1;	/* 1-based view, as the reference */
@@ -1027,7 +1027,7 @@ MD Word16 fft_npp(int16_t *d, Word16 dir)
 
 /* rfft :33 -- real FFT of n points through an n/2-point complex FFT;
  * d must hold 2n shorts */
-MD void rfft(int16_t *d, Word16 n)
+MN void rfft(int16_t *d, Word16 n)
 {
 	const int16_t *wrt = g_der.wr, *wit = g_der.wi;
 	Word16 n2 = shr(n, 1);

@@ -15,7 +15,7 @@ namespace mlp {
 
 /* melp_ana :280 -- analysis of one 180-sample frame; `speech` points at
  * hpspeech[i*FRAME] (the window spans speech[0 .. FRAME_END+PITCHMAX]) */
-MD void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
+MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 {
 	int16_t *sb = E->sigbuf;
 	int16_t ac[17], lpc[LPC_ORD + 1], tdin[LPF_ORD], tdout[LPF_ORD];
@@ -108,7 +108,7 @@ MD bool subEnRel2(const ClassParam *cs, int c)
 
 /* the pitch-track correction shared by frames 0 and 1 of sc_ana when the
  * tracks disagree (melp_ana.c:590-640 and 700-760) */
-MD void sc_track_fix(PitTrack *pt, int16_t *pitch, Word16 prev_pitch)
+MN void sc_track_fix(PitTrack *pt, int16_t *pitch, Word16 prev_pitch)
 {
 	Word16 i1 = trackPitch(prev_pitch, pt);
 	Word16 cand = shl(pt->pit[i1], 7);
@@ -123,7 +123,7 @@ MD void sc_track_fix(PitTrack *pt, int16_t *pitch, Word16 prev_pitch)
 }
 
 /* sc_ana :522 -- superframe pitch smoothing and bpvc smoothing */
-MD void sc_ana(EncState *E, MelpParam *par)
+MN void sc_ana(EncState *E, MelpParam *par)
 {
 	ClassParam *cs = E->classStat;
 	PitTrack *pt = E->pitTrack;
@@ -335,7 +335,7 @@ MD void sc_ana(EncState *E, MelpParam *par)
 }
 
 /* analysis :119 -- 540 NPP-processed samples -> quantised params + chbuf */
-MD void analysis(EncState *E, const int16_t *sp_in)
+MN void analysis(EncState *E, const int16_t *sp_in)
 {
 	MelpParam *par = E->par;
 	int16_t lpc[LPC_ORD + 1];
@@ -373,7 +373,7 @@ MD void analysis(EncState *E, const int16_t *sp_in)
 
 /* melpe_a :91 -- sp (540) is denoised in place, then analysed; the 11-byte
  * frame is left in E->chbuf */
-MD void encode_superframe(EncState *E, NppScratch *w, int16_t *sp)
+MN void encode_superframe(EncState *E, NppScratch *w, int16_t *sp)
 {
 	npp_frame(&E->npp, w, sp, sp);
 	npp_frame(&E->npp, w, sp + FRAME, sp + FRAME);

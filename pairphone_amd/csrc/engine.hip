@@ -17,8 +17,7 @@
 #include <string>
 #include <mutex>
 
-#include "state.h"
-#include "derived.h"
+#include "codec.h"
 #define SYN_FN __host__ __device__ static inline
 #include "synth.h"
 #include "../../include/melpe.h"
@@ -51,8 +50,7 @@ extern "C" const unsigned char melpe_tables_blob_end[];
 __global__ void k_init_tables()
 {
 	if (threadIdx.x == 0 && blockIdx.x == 0) {
-		derive_fft_twiddles(&g_der);
-		derive_lsp_cos(&g_der);
+		derive_all(&g_der);
 	}
 }
 
@@ -80,6 +78,21 @@ __global__ __launch_bounds__(WAVE) void k_npp(EncState *enc, int16_t *sp, int fr
 	int16_t *x = sp + (size_t) c * stride;
 	for (int f = 0; f < frames; f++)
 		npp_frame(&enc[c].npp, &w, x + f * NPP_HOP, x + f * NPP_HOP, rate1200 != 0);
+}
+
+/* melpe_a on every active channel (melpe/melpe.c:91-99): one lane per
+ * channel, sp (C x 540) in place, bits (C x 11) out */
+__global__ __launch_bounds__(WAVE) void k_encode(EncState *enc, int16_t *sp, uint8_t *bits,
+						  const uint8_t *active, int n)
+{
+	int c = blockIdx.x * WAVE + threadIdx.x;
+	if (c >= n || (active && !active[c]))
+		return;
+	NppScratch w;
+	EncState *E = &enc[c];
+	encode_superframe(E, &w, sp + (size_t) c * BLOCK);
+	for (int k = 0; k < 11; k++)
+		bits[(size_t) c * 11 + k] = E->chbuf[k];
 }
 
 __global__ __launch_bounds__(WAVE) void k_synth_seed(synth_state *s, uint32_t seed,
@@ -316,14 +329,48 @@ int melpe_npp_host(melpe_engine *e, int16_t *sp, int frames, int stride, const u
 	return rc;
 }
 
-int melpe_encode_host(melpe_engine *, unsigned char *, int16_t *, const uint8_t *)
+static int encode_launch(melpe_engine *e, unsigned char *d_bits, int16_t *d_sp,
+			 const uint8_t *d_act, hipStream_t s, bool sync)
 {
-	return fail_msg("encode: not built yet");
+	HIPCHK(hipSetDevice(e->device));
+	ev_begin(e, s);
+	k_encode<<<grid_for(e->channels), WAVE, 0, s>>>(e->d_enc, d_sp, d_bits, d_act,
+							  e->channels);
+	HIPCHK(hipGetLastError());
+	ev_end(e, s, sync);
+	return 0;
 }
 
-int melpe_encode_dev(melpe_engine *, void *, void *, const void *, void *)
+int melpe_encode_dev(melpe_engine *e, void *d_bits, void *d_sp, const void *d_active,
+		     void *hip_stream)
 {
-	return fail_msg("encode: not built yet");
+	if (!e || !d_bits || !d_sp)
+		return fail_msg("melpe_encode_dev: null argument");
+	return encode_launch(e, (unsigned char *) d_bits, (int16_t *) d_sp,
+			     (const uint8_t *) d_active, (hipStream_t) hip_stream, false);
+}
+
+int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const uint8_t *active)
+{
+	if (!e || !bits || !sp)
+		return fail_msg("melpe_encode_host: null argument");
+	HIPCHK(hipSetDevice(e->device));
+	size_t pb = sizeof(int16_t) * BLOCK * (size_t) e->channels;
+	size_t bb = (size_t) 11 * e->channels;
+	int rc;
+	const uint8_t *m = stage_mask(e, active, &rc);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(e->d_pcm, sp, pb, hipMemcpyHostToDevice, e->stream));
+	if (active)	/* inactive channels keep the caller's bits */
+		HIPCHK(hipMemcpyAsync(e->d_bits, bits, bb, hipMemcpyHostToDevice, e->stream));
+	rc = encode_launch(e, e->d_bits, e->d_pcm, m, e->stream, true);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(sp, e->d_pcm, pb, hipMemcpyDeviceToHost, e->stream));
+	HIPCHK(hipMemcpyAsync(bits, e->d_bits, bb, hipMemcpyDeviceToHost, e->stream));
+	HIPCHK(hipStreamSynchronize(e->stream));
+	return 0;
 }
 
 int melpe_decode_host(melpe_engine *, int16_t *, const unsigned char *, const uint8_t *)

@@ -102,7 +102,7 @@ MD Word32 npp_spec_sum(const int16_t *v, const int16_t *vs, Word16 maxs)
 }
 
 /* gain_mod :211 -- speech-presence-uncertainty modification of the gain */
-MD void npp_gain_mod(const NppState *s, const NppScratch *w, const int16_t *qk,
+MN void npp_gain_mod(const NppState *s, const NppScratch *w, const int16_t *qk,
 		     int16_t *GainD, int m)
 {
 	for (int i = 0; i < m; i++) {
@@ -156,7 +156,7 @@ MD void npp_gain_mod(const NppState *s, const NppScratch *w, const int16_t *qk,
 }
 
 /* compute_qk :289 -- a-priori speech absence probability */
-MD void npp_compute_qk(NppState *s, int16_t *qk, const int16_t *gk, const int16_t *gks,
+MN void npp_compute_qk(NppState *s, int16_t *qk, const int16_t *gk, const int16_t *gks,
 		       Word16 thr)
 {
 	if (!s->qk_started) {
@@ -171,7 +171,7 @@ MD void npp_compute_qk(NppState *s, int16_t *qk, const int16_t *gk, const int16_
 }
 
 /* gain_log_mmse :319 */
-MD void npp_gain_log_mmse(NppState *s, NppScratch *w, const int16_t *qk, int16_t *Gain,
+MN void npp_gain_log_mmse(NppState *s, NppScratch *w, const int16_t *qk, int16_t *Gain,
 			  const int16_t *gk, const int16_t *gks, int m)
 {
 	for (int i = 0; i < m; i++) {
@@ -246,7 +246,7 @@ MD void npp_gain_log_mmse(NppState *s, NppScratch *w, const int16_t *qk, int16_t
 }
 
 /* ksi_min_adapt :428 */
-MD Word16 npp_ksi_min_adapt(bool nflag, Word16 kmin, Word16 snlt, Word16 snlt_sh)
+MN Word16 npp_ksi_min_adapt(bool nflag, Word16 kmin, Word16 snlt, Word16 snlt_sh)
 {
 	if (nflag)
 		return kmin;
@@ -290,7 +290,7 @@ MD void npp_smoothing_win(int16_t *x)
 }
 
 /* smoothed_periodogram :511 -- optimal recursive smoothing of |Y|^2 */
-MD void npp_smoothed_periodogram(NppState *s, NppScratch *w, Word16 YY_av, Word16 yy_shift)
+MN void npp_smoothed_periodogram(NppState *s, NppScratch *w, Word16 YY_av, Word16 yy_shift)
 {
 	Word16 maxs = SW_MIN_;
 	for (int i = 0; i < NPP_NB; i++)
@@ -406,7 +406,7 @@ MD void npp_smoothed_periodogram(NppState *s, NppScratch *w, Word16 YY_av, Word1
 }
 
 /* bias_compensation :695 */
-MD void npp_bias_compensation(NppState *s, NppScratch *w, int16_t *bsp, int16_t *bsh,
+MN void npp_bias_compensation(NppState *s, NppScratch *w, int16_t *bsp, int16_t *bsh,
 			      int16_t *bsub, int16_t *bsubsh)
 {
 	Word32 vsum = 0;
@@ -515,7 +515,7 @@ MD Word16 npp_noise_slope(const NppState *s)
 }
 
 /* min_search :889 -- minimum tracking over 8 windows of 9 frames */
-MD void npp_min_search(NppState *s, const int16_t *bsp, const int16_t *bsh,
+MN void npp_min_search(NppState *s, const int16_t *bsp, const int16_t *bsh,
 		       const int16_t *bsub, const int16_t *bsubsh)
 {
 	if (s->minspec_counter == 0) {
@@ -598,7 +598,7 @@ MD void npp_min_search(NppState *s, const int16_t *bsp, const int16_t *bsh,
 }
 
 /* minstat_init :1164 */
-MD void npp_minstat_init(NppState *s)
+MN void npp_minstat_init(NppState *s)
 {
 	v_copy(s->smoothedspect, s->lambdaD, NPP_NB);
 	v_scale(s->smoothedspect, NOISE_BIAS, NPP_NB);
@@ -625,7 +625,7 @@ MD void npp_minstat_init(NppState *s)
 }
 
 /* enh_init :1023 -- initial noise estimate from the first 256 samples */
-MD void npp_enh_init(NppState *s, NppScratch *w, int16_t *noise)
+MN void npp_enh_init(NppState *s, NppScratch *w, int16_t *noise)
 {
 	int16_t *yb = w->ybuf;
 	int32_t *ty = w->temp_yy;
@@ -712,7 +712,7 @@ MD void npp_enh_init(NppState *s, NppScratch *w, int16_t *noise)
 }
 
 /* process_frame :1212 -- one 256-sample analysis/synthesis frame */
-MD void npp_process_frame(NppState *s, NppScratch *w, const int16_t *in, int16_t *out)
+MN void npp_process_frame(NppState *s, NppScratch *w, const int16_t *in, int16_t *out)
 {
 	int16_t *yb = w->ybuf;
 	int32_t *ty = w->temp_yy;
@@ -986,7 +986,7 @@ MD void npp_process_frame(NppState *s, NppScratch *w, const int16_t *in, int16_t
 /* npp :170 -- 180 new samples in, 180 enhanced samples out (in place ok).
  * On the first call the initial noise estimate reads 256 samples from sp_in
  * when the codec runs at 1200 bps (npp.c:176-189), else 180 after 76 zeros. */
-MD void npp_frame(NppState *s, NppScratch *w, const int16_t *sp_in, int16_t *sp_out,
+MN void npp_frame(NppState *s, NppScratch *w, const int16_t *sp_in, int16_t *sp_out,
 		  bool rate1200 = true)
 {
 	int16_t outbuf[NPP_WIN];

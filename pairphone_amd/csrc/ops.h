@@ -25,10 +25,13 @@
 #include <hip/hip_runtime.h>
 #define MD __device__ __attribute__((always_inline)) inline
 #define MF __device__
+/* big routines stay out of line: bounded compile time and register use */
+#define MN __device__ __noinline__
 #define MDEV_CONST __device__
 #else
 #define MD static inline
 #define MF static
+#define MN static
 #define MDEV_CONST
 #endif
 

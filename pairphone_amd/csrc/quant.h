@@ -20,7 +20,7 @@ namespace mlp {
 #define LSP_INP_CAND 5
 
 /* vq_lspw, melpe/vq_lib.c:70 -- |A(e^jw)|^-0.3 weights */
-MD void vq_lspw(int16_t *w, const int16_t *lsp, const int16_t *lpc, int order)
+MN void vq_lspw(int16_t *w, const int16_t *lsp, const int16_t *lpc, int order)
 {
 	for (int i = 0; i < order; i++)
 		w[i] = L_pow_fxp(lpc_aejw(lpc, lsp[i], order), -9830, 19, 11);
@@ -29,7 +29,7 @@ MD void vq_lspw(int16_t *w, const int16_t *lsp, const int16_t *lpc, int order)
 }
 
 /* vq_enc, melpe/vq_lib.c:474 -- full search, first minimum wins */
-MD Word32 vq_enc(const int16_t *cb, const int16_t *u, int levels, int order, int16_t *uhat,
+MN Word32 vq_enc(const int16_t *cb, const int16_t *u, int levels, int order, int16_t *uhat,
 		 int16_t *index)
 {
 	int16_t best = 0;
@@ -72,7 +72,7 @@ MD void vq_fsw(int16_t *wfs, int nh, Word16 pitch)
 
 /* wvq1 :221 -- keeps `cand` best entries; a new entry replaces the slot
  * holding the current maximum, exactly as the reference's linear rescan */
-MD void wvq1(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int dim, int cbsize,
+MN void wvq1(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int dim, int cbsize,
 	     int16_t *index, Word32 *dist, int cand)
 {
 	for (int j = 0; j < cand; j++)
@@ -103,7 +103,7 @@ MD void wvq1(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int dim, 
 }
 
 /* wvq2 :302 */
-MD int16_t wvq2(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int dim,
+MN int16_t wvq2(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int dim,
 		const int16_t *index, const Word32 *dist, int cand)
 {
 	Word32 mn = LW_MAX_;
@@ -127,7 +127,7 @@ MD int16_t wvq2(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int di
 }
 
 /* pitch_vq :75 */
-MD void pitch_vq(EncState *E, MelpParam *par)
+MN void pitch_vq(EncState *E, MelpParam *par)
 {
 	QuantParam *q = &E->qpar;
 	int16_t tgt[NF], deltp[NF], deltw[NF], wt[NF];
@@ -203,7 +203,7 @@ MD void pitch_vq(EncState *E, MelpParam *par)
 }
 
 /* gain_vq :368 -- 1024 x 6 full search with the reference's early skip */
-MD void gain_vq(EncState *E, MelpParam *par)
+MN void gain_vq(EncState *E, MelpParam *par)
 {
 	const int16_t *cb = TB(gain_vq_cb);
 	int16_t tg[NF * NUM_GAINFR];
@@ -249,7 +249,7 @@ MD void quant_bp(EncState *E, MelpParam *par)
 /* ------------------------------------------------------------------ */
 
 /* WeightedMSE :669 -- early exit after half the dimensions */
-MD Word16 WeightedMSE(int n, const int16_t *w, const int16_t *x, const int16_t *tgt,
+MN Word16 WeightedMSE(int n, const int16_t *w, const int16_t *x, const int16_t *tgt,
 		      Word16 max_dmin)
 {
 	Word32 d = 0;
@@ -268,7 +268,7 @@ MD Word16 WeightedMSE(int n, const int16_t *w, const int16_t *x, const int16_t *
 }
 
 /* InsertCand :735 -- ordered insert into the M-best list */
-MD Word16 InsertCand(int c1, int s1, int16_t *dMin, Word16 dist, int16_t entry,
+MN Word16 InsertCand(int c1, int s1, int16_t *dMin, Word16 dist, int16_t entry,
 		     int16_t (*nextIndex)[LSP_VQ_STAGES], int16_t (*index)[LSP_VQ_STAGES])
 {
 	int i = 0;
@@ -286,7 +286,7 @@ MD Word16 InsertCand(int c1, int s1, int16_t *dMin, Word16 dist, int16_t entry,
 
 /* lspVQ :482 -- M-best multistage search; qout receives the ncPrev best
  * reconstructions (dim each), cb_index their stage indices (tos each) */
-MD void lspVQ(const int16_t *target, const int16_t *weight, int16_t *qout, const int16_t *cb,
+MN void lspVQ(const int16_t *target, const int16_t *weight, int16_t *qout, const int16_t *cb,
 	      int tos, const int16_t *cb_size, int16_t *cb_index, int dim, bool flag)
 {
 	int16_t index[LSP_VQ_CAND][LSP_VQ_STAGES], nextIndex[LSP_VQ_CAND][LSP_VQ_STAGES];
@@ -381,7 +381,7 @@ MD Word32 lsf_werr(Word32 acc, Word16 w)
 }
 
 /* lsf_vq :895 */
-MD void lsf_vq(EncState *E, MelpParam *par)
+MN void lsf_vq(EncState *E, MelpParam *par)
 {
 	QuantParam *q = &E->qpar;
 	const int16_t melp_cb_size[4] = {256, 64, 32, 32};
@@ -493,7 +493,7 @@ MD void lsf_vq(EncState *E, MelpParam *par)
 }
 
 /* quant_jitter :1198 */
-MD void quant_jitter(EncState *E, MelpParam *par)
+MN void quant_jitter(EncState *E, MelpParam *par)
 {
 	Word16 uvc = 0;
 	int16_t jit[NF];
@@ -536,7 +536,7 @@ MD void quant_jitter(EncState *E, MelpParam *par)
 }
 
 /* quant_fsmag :1277 */
-MD void quant_fsmag(EncState *E, MelpParam *par)
+MN void quant_fsmag(EncState *E, MelpParam *par)
 {
 	int16_t qmag[NUM_HARM];
 	int cnt = 0, last = -1;
@@ -636,7 +636,7 @@ MD void crc4_enc(int16_t *bit, int nbits)
 }
 
 /* low_rate_fec_code :955 -- protects all-unvoiced superframes */
-MD void low_rate_fec_code(QuantParam *q)
+MN void low_rate_fec_code(QuantParam *q)
 {
 	if (!(q->uv_flag[0] && q->uv_flag[1] && q->uv_flag[2]))
 		return;
@@ -671,7 +671,7 @@ MD Word16 parity(Word16 x, int len)	/* melp_chn.c:1367 */
 }
 
 /* low_rate_chn_write :262 -- 81-bit superframe into chbuf (11 bytes) */
-MD void low_rate_chn_write(EncState *E)
+MN void low_rate_chn_write(EncState *E)
 {
 	QuantParam *q = &E->qpar;
 	unsigned char bb[81];

@@ -49,11 +49,30 @@ def make_npp(tmp, seed=11, channels=8, frames=300):
     return out
 
 
+def make_enc(tmp, seed, channels, nsf, keep_bits=0):
+    """melpe_a goldens: per-channel SHA-256 of the bitstream and of the NPP
+    output the reference leaves in the caller's buffer."""
+    bits = os.path.join(tmp, "e.bits")
+    npp = os.path.join(tmp, "e.npp")
+    ref("encgen", seed, 0, channels, nsf, bits, npp)
+    b = np.fromfile(bits, dtype=np.uint8).reshape(channels, nsf * 11)
+    y = np.fromfile(npp, dtype=np.int16).reshape(channels, nsf * 540)
+    out = {"seed": seed, "channels": channels, "superframes": nsf,
+           "bits_sha256": [sha(b[c].tobytes()) for c in range(channels)],
+           "npp_sha256": [sha(y[c].tobytes()) for c in range(channels)]}
+    if keep_bits:
+        out["bits_hex"] = [b[c].tobytes().hex() for c in range(keep_bits)]
+    return out
+
+
 def main():
     if not os.path.exists(TOOL):
         sys.exit("oracle/_ref/ref_tool missing")
     which = sys.argv[1:] or ["npp"]
     with tempfile.TemporaryDirectory() as tmp:
+        if "enc" in which:
+            json.dump(make_enc(tmp, 1, 1024, 149, keep_bits=8),
+                      open(os.path.join(HERE, "enc_1024.json"), "w"))
         if "npp" in which:
             json.dump(make_npp(tmp), open(os.path.join(HERE, "npp.json"), "w"), indent=1)
     print("ok")

@@ -1,0 +1,177 @@
+"""melpe_a (encode) parity against the reference codec.
+
+Goldens (tests/golden/enc_1024.json, made by tests/golden/make_golden.py from
+the reference compiled by oracle/Makefile): SHA-256 of each channel's
+bitstream and of the NPP output melpe_a leaves in the caller's buffer, for
+1024 channels x 149 superframes (10 s) of the csrc/synth.h signal, seed 1.
+
+CPU: the host build of the device sources on a few channels.
+GPU: the HIP engine on all 1024 channels (BASELINE config 2), edge signals
+against the live reference, ragged activity masks and the drop-in
+single-stream API.
+"""
+import ctypes
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, GOLDEN, REF_TOOL
+
+EMU = os.path.join(ROOT, "build", "libmelpe_hostemu.so")
+TABLES = os.path.join(ROOT, "pairphone_amd", "data", "melpe_tables.bin")
+
+
+def golden():
+    return json.load(open(os.path.join(GOLDEN, "enc_1024.json")))
+
+
+def sha(b):
+    return hashlib.sha256(b.tobytes()).hexdigest()
+
+
+def signals(seed, channels, nsf, first=0):
+    from pairphone_amd import synth_signal
+    return np.stack([synth_signal(seed, first + c, nsf * 540) for c in range(channels)])
+
+
+def emu():
+    lib = ctypes.CDLL(EMU)
+    lib.emu_create.restype = ctypes.c_void_p
+    lib.emu_create.argtypes = [ctypes.c_int]
+    lib.emu_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.emu_destroy.argtypes = [ctypes.c_void_p]
+    assert lib.emu_load_tables(TABLES.encode()) == 0
+    return lib
+
+
+def run_superframes(encode, x, nsf):
+    """x: [C, nsf*540] -> (bits [C, nsf*11], npp [C, nsf*540])"""
+    C = x.shape[0]
+    bits = np.zeros((C, nsf * 11), np.uint8)
+    npp = np.zeros((C, nsf * 540), np.int16)
+    for k in range(nsf):
+        sp = np.ascontiguousarray(x[:, k * 540:(k + 1) * 540])
+        b = encode(sp)
+        bits[:, k * 11:(k + 1) * 11] = b
+        npp[:, k * 540:(k + 1) * 540] = sp
+    return bits, npp
+
+
+def test_encode_hostemu_matches_golden():
+    g = golden()
+    ch, nsf = 3, g["superframes"]
+    x = signals(g["seed"], ch, nsf)
+    lib = emu()
+    e = lib.emu_create(ch)
+
+    def enc(sp):
+        b = np.zeros((ch, 11), np.uint8)
+        lib.emu_encode(e, b.ctypes.data, sp.ctypes.data)
+        return b
+    bits, npp = run_superframes(enc, x, nsf)
+    lib.emu_destroy(e)
+    for c in range(ch):
+        assert bits[c].tobytes().hex() == g["bits_hex"][c], "channel %d bits" % c
+        assert sha(npp[c]) == g["npp_sha256"][c], "channel %d npp" % c
+
+
+@pytest.mark.gpu
+def test_encode_gpu_1024_channels_match_golden():
+    from pairphone_amd import MelpeEngine
+    g = golden()
+    C, nsf = g["channels"], g["superframes"]
+    x = signals(g["seed"], C, nsf)
+    eng = MelpeEngine(C)
+    bits, npp = run_superframes(eng.encode, x, nsf)
+    bad = [c for c in range(C) if sha(bits[c]) != g["bits_sha256"][c]]
+    badn = [c for c in range(C) if sha(npp[c]) != g["npp_sha256"][c]]
+    assert not bad, "bitstream mismatch on %d channels, first %s" % (len(bad), bad[:8])
+    assert not badn, "NPP output mismatch on %d channels, first %s" % (len(badn), badn[:8])
+
+
+def edge_signals(n):
+    rng = np.random.default_rng(5)
+    t = np.arange(n)
+    return {
+        "zeros": np.zeros(n, np.int16),
+        "noise_fs": rng.integers(-32768, 32767, n).astype(np.int16),
+        "sine1k_fs": (32767 * np.sin(2 * np.pi * 1000 * t / 8000)).astype(np.int16),
+        "square": np.where((t // 20) % 2 == 0, 32767, -32768).astype(np.int16),
+        "dc_pos": np.full(n, 32767, np.int16),
+        "dc_neg": np.full(n, -32768, np.int16),
+        "impulses": np.where(t % 57 == 0, 30000, 0).astype(np.int16),
+        "sweep": (20000 * np.sin(2 * np.pi * np.cumsum(np.linspace(50, 3900, n)) / 8000)).astype(np.int16),
+        "speech_loud": np.clip(np.asarray(signals(9, 1, n // 540)[0], np.int32) * 4, -32768, 32767).astype(np.int16),
+    }
+
+
+@pytest.mark.gpu
+def test_encode_gpu_edge_signals_match_live_reference(tmp_path, ref_tool):
+    from pairphone_amd import MelpeEngine
+    nsf = 40
+    sig = edge_signals(nsf * 540)
+    names = sorted(sig)
+    x = np.stack([sig[k] for k in names])
+    eng = MelpeEngine(len(names))
+    bits, npp = run_superframes(eng.encode, x, nsf)
+    for i, k in enumerate(names):
+        p = str(tmp_path / (k + ".pcm"))
+        sig[k].tofile(p)
+        subprocess.run([REF_TOOL, "enc", p, p + ".bits"], check=True)
+        rb = np.fromfile(p + ".bits", dtype=np.uint8)
+        np.testing.assert_array_equal(bits[i], rb, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_encode_gpu_ragged_mask():
+    """Inactive channels keep state, PCM and bits untouched: a channel that
+    is paused for some superframes equals the same channel fed only its
+    active superframes."""
+    from pairphone_amd import MelpeEngine
+    g = golden()
+    C, nsf = 8, 30
+    x = signals(g["seed"], C, nsf)
+    rng = np.random.default_rng(3)
+    act = rng.random((nsf + 10, C)) < 0.7
+    eng = MelpeEngine(C)
+    pos = np.zeros(C, int)
+    out = [[] for _ in range(C)]
+    for k in range(act.shape[0]):
+        sp = np.zeros((C, 540), np.int16)
+        for c in range(C):
+            if act[k, c] and pos[c] < nsf:
+                sp[c] = x[c, pos[c] * 540:(pos[c] + 1) * 540]
+        m = np.array([act[k, c] and pos[c] < nsf for c in range(C)], np.uint8)
+        b0 = np.full((C, 11), 0xAB, np.uint8)
+        sp_before = sp.copy()
+        b = eng._raw_encode(sp, b0, m)
+        for c in range(C):
+            if m[c]:
+                out[c].append(b[c].copy())
+                pos[c] += 1
+            else:
+                assert (b[c] == 0xAB).all() and (sp[c] == sp_before[c]).all()
+    for c in range(C):
+        got = np.concatenate(out[c])[:pos[c] * 11]
+        want = bytes.fromhex(g["bits_hex"][c])[:pos[c] * 11]
+        assert got.tobytes() == want, "channel %d" % c
+
+
+@pytest.mark.gpu
+def test_single_stream_dropin_matches_golden():
+    """melpe_i + melpe_a through include/melpe.h, as melpe/encoder.c does."""
+    from pairphone_amd import Melpe
+    g = golden()
+    nsf = 60
+    x = signals(g["seed"], 1, nsf)[0]
+    m = Melpe()
+    m.melpe_i()
+    out = []
+    for k in range(nsf):
+        sp = x[k * 540:(k + 1) * 540].copy()
+        out.append(m.melpe_a(sp))
+    assert np.concatenate(out).tobytes() == bytes.fromhex(g["bits_hex"][0])[:nsf * 11]
