@@ -6,6 +6,7 @@
 #define MELPE_CODEC_H
 
 #include "encoder.h"
+#include "decoder.h"
 #include "derived.h"
 
 namespace mlp {

@@ -1,0 +1,1114 @@
+/*
+ * decoder.h -- one superframe of MELPe-1200 decoding for one channel:
+ * melpe_s (melpe/melpe.c:102-107) = unpack + dequantise + synthesis.
+ *
+ * Restates melpe/melp_syn.c (synthesis, melp_syn), melpe/harm.c
+ * (harm_syn_pitch, realIDFT, set_fc), melpe/postfilt.c, melpe/melp_chn.c
+ * (low_rate_chn_read), melpe/fec_code.c (low_rate_fec_decode) and the
+ * decoder helpers of melpe/melp_sub.c (noise_est, noise_sup, lin_int_bnd,
+ * scale_adj) and melpe/qnt12.c (deqnt_msvq), with every static in DecState.
+ */
+#ifndef MELPE_DECODER_H
+#define MELPE_DECODER_H
+
+#include "quant.h"
+
+namespace mlp {
+
+/* ------------------------------------------------------------------ */
+/* melpe/melp_sub.c decoder helpers                                   */
+/* ------------------------------------------------------------------ */
+
+/* lin_int_bnd :424 */
+MD Word16 lin_int_bnd(Word16 x, Word16 xmin, Word16 xmax, Word16 ymin, Word16 ymax)
+{
+	if (x <= xmin)
+		return ymin;
+	if (x >= xmax)
+		return ymax;
+	Word16 t = mult(sub(x, xmin), sub(ymax, ymin));
+	return add(ymin, divide_s(t, sub(xmax, xmin)));
+}
+
+/* noise_est :465 */
+MD void noise_est(Word16 gain, int16_t *ng, Word16 up, Word16 down, Word16 mn, Word16 mx)
+{
+	Word32 Lng = L_deposit_h(*ng);
+	Word16 t1 = r_ound(L_add(Lng, L_shl(L_deposit_l(up), 5)));
+	Word16 t2 = r_ound(L_add(Lng, L_shl(L_deposit_l(down), 7)));
+	if (gain > t1)
+		*ng = t1;
+	else if (gain < t2)
+		*ng = t2;
+	else
+		*ng = gain;
+	if (*ng < mn)
+		*ng = mn;
+	if (*ng > mx)
+		*ng = mx;
+}
+
+/* noise_sup :513 */
+MN void noise_sup(int16_t *gain, Word16 ng, Word16 max_noise, Word16 max_att, Word16 nfact)
+{
+	Word16 sup;
+	if (ng > max_noise)
+		ng = max_noise;
+	Word16 lev = sub(*gain, add(ng, nfact));
+	if (lev > 0) {
+		Word16 t = extract_h(L_shl(L_mult(-3276, lev), 4));
+		t = pow10_fxp(t, 14);
+		t = sub(16384, t);
+		sup = mult(-20480, log10_fxp(t, 14));
+		if (sup > max_att)
+			sup = max_att;
+	} else {
+		sup = max_att;
+	}
+	*gain = sub(*gain, sup);
+}
+
+/* scale_adj :768 -- match the period's energy to the target gain with a
+ * SCALEOVER-sample cross-fade from the previous scale */
+MN void scale_adj(DecState *D, int16_t *sp, Word16 gain, int len, Word16 over, Word16 inv_over)
+{
+	int16_t tb[PITCHMAX + 8];
+	Word16 sh = 4, t;
+	v_equ_shr(tb, sp, sh, len);
+	Word32 msq = L_v_magsq(tb, len, 0, 1);
+	if (msq) {
+		t = sub(norm_l(msq), 1);
+		sh = sub(sh, shr(t, 1));
+	} else {
+		sh = 0;
+	}
+	v_equ_shr(tb, sp, sh, len);
+	sh = shl(sh, 1);
+	t = shl(256, sh);
+	sh = log10_fxp(t, 8);
+	msq = L_v_magsq(tb, len, 0, 0);
+	msq = L_add(msq, 1);
+	Word16 lmsq = L_log10_fxp(msq, 0);
+	msq = L_add(L_shl(L_deposit_l(lmsq), 1), L_deposit_l(sh));
+	Word16 llen = log10_fxp(shl((Word16) len, 7), 7);
+	Word32 L = L_shl(L_deposit_l(gain), 1);
+	L = L_sub(L, msq);
+	L = L_add(L, L_deposit_l(llen));
+	L = L_shr(L, 1);
+	Word16 scale = pow10_fxp(extract_l(L), 13);
+	for (int i = 1; i < over; i++) {
+		t = shl(sub(over, (Word16) i), 11);
+		t = extract_h(L_shl(L_mult(t, inv_over), 1));
+		Word32 i1 = L_mult(D->prev_scale, t);
+		t = shl((Word16) i, 11);
+		t = extract_h(L_shl(L_mult(t, inv_over), 1));
+		Word32 i2 = L_mult(scale, t);
+		Word32 s = extract_h(L_add(i1, i2));
+		sp[i - 1] = extract_h(L_shl(L_mult(sp[i - 1], (Word16) s), 2));
+	}
+	v_scale_shl(&sp[over - 1], scale, (int16_t) (len - over + 1), 2);
+	D->prev_scale = scale;
+}
+
+/* deqnt_msvq, melpe/qnt12.c:1158 */
+MD void deqnt_msvq(int16_t *qout, const int16_t *cb, int tos, const int16_t *cb_size,
+		   const int16_t *index, int dim)
+{
+	v_zero(qout, dim);
+	const int16_t *p = cb;
+	for (int i = 0; i < tos; i++) {
+		v_add(qout, p + extract_l(L_shr(L_mult(index[i], (Word16) dim), 1)), dim);
+		p += extract_l(L_shr(L_mult(cb_size[i], (Word16) dim), 1));
+	}
+}
+
+/* ------------------------------------------------------------------ */
+/* FEC decode, melpe/fec_code.c                                        */
+/* ------------------------------------------------------------------ */
+
+MD Word16 sbc_syn(const int16_t *x, int n, int k, const int16_t *pmat)
+{
+	Word16 r = 0;
+	for (int i = k, j = n - k - 1; i < n; i++, j--, pmat += k)
+		r = add(r, (Word16) ((x[i] ^ binprod(x, pmat, k)) << j));
+	return r;
+}
+
+MD Word16 sbc_dec(int16_t *x, int n, int k, const int16_t *pmat, const int16_t *syntab)
+{
+	Word16 bep = syntab[sbc_syn(x, n, k, pmat)];
+	if (bep > -1)
+		x[bep] ^= 1;
+	return bep;
+}
+
+MD Word16 crc4_dec(const int16_t *bit, int nbits)
+{
+	int16_t d[4];
+	for (int i = 1; i <= 4; i++)
+		d[4 - i] = bit[nbits - i];
+	for (int i = 5; i <= nbits; i++) {
+		int16_t x = d[3];
+		d[3] = d[2];
+		d[2] = d[1];
+		d[1] = (int16_t) (x ^ d[0]);
+		d[0] = (int16_t) (x ^ bit[nbits - i]);
+	}
+	return (Word16) (d[0] | d[1] | d[2] | d[3]);
+}
+
+/* low_rate_fec_decode :1062 */
+MD Word16 low_rate_fec_decode(QuantParam *q, Word16 erase, int16_t *lsp_check)
+{
+	if (!(q->uv_flag[0] && q->uv_flag[1] && q->uv_flag[2]))
+		return erase;
+	int16_t c84[8], c74[7], c13[13];
+	const int16_t *p84 = TB(pmat84), *p74 = TB(pmat74);
+	vgetbits(c84, q->gain_index[0], 9, 4);
+	vgetbits(&c84[4], q->fs_index, 7, 4);
+	Word16 b = sbc_dec(c84, 8, 4, p84, TB(syntab84));
+	erase |= b == -2;
+	vsetbits(q->gain_index, 9, 4, c84);
+	vgetbits(c84, q->gain_index[0], 5, 4);
+	vgetbits(&c84[4], q->fs_index, 3, 4);
+	b = sbc_dec(c84, 8, 4, p84, TB(syntab84));
+	erase |= b == -2;
+	vsetbits(q->gain_index, 5, 4, c84);
+	if (!erase) {
+		vgetbits(c74, q->gain_index[0], 1, 2);
+		c74[2] = c74[3] = 0;
+		vgetbits(&c74[4], q->bpvc_index[0], 1, 2);
+		vgetbits(&c74[6], q->jit_index[0], 0, 1);
+		sbc_dec(c74, 7, 4, p74, TB(syntab74));
+		vsetbits(q->gain_index, 1, 2, c74);
+		for (int f = 0; f < NF; f++) {
+			vgetbits(&c13[4], q->lsf_index[f][0], 8, 9);
+			vgetbits(&c13[0], q->lsf_index[f][1], 3, 4);
+			lsp_check[f] = crc4_dec(c13, 13);
+		}
+	}
+	return erase;
+}
+
+/* ------------------------------------------------------------------ */
+/* low_rate_chn_read, melpe/melp_chn.c:456-1362                         */
+/* ------------------------------------------------------------------ */
+
+MD void set_uv3(QuantParam *q, MelpParam *par, int16_t a, int16_t b, int16_t c)
+{
+	q->uv_flag[0] = par[0].uv_flag = a;
+	q->uv_flag[1] = par[1].uv_flag = b;
+	q->uv_flag[2] = par[2].uv_flag = c;
+}
+
+/* the pitch-index interpretation shared by three branches of the UV
+ * pattern decoding (melp_chn.c:549-600 etc.): low_rate_pitch_dec, then the
+ * popcount of the raw index picks the single-voiced pattern; `prot` is the
+ * protection field that must agree, `uuu_prot` the one for all-unvoiced */
+MD void rd_pitch_pattern(QuantParam *q, MelpParam *par, Word16 uuu_prot, Word16 prot_bp2,
+			 Word16 *erase_uuu, int16_t *fl_lsp, int16_t *fl_pitch)
+{
+	int j = q->pitch_index;
+	q->pitch_index = TB(low_rate_pitch_dec)[q->pitch_index];
+	if (q->pitch_index == 0) {	/* UV_PIND */
+		set_uv3(q, par, 1, 1, 1);
+		if (uuu_prot != 0) {
+			*erase_uuu |= 1;
+			*fl_lsp = 0;
+			*fl_pitch = 0;
+		}
+	} else if (q->pitch_index == 1) {	/* INVAL_PIND */
+		*erase_uuu |= 1;
+		*fl_lsp = 0;
+		*fl_pitch = 0;
+	} else {
+		q->pitch_index -= 2;
+		int k = 0;
+		for (int i = 0; i < 9; i++) {
+			if ((j & 1) == 1)
+				k++;
+			j >>= 1;
+		}
+		int want = -1;
+		if (k == 6 || k == 7) {
+			set_uv3(q, par, 1, 1, 0);
+			want = 1;
+		} else if (k == 4) {
+			set_uv3(q, par, 1, 0, 1);
+			want = 2;
+		} else if (k == 5) {
+			set_uv3(q, par, 0, 1, 1);
+			want = 3;
+		}
+		if (want >= 0 && prot_bp2 != want) {
+			*erase_uuu |= 1;
+			*fl_lsp = 0;
+			*fl_pitch = 0;
+		}
+	}
+}
+
+MN Word16 low_rate_chn_read(DecState *D)
+{
+	QuantParam *q = &D->qpar;
+	MelpParam *par = D->par;
+	const MelpParam *prev = &D->prev_par;
+	const int16_t v_cb_size[4] = {256, 64, 32, 32};
+	const int16_t res_cb_size[4] = {256, 64, 64, 64};
+	const int16_t uv_cb_size[1] = {512};
+	unsigned char bb[81];
+	int16_t lsp_check[NF] = {0, 0, 0};
+	int16_t il1[LPC_ORD], il2[LPC_ORD], res[2 * LPC_ORD], wfs[NUM_HARM];
+	Word16 erase = 0, erase_uuu = 0, erase_vvv = 0, flag_parity = 0;
+	int16_t fl_lsp = 1, fl_pitch = 1;
+	Word16 idx, dontcare, uv_index, uv_parity, prot_bp1, prot_bp2, prot_lsp;
+	if (!D->rd_started) {
+		Word16 t2 = shl(LPC_ORD, 10), t1 = 819;
+		for (int i = 0; i < LPC_ORD; i++) {
+			D->rd_qplsp[i] = divide_s(t1, t2);
+			t1 = add(t1, 819);
+		}
+		v_set(D->rd_prev_gain, 2560, 2 * NF * NUM_GAINFR);
+		v_set(D->rd_prev_fsmag, 8192, NUM_HARM);
+		D->rd_started = 1;
+	}
+	/* chbuf -> one bit per byte (ERASE_MASK & byte is always 0) */
+	BitCursor cc = {D->chbuf, 0};
+	for (int i = 0; i < 81; i++) {
+		erase |= unpack_code(&cc, &idx, 1, 8, 0x4000);
+		bb[i] = (unsigned char) idx;
+	}
+	BitCursor bc = {bb, 0};
+	unpack_code(&bc, &dontcare, 1, 1, 0);
+	unpack_code(&bc, &uv_index, 3, 1, 0);
+	unpack_code(&bc, &uv_parity, 1, 1, 0);
+	unpack_code(&bc, &q->pitch_index, 9, 1, 0);
+	BitCursor b1 = {bc.p + 39, 0};
+	unpack_code(&b1, &prot_lsp, 3, 1, 0);
+	unpack_code(&b1, &dontcare, 10, 1, 0);
+	unpack_code(&b1, &dontcare, 2, 1, 0);
+	unpack_code(&b1, &prot_bp2, 2, 1, 0);
+	unpack_code(&b1, &prot_bp1, 2, 1, 0);
+	if (uv_parity != parity(uv_index, 3))
+		flag_parity |= 1;
+
+	if (uv_index == 0) {
+		if (!flag_parity || prot_bp1 == 0) {
+			rd_pitch_pattern(q, par, prot_bp2, prot_bp2, &erase_uuu, &fl_lsp, &fl_pitch);
+		} else {
+			if (prot_bp2 == 1 && prot_lsp == 7)
+				set_uv3(q, par, 0, 0, 1);
+			else if (prot_bp2 == 2)
+				set_uv3(q, par, 0, 1, 0);
+			else if (prot_bp2 == 3)
+				set_uv3(q, par, 1, 0, 0);
+			else {
+				erase_vvv |= 1;
+				fl_lsp = 0;
+				fl_pitch = 2;
+			}
+		}
+	} else if (uv_index == 1 || uv_index == 2 || uv_index == 4) {
+		if (!flag_parity) {
+			if (uv_index == 1)
+				set_uv3(q, par, 0, 0, 1);
+			else if (uv_index == 2)
+				set_uv3(q, par, 0, 1, 0);
+			else
+				set_uv3(q, par, 1, 0, 0);
+		} else if (prot_bp1 == 0) {
+			rd_pitch_pattern(q, par, prot_lsp, prot_bp2, &erase_uuu, &fl_lsp, &fl_pitch);
+		} else if (prot_bp1 == 1 && prot_lsp == 7) {
+			set_uv3(q, par, 0, 0, 1);
+		} else {
+			erase_vvv |= 1;
+		}
+	} else if (uv_index == 3 || uv_index == 5) {
+		if (!flag_parity) {
+			set_uv3(q, par, 0, 0, 0);
+			if (uv_index == 5)
+				q->pitch_index = (int16_t) (q->pitch_index + 512);
+		} else if (prot_bp1 == 1 && prot_lsp == 7) {
+			set_uv3(q, par, 0, 0, 1);
+		} else {
+			erase_vvv |= 1;
+			if (uv_index == 5)
+				q->pitch_index = (int16_t) (q->pitch_index + 512);
+		}
+	} else if (uv_index == 6) {
+		if (!flag_parity) {
+			set_uv3(q, par, 0, 0, 0);
+			q->pitch_index = (int16_t) (q->pitch_index + 1024);
+		} else {
+			if (prot_bp1 == 2)
+				set_uv3(q, par, 0, 1, 0);
+			/* the reference's second test is not an else-if (melp_chn.c:808) */
+			if (prot_bp1 == 3) {
+				set_uv3(q, par, 1, 0, 0);
+			} else {
+				erase_vvv |= 1;
+				q->pitch_index = (int16_t) (q->pitch_index + 1024);
+			}
+		}
+	} else if (uv_index == 7) {
+		if (!flag_parity)
+			set_uv3(q, par, 0, 0, 0);
+		else
+			erase_vvv |= 1;
+		q->pitch_index = (int16_t) (q->pitch_index + 1536);
+	}
+	if (erase_uuu)
+		set_uv3(q, par, 1, 1, 1);
+	if (erase_vvv)
+		set_uv3(q, par, 0, 0, 0);
+
+	int last = -1, cnt = 0;
+	for (int i = 0; i < NF; i++)
+		if (!q->uv_flag[i]) {
+			cnt++;
+			last = i;
+		}
+	const int16_t u1 = q->uv_flag[0], u2 = q->uv_flag[1], cu = q->uv_flag[2];
+	int16_t (*L)[MAX_LSF_STAGE] = q->lsf_index;
+	if (u1 == 1 && u2 == 1 && cu == 1) {
+		unpack_code(&bc, &L[0][0], 9, 1, 0);
+		unpack_code(&bc, &L[1][0], 9, 1, 0);
+		unpack_code(&bc, &L[2][0], 9, 1, 0);
+		unpack_code(&bc, &L[0][1], 4, 1, 0);
+		unpack_code(&bc, &L[1][1], 4, 1, 0);
+		unpack_code(&bc, &L[2][1], 4, 1, 0);
+		unpack_code(&bc, &dontcare, 3, 1, 0);
+	} else if (u1 == 1 && u2 == 1 && cu != 1) {
+		unpack_code(&bc, &L[0][0], 9, 1, 0);
+		unpack_code(&bc, &L[1][0], 9, 1, 0);
+		unpack_code(&bc, &L[2][0], 8, 1, 0);
+		unpack_code(&bc, &L[2][1], 6, 1, 0);
+		unpack_code(&bc, &L[2][2], 5, 1, 0);
+		unpack_code(&bc, &L[2][3], 5, 1, 0);
+	} else if (u1 == 1 && u2 != 1 && cu == 1) {
+		unpack_code(&bc, &L[0][0], 9, 1, 0);
+		unpack_code(&bc, &L[1][0], 8, 1, 0);
+		unpack_code(&bc, &L[1][1], 6, 1, 0);
+		unpack_code(&bc, &L[1][2], 5, 1, 0);
+		unpack_code(&bc, &L[1][3], 5, 1, 0);
+		unpack_code(&bc, &L[2][0], 9, 1, 0);
+	} else if (u1 != 1 && u2 == 1 && cu == 1) {
+		unpack_code(&bc, &L[0][0], 8, 1, 0);
+		unpack_code(&bc, &L[0][1], 6, 1, 0);
+		unpack_code(&bc, &L[0][2], 5, 1, 0);
+		unpack_code(&bc, &L[0][3], 5, 1, 0);
+		unpack_code(&bc, &L[1][0], 9, 1, 0);
+		unpack_code(&bc, &L[2][0], 9, 1, 0);
+	} else {
+		const bool vvu = (u1 != 1 && u2 != 1 && cu == 1);
+		if (vvu) {
+			unpack_code(&bc, &L[0][0], 9, 1, 0);
+		} else {
+			unpack_code(&bc, &L[0][0], 8, 1, 0);
+			unpack_code(&bc, &L[0][1], 6, 1, 0);
+			unpack_code(&bc, &L[0][2], 5, 1, 0);
+			unpack_code(&bc, &L[0][3], 5, 1, 0);
+		}
+		unpack_code(&bc, &L[1][0], 4, 1, 0);
+		if (vvu) {
+			unpack_code(&bc, &L[2][0], 8, 1, 0);
+			unpack_code(&bc, &L[2][1], 6, 1, 0);
+			unpack_code(&bc, &L[2][2], 6, 1, 0);
+			unpack_code(&bc, &L[2][3], 6, 1, 0);
+			unpack_code(&bc, &dontcare, 3, 1, 0);
+		} else {
+			unpack_code(&bc, &L[2][0], 8, 1, 0);
+			unpack_code(&bc, &L[2][1], 6, 1, 0);
+		}
+	}
+	unpack_code(&bc, &q->gain_index[0], 10, 1, 0);
+	for (int i = 0; i < NF; i++)
+		if (!q->uv_flag[i])
+			unpack_code(&bc, &q->bpvc_index[i], 2, 1, 0);
+	if (cnt == 2) {
+		unpack_code(&bc, &prot_bp1, 2, 1, 0);
+	} else if (cnt == 1) {
+		unpack_code(&bc, &prot_bp2, 2, 1, 0);
+		unpack_code(&bc, &prot_bp1, 2, 1, 0);
+	} else if (cnt == 0) {
+		for (int i = 0; i < NF; i++)
+			unpack_code(&bc, &q->bpvc_index[i], 2, 1, 0);
+	}
+	unpack_code(&bc, &q->fs_index, 8, 1, 0);
+	unpack_code(&bc, &q->jit_index[0], 1, 1, 0);
+	erase = low_rate_fec_decode(q, erase, lsp_check);
+
+	/* pitch */
+	if (fl_pitch == 1) {
+		if (cnt == 0) {
+			for (int i = 0; i < NF; i++)
+				par[i].pitch = LOG_UV_PITCH_Q12;
+		} else if (cnt == 1) {
+			for (int i = 0; i < NF; i++) {
+				if (!par[i].uv_flag)
+					par[i].pitch = quant_u_dec(q->pitch_index, 5329, 9028, 25088, 7);
+				else
+					par[i].pitch = LOG_UV_PITCH_Q12;
+				par[i].pitch = pow10_fxp(par[i].pitch, 7);
+			}
+		} else {
+			const int16_t *cb = cnt == NF ? TB(pitch_vq_cb_vvv) : TB(pitch_vq_cb_uvv);
+			int k = q->pitch_index;
+			for (int i = 0; i < NF; i++)
+				par[i].pitch = par[i].uv_flag == 1 ? (int16_t) UV_PITCH_Q7
+								   : pow10_fxp(cb[k * NF + i], 7);
+		}
+	} else if (fl_pitch == 2) {
+		const int16_t *cb = TB(pitch_vq_cb_uvv);
+		int k = q->pitch_index;
+		for (int i = 0; i < NF; i++)
+			par[i].pitch = pow10_fxp(cb[k * NF + i], 7);
+	}
+
+	/* LSF */
+	const int16_t *cb_uv = TB(lsp_uv_9), *cb_v = TB(lsp_v_256x64x32x32);
+	if (fl_lsp) {
+		if (u1 == 1 && u2 == 1 && cu == 1) {
+			for (int f = 0; f < NF; f++)
+				deqnt_msvq(par[f].lsf, cb_uv, 1, uv_cb_size, L[f], LPC_ORD);
+		} else if (u1 == 1 && u2 == 1 && cu != 1) {
+			deqnt_msvq(par[0].lsf, cb_uv, 1, uv_cb_size, L[0], LPC_ORD);
+			deqnt_msvq(par[1].lsf, cb_uv, 1, uv_cb_size, L[1], LPC_ORD);
+			deqnt_msvq(par[2].lsf, cb_v, 4, v_cb_size, L[2], LPC_ORD);
+		} else if (u1 == 1 && u2 != 1 && cu == 1) {
+			deqnt_msvq(par[0].lsf, cb_uv, 1, uv_cb_size, L[0], LPC_ORD);
+			deqnt_msvq(par[1].lsf, cb_v, 4, v_cb_size, L[1], LPC_ORD);
+			deqnt_msvq(par[2].lsf, cb_uv, 1, uv_cb_size, L[2], LPC_ORD);
+		} else if (u1 != 1 && u2 == 1 && cu == 1) {
+			deqnt_msvq(par[0].lsf, cb_v, 4, v_cb_size, L[0], LPC_ORD);
+			deqnt_msvq(par[1].lsf, cb_uv, 1, uv_cb_size, L[1], LPC_ORD);
+			deqnt_msvq(par[2].lsf, cb_uv, 1, uv_cb_size, L[2], LPC_ORD);
+		} else {
+			const bool vvu = (u1 != 1 && u2 != 1 && cu == 1);
+			if (vvu)
+				deqnt_msvq(par[2].lsf, cb_uv, 1, uv_cb_size, L[0], LPC_ORD);
+			else
+				deqnt_msvq(par[2].lsf, cb_v, 4, v_cb_size, L[0], LPC_ORD);
+			const int16_t *ic = TB(inpCoef) + L[1][0] * 20;
+			for (int j = 0; j < LPC_ORD; j++) {
+				Word16 f = ic[j];
+				Word32 acc = L_mult(f, D->rd_qplsp[j]);
+				acc = L_mac(acc, sub(16384, f), par[2].lsf[j]);
+				il1[j] = extract_h(L_shl(acc, 1));
+				f = ic[j + LPC_ORD];
+				acc = L_mult(f, D->rd_qplsp[j]);
+				acc = L_mac(acc, sub(16384, f), par[2].lsf[j]);
+				il2[j] = extract_h(L_shl(acc, 1));
+			}
+			deqnt_msvq(res, TB(res256x64x64x64), vvu ? 4 : 2, res_cb_size, L[2], 20);
+			for (int i = 0; i < LPC_ORD; i++) {
+				par[0].lsf[i] = add(shr(res[i], 2), il1[i]);
+				par[1].lsf[i] = add(shr(res[i + LPC_ORD], 2), il2[i]);
+			}
+		}
+		if (u1 == 1 && u2 == 1 && cu == 1) {
+			const int c0 = lsp_check[0], c1 = lsp_check[1], c2 = lsp_check[2];
+			for (int i = 0; i < LPC_ORD; i++) {
+				if (c0 == 1 && c1 == 1 && c2 == 1) {
+					par[0].lsf[i] = par[1].lsf[i] = par[2].lsf[i] = prev->lsf[i];
+				} else if (c0 == 1 && c1 == 1 && c2 == 0) {
+					par[0].lsf[i] = add(mult(prev->lsf[i], 21845), mult(par[2].lsf[i], 10923));
+					par[1].lsf[i] = add(mult(prev->lsf[i], 10923), mult(par[2].lsf[i], 21845));
+				} else if (c0 == 1 && c1 == 0 && c2 == 1) {
+					par[0].lsf[i] = add(shr(prev->lsf[i], 1), shr(par[1].lsf[i], 1));
+					par[2].lsf[i] = par[1].lsf[i];
+				} else if (c0 == 0 && c1 == 1 && c2 == 1) {
+					par[1].lsf[i] = par[0].lsf[i];
+					par[2].lsf[i] = par[0].lsf[i];
+				} else if (c0 == 1 && c1 == 0 && c2 == 0) {
+					par[0].lsf[i] = add(shr(prev->lsf[i], 1), shr(par[1].lsf[i], 1));
+				} else if (c0 == 0 && c1 == 1 && c2 == 0) {
+					par[1].lsf[i] = add(shr(par[0].lsf[i], 1), shr(par[2].lsf[i], 1));
+				} else if (c0 == 0 && c1 == 0 && c2 == 1) {
+					par[2].lsf[i] = par[1].lsf[i];
+				}
+			}
+		}
+		for (int f = 0; f < NF; f++)
+			if (!lspStable(par[f].lsf, LPC_ORD))
+				lspSort(par[f].lsf, LPC_ORD);
+		v_copy(D->rd_qplsp, par[NF - 1].lsf, LPC_ORD);
+	} else {
+		for (int i = 0; i < NF; i++)
+			v_copy(par[i].lsf, prev->lsf, LPC_ORD);
+		v_copy(D->rd_qplsp, par[NF - 1].lsf, LPC_ORD);
+	}
+
+	/* gain, bandpass voicing, Fourier magnitudes, jitter */
+	const int16_t *gcb = TB(gain_vq_cb) + q->gain_index[0] * NUM_GAINFR * NF;
+	for (int i = 0; i < NF; i++)
+		for (int j = 0; j < NUM_GAINFR; j++)
+			par[i].gain[j] = gcb[i * NUM_GAINFR + j];
+	for (int i = 0; i < NF; i++)
+		q_bpvc_dec(par[i].bpvc, TB(inv_bp_index_map)[q->bpvc_index[i]], q->uv_flag[i],
+			   NUM_BANDS);
+	if (cnt != 0) {
+		v_copy(par[last].fs_mag, TB(fsvq_cb) + NUM_HARM * q->fs_index, NUM_HARM);
+		v_copy(wfs, par[last].fs_mag, NUM_HARM);
+	}
+	if (cnt > 1) {
+		if (D->rd_prev_uv) {
+			for (int i = 0; i < last; i++)
+				if (!par[i].uv_flag)
+					v_copy(par[i].fs_mag, par[last].fs_mag, NUM_HARM);
+		} else if (par[0].uv_flag) {
+			v_copy(par[1].fs_mag, par[last].fs_mag, NUM_HARM);
+		} else if (par[1].uv_flag) {
+			v_copy(par[0].fs_mag, D->rd_prev_fsmag, NUM_HARM);
+		} else if (par[2].uv_flag) {
+			for (int i = 0; i < NUM_HARM; i++)
+				par[0].fs_mag[i] = add(shr(wfs[i], 1), shr(D->rd_prev_fsmag[i], 1));
+		} else {
+			for (int i = 0; i < NUM_HARM; i++) {
+				Word16 p = D->rd_prev_fsmag[i], v = wfs[i];
+				par[0].fs_mag[i] = add(mult(p, 21845), mult(v, 10923));
+				par[1].fs_mag[i] = add(mult(p, 10923), mult(v, 21845));
+			}
+		}
+	}
+	D->rd_prev_uv = par[NF - 1].uv_flag;
+	if (par[NF - 1].uv_flag) {
+		v_set(D->rd_prev_fsmag, 8192, NUM_HARM);
+		window_Q(D->rd_prev_fsmag, g_der.w_fs, D->rd_prev_fsmag, NUM_HARM, 14);
+	} else {
+		v_copy(D->rd_prev_fsmag, par[NF - 1].fs_mag, NUM_HARM);
+	}
+	for (int i = 0; i < NF; i++)
+		par[i].jitter = par[i].uv_flag == 1 ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;
+	if (cnt != 0 || !(u1 == 0 && u2 == 1 && cu == 0)) {
+		if (q->jit_index[0] == 1) {
+			if (u1 && u2 && cu)
+				;
+			else if (u1 && u2 && !cu)
+				par[2].jitter = MAX_JITTER_Q15;
+			else if (u1 && !u2 && cu)
+				par[1].jitter = MAX_JITTER_Q15;
+			else if (!u1 && u2 && cu)
+				par[0].jitter = MAX_JITTER_Q15;
+			else if (u1 && !u2 && !cu)
+				par[1].jitter = MAX_JITTER_Q15;
+			else if (!u1 && u2 && !cu)
+				;
+			else if (!u1 && !u2 && cu)
+				par[1].jitter = MAX_JITTER_Q15;
+			else
+				par[0].jitter = par[1].jitter = par[2].jitter = MAX_JITTER_Q15;
+		}
+	}
+
+	/* smoothing on parity errors / gain jumps (melp_chn.c:1268-1325) */
+	const Word16 SM = 16383, SM1 = sub(32767, 16383);
+	if (flag_parity) {
+		Word16 p = prev->pitch;
+		for (int i = 0; i < NF; i++) {
+			if (par[i].uv_flag)
+				par[i].pitch = UV_PITCH_Q7;
+			else
+				par[i].pitch = add(mult(SM, p), mult(SM1, par[i].pitch));
+			p = par[i].pitch;
+		}
+		p = prev->gain[1];
+		for (int i = 0; i < NF; i++)
+			for (int j = 0; j < NUM_GAINFR; j++) {
+				par[i].gain[j] = add(mult(SM, p), mult(SM1, par[i].gain[j]));
+				p = par[i].gain[j];
+			}
+		for (int j = 0; j < LPC_ORD; j++) {
+			p = prev->lsf[j];
+			for (int i = 0; i < NF; i++) {
+				par[i].lsf[j] = add(mult(SM, p), mult(SM1, par[i].lsf[j]));
+				p = par[i].lsf[j];
+			}
+		}
+	} else {
+		Word32 s1 = 0, s2 = 0;
+		for (int i = 0; i < 2 * NF * NUM_GAINFR; i++)
+			s1 = L_add(s1, L_deposit_l(D->rd_prev_gain[i]));
+		s1 = L_shr(s1, 1);
+		for (int i = 0; i < NF; i++)
+			for (int j = 0; j < NUM_GAINFR; j++)
+				s2 = L_add(s2, L_deposit_l(par[i].gain[j]));
+		if (s2 > L_add(s1, 92160L) || s2 < L_sub(s1, 92160L)) {
+			s1 = L_mpy_ls(L_shr(s1, 1), 10923);
+			Word16 t = extract_l(s1);
+			for (int i = 0; i < NF; i++)
+				for (int j = 0; j < NUM_GAINFR; j++) {
+					par[i].gain[j] = add(mult(SM, t), mult(SM1, par[i].gain[j]));
+					t = par[i].gain[j];
+				}
+		}
+	}
+	for (int i = 0; i < NF * NUM_GAINFR; i++)
+		D->rd_prev_gain[i] = D->rd_prev_gain[i + NF * NUM_GAINFR];
+	for (int i = 0; i < NF; i++)
+		for (int j = 0; j < NUM_GAINFR; j++)
+			D->rd_prev_gain[NF * NUM_GAINFR + i * NUM_GAINFR + j] = par[i].gain[j];
+
+	if (erase) {
+		for (int i = 0; i < NF; i++) {
+			par[i].pitch = UV_PITCH_Q7;
+			v_copy(par[i].lsf, prev->lsf, LPC_ORD);
+			par[i].gain[0] = par[i].gain[1] = prev->gain[1];
+			v_zero(par[i].bpvc, NUM_BANDS);
+			v_set(par[i].fs_mag, 8192, NUM_HARM);
+			par[i].jitter = MAX_JITTER_Q15;
+		}
+		v_copy(D->rd_qplsp, par[NF - 1].lsf, LPC_ORD);
+		D->rd_prev_uv = 1;
+		v_set(D->rd_prev_fsmag, 8192, NUM_HARM);
+	} else if (erase_uuu) {
+		for (int i = 0; i < NF; i++) {
+			par[i].pitch = UV_PITCH_Q7;
+			v_zero(par[i].bpvc, NUM_BANDS);
+			v_set(par[i].fs_mag, 8192, NUM_HARM);
+			par[i].jitter = MAX_JITTER_Q15;
+		}
+		D->rd_prev_uv = 1;
+		v_set(D->rd_prev_fsmag, 8192, NUM_HARM);
+	} else if (erase_vvv) {
+		for (int i = 0; i < NF; i++) {
+			v_zero(&par[i].bpvc[1], NUM_BANDS - 1);
+			v_set(par[i].fs_mag, 8192, NUM_HARM);
+		}
+		D->rd_prev_uv = 0;
+		v_set(D->rd_prev_fsmag, 8192, NUM_HARM);
+	}
+	return erase;
+}
+
+/* ------------------------------------------------------------------ */
+/* harmonic excitation, melpe/harm.c                                   */
+/* ------------------------------------------------------------------ */
+
+/* realIDFT :63 -- direct real inverse DFT of one pitch period */
+MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
+{
+	int16_t c[PITCHMAX];
+	Word16 len2 = add(shr(len, 1), 1);
+	Word16 w = divide_s(16, len);	/* TWO_Q3 */
+	for (int i = 0; i < len; i++) {
+		Word32 L = L_mult(w, (Word16) i);
+		if (L > 524288L)
+			L = L_sub(1048576L, L);
+		else if (L == 524288L)
+			L = L_sub(L, 1);
+		c[i] = cos_fxp(extract_l(L_shr(L, 4)));
+	}
+	w = shr(w, 1);
+	Word16 w2 = shr(w, 1);
+	mag[0] = mult(mag[0], w2);
+	Word16 t = sub(len2, 1);
+	int i;
+	for (i = 1; i < t; i++)
+		mag[i] = mult(mag[i], w);
+	if (shl((Word16) i, 1) == len)
+		mag[i] = mult(mag[i], w2);
+	else
+		mag[i] = mult(mag[i], w);
+	for (i = 0; i < len; i++) {
+		Word32 L = L_deposit_h(mag[0]);
+		Word16 k = (Word16) i;
+		for (int j = 1; j < len2; j++) {
+			k = add(k, phase[j]);
+			while (k < 0)
+				k = add(k, len);
+			while (k >= len)
+				k = sub(k, len);
+			L = L_mac(L, mag[j], c[k]);
+			k = sub(k, phase[j]);
+			k = add(k, (Word16) i);
+		}
+		sig[i] = r_ound(L);
+	}
+}
+
+/* set_fc :145 -- mixed-excitation cutoff from the voicing pattern */
+MD Word16 set_fc(int16_t *bpvc)
+{
+	/* syn_bp_map of the reference (harm.c:150-153), in Hz */
+	const int16_t map[16] = {500, 500, 500, 500, 500, 500, 500, 4000,
+				 1000, 1000, 1000, 4000, 2000, 3000, 3000, 4000};
+	if (bpvc[0] < 8192)
+		return 0;
+	int k = 0;
+	bpvc[0] = 16384;
+	for (int i = 1; i < NUM_BANDS; i++) {
+		k <<= 1;
+		if (bpvc[i] > 8192) {
+			bpvc[i] = 16384;
+			k |= 1;
+		} else {
+			bpvc[i] = 0;
+		}
+	}
+	return (Word16) (map[k] << 3);
+}
+
+/* harm_syn_pitch :192 */
+MN void harm_syn_pitch(DecState *D, const int16_t *amp, int16_t *sig, Word16 fc, Word16 len)
+{
+	int16_t rnd[129], mag[129], phase[129];
+	Word16 fc1, fc2, factor;
+	v_zero(phase, 129);
+	for (int i = 0; i < len / 2 + 1; i++)
+		rnd[i] = mult(len, rand_minstdgen(&D->seed));
+	if (fc <= 4000) {
+		fc1 = mult(13926, fc);
+		fc2 = mult(17203, fc);
+		factor = SW_MAX_;
+	} else if (fc <= 8000) {
+		fc1 = mult(15565, fc);
+		fc2 = mult(17203, fc);
+		factor = 29491;
+	} else if (fc <= 16000) {
+		fc1 = mult(16056, fc);
+		fc2 = mult(16712, fc);
+		factor = 26214;
+	} else if (fc <= 24000) {
+		fc1 = mult(15565, fc);
+		fc2 = mult(17203, fc);
+		factor = 24576;
+	} else {
+		fc1 = mult(15073, fc);
+		fc2 = shift_r(fc, -1);
+		factor = 22938;
+	}
+	Word16 t1 = divide_s(fc1, shl(8000, 2));
+	Word16 t2 = divide_s(fc2, shl(8000, 2));
+	Word16 vc = mult(t1, len);
+	Word16 mc = mult(t2, len);
+	Word16 tot = (Word16) ((len / 2) + 1);
+	v_copy(mag, amp, add(vc, 1));
+	t1 = 0;
+	t2 = shr(extract_l(L_mult(1, len)), 1);
+	while (t2 >= 2 * len)
+		t2 = sub(t2, (Word16) (2 * len));
+	for (int i = 0; i < mc + 1; i++) {
+		phase[i] = shr(t1, 1);
+		t1 = add(t1, t2);
+		if (t1 >= 2 * len)
+			t1 = sub(t1, (Word16) (2 * len));
+	}
+	int idx = 0;
+	for (Word16 i = add(vc, 1); i < add(mc, 1); i++, idx++) {
+		Word16 fn = divide_s(sub(i, vc), sub(mc, vc));
+		t1 = add(mult(factor, fn), sub(SW_MAX_, fn));
+		mag[i] = mult(amp[i], t1);
+		t2 = sub(phase[i], mult(fn, rnd[idx]));
+		if (t2 < 0)
+			t2 = add(t2, len);
+		phase[i] = t2;
+	}
+	for (Word16 i = add(mc, 1); i < tot; i++, idx++) {
+		mag[i] = mult(amp[i], factor);
+		t2 = negate(rnd[idx]);
+		if (t2 < 0)
+			t2 = add(t2, len);
+		phase[i] = t2;
+	}
+	realIDFT(mag, phase, sig, len);
+}
+
+/* ------------------------------------------------------------------ */
+/* postfilter, melpe/postfilt.c                                        */
+/* ------------------------------------------------------------------ */
+
+/* block energy in (mantissa, shift) form (postfilt.c:95-110 / 220-235) */
+MD Word16 pf_energy(const int16_t *sp, Word16 *sh_out)
+{
+	Word16 mx = 0;
+	for (int i = 0; i < FRAME; i++) {
+		Word16 t = abs_s(sp[i]);
+		if (mx < t)
+			mx = t;
+	}
+	Word16 ts = norm_s(mx);
+	Word32 sum = 0;
+	for (int i = 0; i < FRAME; i++) {
+		Word16 t = shl(sp[i], ts);
+		sum = L_add(sum, L_shr(L_mult(t, t), 8));
+	}
+	Word16 sh = sub(8, shl(ts, 1));
+	ts = norm_l(sum);
+	*sh_out = sub(sh, ts);
+	return extract_h(L_shl(sum, ts));
+}
+
+/* postfilt :60 */
+MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_t *cur_lsf)
+{
+	const int16_t syn_inp[4] = {4096, 12288, 20480, 28672};
+	int16_t synLPC[LPC_ORD], inplsf[LPC_ORD], synhp[45], m1o[LPC_ORD], m2o[LPC_ORD];
+	int16_t nokori[20];
+	Word16 sp_sh, op_sh, t, t1, t2;
+	Word32 L;
+	Word16 spE = pf_energy(sp, &sp_sh);
+	for (int i = 0; i < 4; i++) {
+		for (int j = 0; j < LPC_ORD; j++)
+			inplsf[j] = add(mult(prev_lsf[j], sub(SW_MAX_, syn_inp[i])),
+					mult(cur_lsf[j], syn_inp[i]));
+		lpc_lsp2pred(inplsf, synLPC, LPC_ORD);
+		t = mult(4915, synLPC[1]);
+		if (t > 2048)
+			t = 2048;
+		if (t < 0)
+			t = 0;
+		Word16 emph = shl(t, 3);
+		for (int j = 0; j < 45; j++) {
+			t = mult(emph, D->pf_hpm);
+			D->pf_hpm = sp[i * 45 + j];
+			synhp[j] = sub(D->pf_hpm, t);
+		}
+		if (i == 0) {
+			/* run the previous frame's filter over the first 20 samples for
+			 * the cross-fade tail */
+			v_copy(m1o, D->pf_mem1, LPC_ORD);
+			v_copy(m2o, D->pf_mem2, LPC_ORD);
+			for (int j = 0; j < 20; j++) {
+				L = 0;
+				for (int k = 0; k < LPC_ORD; k++)
+					L = L_add(L, L_mult(m1o[k], D->pf_aFIR[k]));
+				for (int k = LPC_ORD - 1; k > 0; k--)
+					m1o[k] = m1o[k - 1];
+				m1o[0] = synhp[j];
+				L = L_add(L, L_shl(L_deposit_l(synhp[j]), 13));
+				for (int k = 0; k < LPC_ORD; k++)
+					L = L_sub(L, L_mult(m2o[k], D->pf_aIIR[k]));
+				for (int k = LPC_ORD - 1; k > 0; k--)
+					m2o[k] = m2o[k - 1];
+				t1 = extract_l(L_shr(L, 13));
+				m2o[0] = t1;
+				t = sub(SW_MAX_, (Word16) (j * 1638));	/* window[j] */
+				t1 = mult(t, t1);
+				nokori[j] = extract_l(L_shr(L_mult(D->pf_gain, t1), 15));
+			}
+		}
+		t1 = 18678;	/* ALPH */
+		t2 = 24576;	/* BETA */
+		for (int j = 0; j < LPC_ORD; j++) {
+			D->pf_aFIR[j] = mult(synLPC[j], t1);
+			D->pf_aIIR[j] = mult(synLPC[j], t2);
+			t1 = mult(18678, t1);
+			t2 = mult(24576, t2);
+		}
+		for (int j = 0; j < 45; j++) {
+			L = 0;
+			for (int k = 0; k < LPC_ORD; k++)
+				L = L_add(L, L_mult(D->pf_mem1[k], D->pf_aFIR[k]));
+			for (int k = LPC_ORD - 1; k > 0; k--)
+				D->pf_mem1[k] = D->pf_mem1[k - 1];
+			D->pf_mem1[0] = synhp[j];
+			L = L_add(L, L_shl(L_deposit_l(synhp[j]), 13));
+			for (int k = 0; k < LPC_ORD; k++)
+				L = L_sub(L, L_mult(D->pf_mem2[k], D->pf_aIIR[k]));
+			for (int k = LPC_ORD - 1; k > 0; k--)
+				D->pf_mem2[k] = D->pf_mem2[k - 1];
+			L = L_shr(L, 13);
+			D->pf_mem2[0] = extract_l(L);
+			sp[i * 45 + j] = extract_l(L);
+		}
+	}
+	Word16 opE = pf_energy(sp, &op_sh);
+	if (op_sh >= -22) {
+		spE = shr(spE, 1);
+		sp_sh = add(sp_sh, 1);
+		Word16 ts = sub(sp_sh, op_sh);
+		if (ts & 1) {
+			spE = shr(spE, 1);
+			ts = add(ts, 1);
+		}
+		t = divide_s(spE, opE);
+		ts = shr(ts, 1);
+		t = sqrt_Q15(t);
+		ts = sub(ts, 1);
+		D->pf_gain = shl(t, ts);
+	} else {
+		D->pf_gain = 0;
+	}
+	for (int i = 0; i < FRAME; i++)
+		sp[i] = extract_l(L_shr(L_mult(D->pf_gain, sp[i]), 15));
+	for (int i = 0; i < 20; i++)
+		sp[i] = add(mult(sp[i], (Word16) (i * 1638)), nokori[i]);
+	v_scale(sp, 29088, FRAME);
+	iir_2nd_d(sp, TB(lpf3500_den), TB(lpf3500_num), sp, D->lpf_din, D->lpf_dhi, D->lpf_dlo,
+		  FRAME);
+	iir_2nd_d(sp, TB(hpf60_den), TB(hpf60_num), sp, D->hpf_din, D->hpf_dhi, D->hpf_dlo, FRAME);
+}
+
+/* ------------------------------------------------------------------ */
+/* melp_syn :160 -- pitch-synchronous synthesis of one frame          */
+/* ------------------------------------------------------------------ */
+MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
+{
+	const int BEGIN = DISP_ORD;	/* max(MIX_ORD, DISP_ORD) */
+	int16_t fs_real[PITCHMAX], refc[LPC_ORD], sb[BEGIN + PITCHMAX];
+	int16_t lsf[LPC_ORD], lpc[LPC_ORD + 1], ase_num[LPC_ORD + 1], ase_den[LPC_ORD];
+	int16_t cur_p[MIX_ORD + 1], cur_n[MIX_ORD + 1], pul[MIX_ORD + 1], noi[MIX_ORD + 1];
+	int16_t tilt_cof[2];
+	MelpParam *prev = &D->prev_par;
+	Word16 t1, t2;
+	if (!D->syn_started) {
+		D->noise_gain = par->gain[NUM_GAINFR - 1];
+		D->prev_tilt = 0;
+		v_zero(D->prev_pcof, MIX_ORD + 1);
+		v_zero(D->prev_ncof, MIX_ORD + 1);
+		D->prev_ncof[MIX_ORD / 2] = SW_MAX_;
+		v_zero(D->disp_del, DISP_ORD);
+		v_zero(D->ase_del, LPC_ORD);
+		v_zero(D->tilt_del, 1);
+		D->syn_started = 1;
+	} else if (!D->erase) {
+		for (int i = 0; i < NUM_GAINFR; i++) {
+			noise_est(par->gain[i], &D->noise_gain, 17691, -17749, 2560, 20480);
+			noise_sup(&par->gain[i], D->noise_gain, 5120, 1536, 768);
+		}
+	}
+	if (par->uv_flag) {
+		v_set(par->fs_mag, 8192, NUM_HARM);
+		par->pitch = UV_PITCH_Q7;
+		par->jitter = 8192;	/* X025_Q15 */
+	}
+	if (!par->uv_flag && !D->erase)
+		window_Q(par->fs_mag, g_der.w_fs_inv, par->fs_mag, NUM_HARM, 14);
+	lpc_clmp(par->lsf, 409, LPC_ORD);
+	tilt_cof[0] = SW_MAX_;
+	lpc_lsp2pred(par->lsf, &lpc[1], LPC_ORD);
+	Word16 lpc_gain = lpc_pred2refl(&lpc[1], refc, LPC_ORD);
+	lpc_gain = sqrt_fxp(lpc_gain, 15);
+	Word16 cur_tilt = (refc[0] < 0) ? shr(refc[0], 1) : (Word16) 0;
+	t1 = shr(prev->pitch, 1);
+	t2 = add(1536, prev->gain[NUM_GAINFR - 1]);
+	if (par->pitch < t1 && par->gain[0] > t2)
+		prev->pitch = par->pitch;
+	v_zero(cur_p, MIX_ORD + 1);
+	v_zero(cur_n, MIX_ORD + 1);
+	const int16_t *bpc = TB(bp_cof);
+	for (int i = 0; i < NUM_BANDS; i++) {
+		if (par->bpvc[i] > 8192)
+			v_add(cur_p, bpc + i * (MIX_ORD + 1), MIX_ORD + 1);
+		else
+			v_add(cur_n, bpc + i * (MIX_ORD + 1), MIX_ORD + 1);
+	}
+	while (D->syn_begin < FRAME) {
+		Word16 sb0 = D->syn_begin;
+		Word16 ifact = divide_s(sb0, FRAME);
+		Word16 gcnt, ifg, gain, intfact;
+		if (sb0 >= 90) {
+			gcnt = 2;
+			ifg = divide_s(sub(sb0, 90), 90);
+		} else {
+			gcnt = 1;
+			ifg = divide_s(sb0, 90);
+		}
+		Word32 La = L_mult(par->gain[gcnt - 1], ifg);
+		Word32 Lb = L_mult(gcnt > 1 ? par->gain[gcnt - 2] : prev->gain[NUM_GAINFR - 1],
+				   sub(SW_MAX_, ifg));
+		gain = extract_h(L_add(La, Lb));
+		t1 = sub(par->gain[NUM_GAINFR - 1], prev->gain[NUM_GAINFR - 1]);
+		if (abs_s(t1) > 1536) {
+			t2 = sub(gain, prev->gain[NUM_GAINFR - 1]);
+			if ((t2 > 0 && t1 < 0) || (t2 < 0 && t1 > 0)) {
+				intfact = 0;
+			} else {
+				t1 = abs_s(t1);
+				t2 = abs_s(t2);
+				intfact = (t2 >= t1) ? (Word16) SW_MAX_ : divide_s(t2, t1);
+			}
+		} else {
+			intfact = ifact;
+		}
+		interp_array(prev->lsf, par->lsf, lsf, intfact, LPC_ORD);
+		lpc_lsp2pred(lsf, &lpc[1], LPC_ORD);
+		Word16 sig_prob = lin_int_bnd(gain, add(D->noise_gain, 3072), add(D->noise_gain, 7680),
+					      0, SW_MAX_);
+		ase_num[0] = 4096;
+		lpc_bwex(&lpc[1], &ase_num[1], mult(sig_prob, 16384), LPC_ORD);
+		lpc_bwex(&lpc[1], ase_den, mult(sig_prob, 26214), LPC_ORD);
+		Word16 if1 = sub(SW_MAX_, intfact);
+		t1 = add(mult(cur_tilt, intfact), mult(D->prev_tilt, if1));
+		tilt_cof[1] = mult(sig_prob, t1);
+		t1 = add(mult(lpc_gain, intfact), mult(D->prev_lpc_gain, if1));
+		Word16 syn_gain = mult(32000, t1);
+		Word16 pitch = add(mult(par->pitch, intfact), mult(prev->pitch, if1));
+		Word16 pulse_gain = extract_h(L_shl(L_mult(syn_gain, sqrt_fxp(pitch, 7)), 4));
+		t1 = sqrt_fxp(ifact, 15);
+		interp_array(D->prev_pcof, cur_p, pul, t1, MIX_ORD + 1);
+		interp_array(D->prev_ncof, cur_n, noi, t1, MIX_ORD + 1);
+		Word16 fc_prev = set_fc(prev->bpvc);
+		Word16 fc_cur = set_fc(par->bpvc);
+		t2 = sub(SW_MAX_, t1);
+		Word16 fc = add(mult(t1, fc_cur), mult(t2, fc_prev));
+		Word16 jitter = add(mult(par->jitter, ifact), mult(prev->jitter, sub(SW_MAX_, ifact)));
+		gain = mult(26214, gain);	/* X005_Q19 */
+		int16_t r;
+		rand_num(&r, SW_MAX_, 1, &D->seed);
+		t1 = shr(mult(jitter, r), 1);
+		t1 = mult(pitch, sub(16384, t1));
+		Word16 len = shift_r(t1, -6);
+		if (len < PITCHMIN)
+			len = PITCHMIN;
+		if (len > PITCHMAX)
+			len = PITCHMAX;
+		v_set(fs_real, 8192, len);
+		fs_real[0] = 0;
+		interp_array(prev->fs_mag, par->fs_mag, &fs_real[1], intfact, NUM_HARM);
+		harm_syn_pitch(D, fs_real, &sb[BEGIN], fc, len);
+		v_scale(&sb[BEGIN], pulse_gain, len);
+		v_copy(&sb[BEGIN - LPC_ORD], D->ase_del, LPC_ORD);
+		lpc_syn(&sb[BEGIN], &sb[BEGIN], ase_den, LPC_ORD, len);
+		v_copy(D->ase_del, &sb[BEGIN + len - LPC_ORD], LPC_ORD);
+		zerflt(&sb[BEGIN], ase_num, &sb[BEGIN], LPC_ORD, len);
+		v_copy(&sb[BEGIN - 1], D->tilt_del, 1);
+		v_copy(D->tilt_del, &sb[len + BEGIN - 1], 1);
+		zerflt_Q(&sb[BEGIN], tilt_cof, &sb[BEGIN], 1, len, 15);
+		v_copy(&sb[BEGIN - LPC_ORD], D->lpc_del, LPC_ORD);
+		lpc_syn(&sb[BEGIN], &sb[BEGIN], &lpc[1], LPC_ORD, len);
+		v_copy(D->lpc_del, &sb[len + BEGIN - LPC_ORD], LPC_ORD);
+		scale_adj(D, &sb[BEGIN], gain, len, 10, 26214);
+		v_copy(&sb[BEGIN - DISP_ORD], D->disp_del, DISP_ORD);
+		v_copy(D->disp_del, &sb[len + BEGIN - DISP_ORD], DISP_ORD);
+		zerflt_Q(&sb[BEGIN], TB(disp_cof), &sb[BEGIN], DISP_ORD, len, 15);
+		if (add(sb0, len) >= FRAME) {
+			v_copy(&out[sb0], &sb[BEGIN], FRAME - sb0);
+			postfilt(D, out, prev->lsf, par->lsf);
+			v_copy(D->sigsave, &sb[BEGIN + FRAME - sb0], len - (FRAME - sb0));
+		} else {
+			v_copy(&out[sb0], &sb[BEGIN], len);
+		}
+		D->syn_begin = add(sb0, len);
+	}
+	v_copy(D->prev_pcof, cur_p, MIX_ORD + 1);
+	v_copy(D->prev_ncof, cur_n, MIX_ORD + 1);
+	*prev = *par;
+	D->prev_tilt = cur_tilt;
+	D->prev_lpc_gain = lpc_gain;
+	D->syn_begin = sub(D->syn_begin, FRAME);
+}
+
+/* synthesis :110 -- melpe_s: D->chbuf (11 bytes) -> 540 samples */
+MN void decode_superframe(DecState *D, int16_t *out)
+{
+	if (D->syn_begin > 0) {
+		if (D->syn_begin > BLOCK) {	/* frameSize = 540 */
+			v_copy(out, D->sigsave, BLOCK);
+			v_copy(D->sigsave, &D->sigsave[BLOCK], D->syn_begin - BLOCK);
+		} else {
+			v_copy(out, D->sigsave, D->syn_begin);
+		}
+	}
+	D->erase = low_rate_chn_read(D);
+	for (int i = 0; i < NF; i++) {
+		melp_syn(D, &D->par[i], &out[i * FRAME]);
+		if (D->syn_begin > 0 && i < NF - 1)
+			v_copy(&out[(i + 1) * FRAME], D->sigsave, D->syn_begin);
+	}
+}
+
+}  // namespace mlp
+
+#endif

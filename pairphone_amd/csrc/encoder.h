@@ -371,6 +371,55 @@ MN void analysis(EncState *E, const int16_t *sp_in)
 	v_copy(E->hpspeech, &E->hpspeech[NF * FRAME], IN_BEG);
 }
 
+/* debug aid: analysis() stopped after `upto` of its stages (1 = dc_rmv +
+ * melp_ana, 2 = + sc_ana, 3 = + lsf_vq, 4 = + pitch/gain/jitter/bp,
+ * 5 = + Fourier magnitudes, 6 = + channel write) */
+MN void analysis_upto(EncState *E, const int16_t *sp_in, int upto)
+{
+	MelpParam *par = E->par;
+	int16_t lpc[LPC_ORD + 1];
+	for (int i = 0; i < NF; i++) {
+		dc_rmv(&sp_in[i * FRAME], &E->hpspeech[IN_BEG + i * FRAME], E->dcdelin,
+		       E->dcdelout_hi, E->dcdelout_lo, FRAME);
+		melp_ana(E, &E->hpspeech[i * FRAME], &par[i], i);
+	}
+	if (upto < 2)
+		return;
+	sc_ana(E, par);
+	if (upto < 3)
+		return;
+	lpc[0] = 4096;
+	lsf_vq(E, par);
+	if (upto < 4)
+		return;
+	pitch_vq(E, par);
+	gain_vq(E, par);
+	for (int i = 0; i < NF; i++)
+		quant_u(&par[i].jitter, &E->qpar.jit_index[i], 0, MAX_JITTER_Q15, 2, SW_MAX_,
+			true, 7);
+	quant_bp(E, par);
+	quant_jitter(E, par);
+	if (upto < 5)
+		return;
+	for (int i = 0; i < NF; i++) {
+		v_set(par[i].fs_mag, 8192, NUM_HARM);
+		if (!par[i].uv_flag) {
+			lpc_lsp2pred(par[i].lsf, &lpc[1], LPC_ORD);
+			zerflt(&E->hpspeech[i * FRAME + FRAME_END - LPC_FRAME / 2], lpc, E->sigbuf,
+			       LPC_ORD, LPC_FRAME);
+			window(E->sigbuf, TB(win_cof), E->sigbuf, LPC_FRAME);
+			find_harm(E->sigbuf, par[i].fs_mag, par[i].pitch, NUM_HARM, LPC_FRAME);
+		}
+	}
+	quant_fsmag(E, par);
+	if (upto < 6)
+		return;
+	for (int i = 0; i < NF; i++)
+		E->qpar.uv_flag[i] = par[i].uv_flag;
+	low_rate_chn_write(E);
+	v_copy(E->hpspeech, &E->hpspeech[NF * FRAME], IN_BEG);
+}
+
 /* melpe_a :91 -- sp (540) is denoised in place, then analysed; the 11-byte
  * frame is left in E->chbuf */
 MN void encode_superframe(EncState *E, NppScratch *w, int16_t *sp)

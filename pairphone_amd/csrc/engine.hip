@@ -95,6 +95,22 @@ __global__ __launch_bounds__(WAVE) void k_encode(EncState *enc, int16_t *sp, uin
 		bits[(size_t) c * 11 + k] = E->chbuf[k];
 }
 
+/* debug aid: encode with the pipeline cut after `upto` stages (0 = NPP only) */
+__global__ __launch_bounds__(WAVE) void k_encode_dbg(EncState *enc, int16_t *sp, int n, int upto)
+{
+	int c = blockIdx.x * WAVE + threadIdx.x;
+	if (c >= n)
+		return;
+	NppScratch w;
+	EncState *E = &enc[c];
+	int16_t *x = sp + (size_t) c * BLOCK;
+	npp_frame(&E->npp, &w, x, x);
+	npp_frame(&E->npp, &w, x + FRAME, x + FRAME);
+	npp_frame(&E->npp, &w, x + 2 * FRAME, x + 2 * FRAME);
+	if (upto > 0)
+		analysis_upto(E, x, upto);
+}
+
 __global__ __launch_bounds__(WAVE) void k_synth_seed(synth_state *s, uint32_t seed,
 						      uint32_t ch0, int n)
 {
@@ -411,6 +427,16 @@ int melpe_synth_host(uint32_t run_seed, uint32_t channel, int16_t *out, int samp
 	synth_state st;
 	synth_init(&st, synth_mix(run_seed, channel));
 	synth_block(&st, out, samples);
+	return 0;
+}
+
+int melpe_debug_encode_stage(melpe_engine *e, void *d_sp, int upto)
+{
+	HIPCHK(hipSetDevice(e->device));
+	k_encode_dbg<<<grid_for(e->channels), WAVE, 0, e->stream>>>(e->d_enc, (int16_t *) d_sp,
+								      e->channels, upto);
+	HIPCHK(hipGetLastError());
+	HIPCHK(hipStreamSynchronize(e->stream));
 	return 0;
 }
 

@@ -79,6 +79,17 @@ int emu_encode(emu_engine *e, unsigned char *bits, int16_t *sp)
 	return 0;
 }
 
+/* melpe_s on every channel: bits (C x 11) in, sp (C x 540) out */
+int emu_decode(emu_engine *e, int16_t *sp, const unsigned char *bits)
+{
+	for (int c = 0; c < e->channels; c++) {
+		DecState *D = &e->dec[c];
+		memcpy(D->chbuf, bits + c * 11, 11);
+		decode_superframe(D, sp + (size_t) c * BLOCK);
+	}
+	return 0;
+}
+
 /* per-superframe debug view of channel c: melp_par (3 x 30 int16) and
  * quant_par (30 int16), in the layout oracle/ref_tool.c dumps */
 int emu_enc_params(emu_engine *e, int c, int16_t *out)
@@ -105,6 +116,13 @@ int emu_enc_params(emu_engine *e, int c, int16_t *out)
 		w[k++] = q->msvq_index[i];
 	w[k++] = q->fsvq_index;
 	return k;
+}
+
+/* decoder's melp_par of channel c after the last superframe (3 x 30 int16) */
+int emu_dec_params(emu_engine *e, int c, int16_t *out)
+{
+	memcpy(out, e->dec[c].par, sizeof(e->dec[c].par));
+	return 90;
 }
 
 }  // extern "C"

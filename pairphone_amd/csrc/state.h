@@ -133,8 +133,35 @@ struct EncState {
 	uint8_t chbuf[12];
 };
 
+#define MIX_ORD 32
+#define DISP_ORD 64
+
 struct DecState {
-	int16_t dummy;
+	MelpParam par[NF];	/* melp_par: error paths read last superframe's */
+	QuantParam qpar;	/* quant_par: ditto (uv_flag, indices) */
+	/* melpe/melp_syn.c */
+	MelpParam prev_par;
+	int16_t sigsave[PITCHMAX];
+	int16_t syn_begin, erase;
+	int16_t syn_started, noise_gain, prev_lpc_gain, prev_tilt;
+	int16_t lpc_del[LPC_ORD], ase_del[LPC_ORD], tilt_del[1];
+	int16_t prev_pcof[MIX_ORD + 1], prev_ncof[MIX_ORD + 1];
+	int16_t disp_del[DISP_ORD];
+	/* melpe/melp_sub.c scale_adj */
+	int16_t prev_scale;
+	/* melpe/postfilt.c */
+	int16_t pf_hpm, pf_gain;
+	int16_t pf_mem1[LPC_ORD], pf_mem2[LPC_ORD];
+	int16_t pf_aFIR[LPC_ORD], pf_aIIR[LPC_ORD];
+	int16_t hpf_din[2], hpf_dhi[2], hpf_dlo[2];
+	int16_t lpf_din[2], lpf_dhi[2], lpf_dlo[2];
+	/* melpe/melp_chn.c low_rate_chn_read */
+	int16_t rd_started, rd_prev_uv;
+	int16_t rd_prev_fsmag[NUM_HARM], rd_qplsp[LPC_ORD];
+	int16_t rd_prev_gain[2 * NF * NUM_GAINFR];
+	uint8_t chbuf[12];
+	/* melpe/dsp_sub.c rand_minstdgen */
+	uint32_t seed;
 };
 
 /* melp_ana_init, melpe/melp_ana.c:475-506 (the part melpe_i re-runs) */
@@ -172,9 +199,36 @@ MD void enc_reset(EncState *e)
 	enc_melpe_i(e);
 }
 
+/* melp_syn_init, melpe/melp_syn.c:478-502 (the part melpe_i re-runs) */
+MD void dec_melpe_i(DecState *d)
+{
+	d->prev_par.gain[0] = d->prev_par.gain[1] = 0;
+	d->prev_par.pitch = UV_PITCH_Q7;
+	Word16 t = 0;
+	for (int i = 0; i < LPC_ORD; i++) {
+		t = add(t, 2979);
+		d->prev_par.lsf[i] = t;
+	}
+	d->prev_par.jitter = 0;
+	for (int i = 0; i < NUM_BANDS; i++)
+		d->prev_par.bpvc[i] = 0;
+	d->syn_begin = 0;
+	for (int i = 0; i < PITCHMAX; i++)
+		d->sigsave[i] = 0;
+	for (int i = 0; i < NUM_HARM; i++)
+		d->prev_par.fs_mag[i] = 8192;
+}
+
 MD void dec_reset(DecState *d)
 {
-	d->dummy = 0;
+	int16_t *p = (int16_t *) d;
+	for (unsigned i = 0; i < sizeof(DecState) / 2; i++)
+		p[i] = 0;
+	d->noise_gain = 2560;	/* melp_syn.c:165-166 */
+	d->prev_lpc_gain = SW_MAX_;
+	d->rd_prev_uv = 1;	/* melp_chn.c:460 */
+	d->seed = 1;	/* dsp_sub.c:369 */
+	dec_melpe_i(d);
 }
 
 }  // namespace mlp
