@@ -81,6 +81,12 @@ double melpe_last_kernel_ms(const melpe_engine *e);
 
 const char *melpe_last_error(void);
 
+/* Extension of the single-stream drop-in (include/melpe.h): return its one
+ * instance to the state of a freshly started reference process (melpe_i
+ * alone re-initialises only what melp_ana_init / melp_syn_init touch, as in
+ * the reference).  Lets one process host several independent sessions. */
+int melpe_single_reset(void);
+
 #ifdef __cplusplus
 }
 #endif

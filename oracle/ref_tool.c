@@ -18,6 +18,10 @@
  *   enc    <in.pcm> <out.bits> [<dump.bin>]
  *   dec    <in.bits> <out.pcm> [<dump.bin>]
  *   npp    <in.pcm> <out.pcm>
+ *   duplex <in.pcm> <in.bits> <out.bits> <out.pcm>
+ *          one process running melpe_a (on in.pcm) and melpe_s (on in.bits)
+ *          alternately, superframe by superframe, as a PairPhone endpoint
+ *          does: the two share melp_par / quant_par / chbuf
  *   encgen <seed> <ch0> <nch> <nsf> <out.bits> [<out.npp.pcm>]
  *          channel c = synth_mix(seed, c) signal, nsf superframes each,
  *          bitstreams concatenated channel-major (nch*nsf*11 bytes)
@@ -281,6 +285,30 @@ int main(int argc, char **argv)
 		fclose(f);
 		if (dump)
 			fclose(dump);
+		return 0;
+	}
+	if (!strcmp(argv[1], "duplex") && argc == 6) {
+		long plen, blen, k, nsf;
+		int16_t *pcm = (int16_t *) read_file(argv[2], &plen);
+		unsigned char *bits = (unsigned char *) read_file(argv[3], &blen);
+		FILE *fb, *fp;
+		int16_t out[BLOCK];
+		unsigned char buf[11];
+		nsf = plen / 2 / BLOCK;
+		if (blen / 11 < nsf)
+			nsf = blen / 11;
+		fb = fopen(argv[4], "wb");
+		fp = fopen(argv[5], "wb");
+		melpe_i();
+		for (k = 0; k < nsf; k++) {
+			melpe_a(buf, pcm + k * BLOCK);
+			fwrite(buf, 1, 11, fb);
+			memcpy(buf, bits + k * 11, 11);
+			melpe_s(out, buf);
+			fwrite(out, 2, BLOCK, fp);
+		}
+		fclose(fb);
+		fclose(fp);
 		return 0;
 	}
 	if (!strcmp(argv[1], "npp") && argc == 4) {

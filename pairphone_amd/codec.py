@@ -48,6 +48,7 @@ def load_library(path=None):
         "melpe_synth_host": (i32, [u32, u32, vp, i32]),
         "melpe_last_kernel_ms": (ctypes.c_double, [vp]),
         "melpe_last_error": (ctypes.c_char_p, []),
+        "melpe_single_reset": (i32, []),
         "melpe_i": (None, []),
         "melpe_a": (None, [vp, vp]),
         "melpe_s": (None, [vp, vp]),
@@ -164,6 +165,10 @@ class Melpe:
 
     def __init__(self):
         self.lib = load_library()
+
+    def reset_process_state(self):
+        """fresh-process state (melpe_single_reset extension)"""
+        _check(self.lib.melpe_single_reset())
 
     def melpe_i(self):
         self.lib.melpe_i()

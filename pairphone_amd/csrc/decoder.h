@@ -1093,14 +1093,10 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 /* synthesis :110 -- melpe_s: D->chbuf (11 bytes) -> 540 samples */
 MN void decode_superframe(DecState *D, int16_t *out)
 {
-	if (D->syn_begin > 0) {
-		if (D->syn_begin > BLOCK) {	/* frameSize = 540 */
-			v_copy(out, D->sigsave, BLOCK);
-			v_copy(D->sigsave, &D->sigsave[BLOCK], D->syn_begin - BLOCK);
-		} else {
-			v_copy(out, D->sigsave, D->syn_begin);
-		}
-	}
+	/* syn_begin < PITCHMAX <= BLOCK always, so the reference's "impossible"
+	 * syn_begin > frameSize branch (melp_syn.c:120-125) is not restated */
+	if (D->syn_begin > 0)
+		v_copy(out, D->sigsave, D->syn_begin);
 	D->erase = low_rate_chn_read(D);
 	for (int i = 0; i < NF; i++) {
 		melp_syn(D, &D->par[i], &out[i * FRAME]);

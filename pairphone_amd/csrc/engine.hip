@@ -66,6 +66,32 @@ __global__ __launch_bounds__(WAVE) void k_reset(EncState *enc, DecState *dec,
 		dec_reset(&dec[c]);
 }
 
+/*
+ * Private-segment guard.  On gfx950 a FLAT load/store is aperture-checked on
+ * its base register BEFORE the unsigned immediate offset is added.  Code that
+ * only sees a generic pointer (every __noinline__ callee) may fold p[i - k]
+ * into (p - k)[i] + offset:k, so a private object lying within 4 KiB of the
+ * bottom of the lane's private segment faults with MEMORY_APERTURE_VIOLATION
+ * (tools/exp/flat_private.hip, mode 2, reproduces it).  Every kernel that
+ * calls into the codec therefore owns exactly one private object whose first
+ * member is this guard; callee frames sit above the kernel frame, so no
+ * private object the codec touches starts below FLAT_GUARD_BYTES.
+ */
+#define FLAT_GUARD_BYTES 4608
+
+struct NppLane {
+	uint8_t guard[FLAT_GUARD_BYTES];
+	NppScratch w;
+};
+
+struct DecLane {
+	uint8_t guard[FLAT_GUARD_BYTES];
+	int16_t out[BLOCK];
+};
+
+/* keep the guard alive: the compiler may not drop or shrink the object */
+#define PIN_FRAME(obj) __asm__ volatile("" : : "v"(&(obj)) : "memory")
+
 /* melpe_n on `frames` frames per channel (melpe/melpe.c:63-67) */
 __global__ __launch_bounds__(WAVE) void k_npp(EncState *enc, int16_t *sp, int frames,
 					       int stride, const uint8_t *active, int n,
@@ -74,10 +100,11 @@ __global__ __launch_bounds__(WAVE) void k_npp(EncState *enc, int16_t *sp, int fr
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (c >= n || (active && !active[c]))
 		return;
-	NppScratch w;
+	NppLane L;
+	PIN_FRAME(L);
 	int16_t *x = sp + (size_t) c * stride;
 	for (int f = 0; f < frames; f++)
-		npp_frame(&enc[c].npp, &w, x + f * NPP_HOP, x + f * NPP_HOP, rate1200 != 0);
+		npp_frame(&enc[c].npp, &L.w, x + f * NPP_HOP, x + f * NPP_HOP, rate1200 != 0);
 }
 
 /* melpe_a on every active channel (melpe/melpe.c:91-99): one lane per
@@ -88,9 +115,10 @@ __global__ __launch_bounds__(WAVE) void k_encode(EncState *enc, int16_t *sp, uin
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (c >= n || (active && !active[c]))
 		return;
-	NppScratch w;
+	NppLane L;
+	PIN_FRAME(L);
 	EncState *E = &enc[c];
-	encode_superframe(E, &w, sp + (size_t) c * BLOCK);
+	encode_superframe(E, &L.w, sp + (size_t) c * BLOCK);
 	for (int k = 0; k < 11; k++)
 		bits[(size_t) c * 11 + k] = E->chbuf[k];
 }
@@ -101,14 +129,66 @@ __global__ __launch_bounds__(WAVE) void k_encode_dbg(EncState *enc, int16_t *sp,
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (c >= n)
 		return;
-	NppScratch w;
+	NppLane L;
+	PIN_FRAME(L);
 	EncState *E = &enc[c];
 	int16_t *x = sp + (size_t) c * BLOCK;
-	npp_frame(&E->npp, &w, x, x);
-	npp_frame(&E->npp, &w, x + FRAME, x + FRAME);
-	npp_frame(&E->npp, &w, x + 2 * FRAME, x + 2 * FRAME);
+	npp_frame(&E->npp, &L.w, x, x);
+	npp_frame(&E->npp, &L.w, x + FRAME, x + FRAME);
+	npp_frame(&E->npp, &L.w, x + 2 * FRAME, x + 2 * FRAME);
 	if (upto > 0)
 		analysis_upto(E, x, upto);
+}
+
+/* melpe_s on every active channel (melpe/melpe.c:102-107): bits (C x 11) in,
+ * sp (C x 540) out */
+__global__ __launch_bounds__(WAVE) void k_decode(DecState *dec, int16_t *sp,
+						  const uint8_t *bits, const uint8_t *active, int n)
+{
+	int c = blockIdx.x * WAVE + threadIdx.x;
+	if (c >= n || (active && !active[c]))
+		return;
+	DecLane L;
+	PIN_FRAME(L);
+	DecState *D = &dec[c];
+	for (int k = 0; k < 11; k++)
+		D->chbuf[k] = bits[(size_t) c * 11 + k];
+	decode_superframe(D, L.out);
+	int16_t *o = sp + (size_t) c * BLOCK;
+	for (int i = 0; i < BLOCK; i++)
+		o[i] = L.out[i];
+}
+
+/* melpe_i on channel 0 of the single-stream engine: melp_ana_init +
+ * melp_syn_init (melpe/melpe.c:72-88) */
+__global__ void k_melpe_i(EncState *enc, DecState *dec)
+{
+	if (threadIdx.x == 0) {
+		enc_melpe_i(enc);
+		dec_melpe_i(dec);
+	}
+}
+
+/* The reference's analysis and synthesis share melp_par, quant_par and chbuf
+ * (melpe/global.c:27-39).  For the single-stream drop-in the engine keeps
+ * them in EncState and hands them to the decoder around each melpe_s, so an
+ * interleaved melpe_a / melpe_s sequence sees exactly the reference's
+ * process-global state.  dir 0: encoder -> decoder, 1: decoder -> encoder. */
+__global__ void k_share_params(EncState *enc, DecState *dec, int dir)
+{
+	if (threadIdx.x != 0)
+		return;
+	if (dir == 0) {
+		for (int i = 0; i < NF; i++)
+			dec->par[i] = enc->par[i];
+		dec->qpar = enc->qpar;
+	} else {
+		for (int i = 0; i < NF; i++)
+			enc->par[i] = dec->par[i];
+		enc->qpar = dec->qpar;
+		for (int k = 0; k < 11; k++)
+			enc->chbuf[k] = dec->chbuf[k];
+	}
 }
 
 __global__ __launch_bounds__(WAVE) void k_synth_seed(synth_state *s, uint32_t seed,
@@ -389,14 +469,48 @@ int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const u
 	return 0;
 }
 
-int melpe_decode_host(melpe_engine *, int16_t *, const unsigned char *, const uint8_t *)
+static int decode_launch(melpe_engine *e, int16_t *d_sp, const unsigned char *d_bits,
+			 const uint8_t *d_act, hipStream_t s, bool sync)
 {
-	return fail_msg("decode: not built yet");
+	HIPCHK(hipSetDevice(e->device));
+	ev_begin(e, s);
+	k_decode<<<grid_for(e->channels), WAVE, 0, s>>>(e->d_dec, d_sp, d_bits, d_act,
+							  e->channels);
+	HIPCHK(hipGetLastError());
+	ev_end(e, s, sync);
+	return 0;
 }
 
-int melpe_decode_dev(melpe_engine *, void *, const void *, const void *, void *)
+int melpe_decode_dev(melpe_engine *e, void *d_sp, const void *d_bits, const void *d_active,
+		     void *hip_stream)
 {
-	return fail_msg("decode: not built yet");
+	if (!e || !d_sp || !d_bits)
+		return fail_msg("melpe_decode_dev: null argument");
+	return decode_launch(e, (int16_t *) d_sp, (const unsigned char *) d_bits,
+			     (const uint8_t *) d_active, (hipStream_t) hip_stream, false);
+}
+
+int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
+		      const uint8_t *active)
+{
+	if (!e || !bits || !sp)
+		return fail_msg("melpe_decode_host: null argument");
+	HIPCHK(hipSetDevice(e->device));
+	size_t pb = sizeof(int16_t) * BLOCK * (size_t) e->channels;
+	size_t bb = (size_t) 11 * e->channels;
+	int rc;
+	const uint8_t *m = stage_mask(e, active, &rc);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(e->d_bits, bits, bb, hipMemcpyHostToDevice, e->stream));
+	if (active)	/* inactive channels keep the caller's samples */
+		HIPCHK(hipMemcpyAsync(e->d_pcm, sp, pb, hipMemcpyHostToDevice, e->stream));
+	rc = decode_launch(e, e->d_pcm, e->d_bits, m, e->stream, true);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(sp, e->d_pcm, pb, hipMemcpyDeviceToHost, e->stream));
+	HIPCHK(hipStreamSynchronize(e->stream));
+	return 0;
 }
 
 int melpe_synth_seed(melpe_engine *e, uint32_t run_seed, uint32_t first_channel)
@@ -487,10 +601,21 @@ void melpe_n(short *sp)
 	}
 }
 
+int melpe_single_reset(void)
+{
+	melpe_engine *e = single_engine();
+	g_single_rate1200 = false;
+	return melpe_engine_reset(e, nullptr, 3);
+}
+
 void melpe_i(void)
 {
 	melpe_engine *e = single_engine();
-	(void) e;
+	k_melpe_i<<<1, WAVE, 0, e->stream>>>(e->d_enc, e->d_dec);
+	if (hipGetLastError() != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess) {
+		fprintf(stderr, "libmelpe_amd: melpe_i failed\n");
+		abort();
+	}
 	g_single_rate1200 = true;
 }
 
@@ -506,7 +631,15 @@ void melpe_a(unsigned char *buf, short *sp)
 void melpe_s(short *sp, unsigned char *buf)
 {
 	melpe_engine *e = single_engine();
-	if (melpe_decode_host(e, sp, buf, nullptr)) {
+	k_share_params<<<1, WAVE, 0, e->stream>>>(e->d_enc, e->d_dec, 0);
+	int rc = hipGetLastError() != hipSuccess;
+	if (!rc)
+		rc = melpe_decode_host(e, sp, buf, nullptr);
+	if (!rc) {
+		k_share_params<<<1, WAVE, 0, e->stream>>>(e->d_enc, e->d_dec, 1);
+		rc = hipGetLastError() != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess;
+	}
+	if (rc) {
 		fprintf(stderr, "libmelpe_amd: melpe_s failed: %s\n", g_err.c_str());
 		abort();
 	}

@@ -118,6 +118,23 @@ int emu_enc_params(emu_engine *e, int c, int16_t *out)
 	return k;
 }
 
+/* the single-stream engine's melp_par / quant_par / chbuf hand-over around
+ * melpe_s (engine.hip k_share_params), channel 0 */
+int emu_share(emu_engine *e, int dir)
+{
+	EncState *E = &e->enc[0];
+	DecState *D = &e->dec[0];
+	if (dir == 0) {
+		memcpy(D->par, E->par, sizeof(D->par));
+		D->qpar = E->qpar;
+	} else {
+		memcpy(E->par, D->par, sizeof(E->par));
+		E->qpar = D->qpar;
+		memcpy(E->chbuf, D->chbuf, 11);
+	}
+	return 0;
+}
+
 /* decoder's melp_par of channel c after the last superframe (3 x 30 int16) */
 int emu_dec_params(emu_engine *e, int c, int16_t *out)
 {

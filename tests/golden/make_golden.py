@@ -9,7 +9,9 @@ outputs (and, for small cases, the outputs themselves).
 
   npp.json   melpe_n over F frames per channel  (ref_tool npp)
   enc.json   melpe_a bitstreams, per channel     (ref_tool encgen)
-  dec.json   melpe_s PCM of those bitstreams     (ref_tool decgen)
+  dec_1024.json  melpe_s PCM of the enc_1024 bitstreams (ref_tool decgen)
+  dec_fuzz.json  melpe_s PCM of uniformly random bitstreams (FEC, parity and
+                 erasure paths), bits regenerated from numpy's PCG64(seed)
 """
 import hashlib
 import json
@@ -65,6 +67,32 @@ def make_enc(tmp, seed, channels, nsf, keep_bits=0):
     return out
 
 
+def make_dec(tmp, seed, channels, nsf):
+    bits = os.path.join(tmp, "d.bits")
+    ref("encgen", seed, 0, channels, nsf, bits)
+    pcm = os.path.join(tmp, "d.pcm")
+    ref("decgen", bits, channels, nsf, pcm)
+    y = np.fromfile(pcm, dtype=np.int16).reshape(channels, nsf * 540)
+    return {"seed": seed, "channels": channels, "superframes": nsf,
+            "pcm_sha256": [sha(y[c].tobytes()) for c in range(channels)]}
+
+
+def fuzz_bits(seed, channels, nsf):
+    return np.random.Generator(np.random.PCG64(seed)).integers(
+        0, 256, (channels, nsf * 11), dtype=np.uint8)
+
+
+def make_dec_fuzz(tmp, seed, channels, nsf):
+    bits = os.path.join(tmp, "f.bits")
+    fuzz_bits(seed, channels, nsf).tofile(bits)
+    pcm = os.path.join(tmp, "f.pcm")
+    ref("decgen", bits, channels, nsf, pcm)
+    y = np.fromfile(pcm, dtype=np.int16).reshape(channels, nsf * 540)
+    return {"seed": seed, "channels": channels, "superframes": nsf,
+            "pcm_sha256": [sha(y[c].tobytes()) for c in range(channels)],
+            "pcm0_first_sf": y[0, :540].tolist()}
+
+
 def main():
     if not os.path.exists(TOOL):
         sys.exit("oracle/_ref/ref_tool missing")
@@ -73,6 +101,10 @@ def main():
         if "enc" in which:
             json.dump(make_enc(tmp, 1, 1024, 149, keep_bits=8),
                       open(os.path.join(HERE, "enc_1024.json"), "w"))
+        if "dec" in which:
+            json.dump(make_dec(tmp, 1, 1024, 149), open(os.path.join(HERE, "dec_1024.json"), "w"))
+            json.dump(make_dec_fuzz(tmp, 77, 256, 200),
+                      open(os.path.join(HERE, "dec_fuzz.json"), "w"))
         if "npp" in which:
             json.dump(make_npp(tmp), open(os.path.join(HERE, "npp.json"), "w"), indent=1)
     print("ok")

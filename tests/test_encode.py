@@ -169,6 +169,7 @@ def test_single_stream_dropin_matches_golden():
     nsf = 60
     x = signals(g["seed"], 1, nsf)[0]
     m = Melpe()
+    m.reset_process_state()   # a fresh reference process per test
     m.melpe_i()
     out = []
     for k in range(nsf):
