@@ -1,0 +1,218 @@
+#!/usr/bin/env python3
+"""Benchmark: MELPe-1200 channel-seconds encoded per second on MI355X.
+
+Workload (BASELINE.json config 4 at N=1): 262,144 independent 8 kHz channels
+per GPU, each step = one melpe_a superframe (540 samples -> 81 bits) of every
+channel, i.e. 262,144 x 67.5 ms = 17,694 channel-seconds of audio per GPU per
+step.  Channels are sharded statically across ranks (rank r owns channels
+[r*C, (r+1)*C)) with no collective on the data path: weak scaling.
+
+Inputs: the integer speech-like generator (pairphone_amd/csrc/synth.h) run on
+the device before the timed region, so every step's PCM is resident in HBM;
+bitstreams stay on the device.  The decode leg (melpe_s of the bits just
+produced) is timed the same way and reported beside the headline.
+
+Roofline: the codec is bit-exact saturating int16/int32 arithmetic with
+serial recursions per channel, so it is bounded by INT VALU issue, not HBM
+and not MFMA.  achieved = W (basic ops per channel-superframe,
+profiles/opcount.json, counted by tools/opcount.py on this same input) x
+channels / average kernel duration (HIP events on the launch stream);
+peak = 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s.
+
+cpu_baseline: the reference codec itself (oracle/_ref/ref_tool, compiled
+from /root/reference by oracle/Makefile), one process per core on a bounded
+sample of the same channels; its bitstreams double as a parity spot check of
+the timed GPU output.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+RUN_SEED = 2026
+SF_SAMPLES = 540
+SF_BYTES = 11
+SF_SECONDS = SF_SAMPLES / 8000.0
+PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12     # INT32 lane-ops/s, T
+REF_TOOL = os.path.join(ROOT, "oracle", "_ref", "ref_tool")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--channels", type=int, default=262144, help="channels per GPU")
+    ap.add_argument("--no-decode", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-channels", type=int, default=32)
+    ap.add_argument("--cpu-jobs", type=int, default=0, help="0 = min(16, usable cores)")
+    return ap.parse_args()
+
+
+def opcount():
+    p = os.path.join(ROOT, "profiles", "opcount.json")
+    if not os.path.exists(p):
+        return None
+    return json.load(open(p))
+
+
+def pmc_traffic():
+    """HBM bytes per encode launch from the committed rocprofv3 --pmc pass
+    (profiles/*_pmc.json, written by tools/pmc_summary.py), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if not os.path.exists(p):
+        return None
+    d = json.load(open(p))
+    return d.get("encode_bytes_per_launch"), d.get("source")
+
+
+def cpu_baseline(args, gpu_bits):
+    """Reference codec, one process per core, on channels 0..S-1 of the same
+    synthetic input.  Returns (baseline dict, parity dict)."""
+    if args.no_cpu_baseline or not os.path.exists(REF_TOOL):
+        return None, None
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    jobs = args.cpu_jobs or min(16, usable)
+    S = args.cpu_sample_channels
+    nsf = max(149, gpu_bits.shape[0])
+    with tempfile.TemporaryDirectory() as tmp:
+        out = os.path.join(tmp, "b.bits")
+        t0 = time.perf_counter()
+        subprocess.run([REF_TOOL, "jobs", str(jobs), "encgen", str(RUN_SEED), "0", str(S),
+                        str(nsf), out], check=True)
+        dt = time.perf_counter() - t0
+        ref = np.fromfile(out, dtype=np.uint8).reshape(S, nsf * SF_BYTES)
+    base = {"value": S * nsf * SF_SECONDS / dt, "unit": "channel-s/s", "cores": jobs,
+            "kind": "reference",
+            "sample": "%d channels x %d superframes (%.1f s of audio each), melpe_a, "
+                      "one forked reference process per channel, %d at a time, %.1f s wall"
+                      % (S, nsf, nsf * SF_SECONDS, jobs, dt)}
+    n = min(S, gpu_bits.shape[1])
+    k = gpu_bits.shape[0]
+    g = np.ascontiguousarray(gpu_bits[:, :n, :].transpose(1, 0, 2)).reshape(n, k * SF_BYTES)
+    same = bool(np.array_equal(g, ref[:n, :k * SF_BYTES]))
+    parity = {"channels": n, "superframes": k, "bit_exact_vs_reference": same}
+    return base, parity
+
+
+def log(msg):
+    print("[bench] " + msg, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    if not torch.cuda.is_available():
+        sys.exit("bench.py needs a HIP device (MI355X)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from pairphone_amd import MelpeEngine
+    C, K, W = args.channels, args.steps, args.warmup
+    eng = MelpeEngine(C, device=local)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    # every step's PCM generated on the device before the timed region
+    pcm = torch.empty((W + K, C, SF_SAMPLES), dtype=torch.int16, device=dev)
+    bits = torch.zeros((W + K, C, SF_BYTES), dtype=torch.uint8, device=dev)
+    eng.synth_seed(RUN_SEED, first_channel=rank * C)
+    for s in range(W + K):
+        eng.synth_dev(pcm[s].data_ptr(), SF_SAMPLES, sptr)
+    torch.cuda.synchronize(dev)
+    log("rank %d: %d channels x %d superframes of input resident" % (rank, C, W + K))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def timed(fn):
+        for s in range(W):
+            fn(s)
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(K)]
+        t0 = time.perf_counter()
+        for i in range(K):
+            ev[i][0].record(stream)
+            fn(W + i)
+            ev[i][1].record(stream)
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        kms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt, kms
+
+    enc_s, enc_kms = timed(lambda s: eng.encode_dev(bits[s].data_ptr(), pcm[s].data_ptr(), None, sptr))
+    log("encode: %.1f ms/step (kernel %.1f ms)" % (1e3 * enc_s / K, enc_kms))
+    dec = None
+    if not args.no_decode:
+        out = torch.empty((W + K, C, SF_SAMPLES), dtype=torch.int16, device=dev)
+        dec_s, dec_kms = timed(lambda s: eng.decode_dev(out[s].data_ptr(), bits[s].data_ptr(), None, sptr))
+        dec = {"value": world * C * K * SF_SECONDS / dec_s, "unit": "channel-s/s decoded",
+               "ms_per_step": 1e3 * dec_s / K, "kernel_ms": dec_kms}
+        log("decode: %.1f ms/step (kernel %.1f ms)" % (1e3 * dec_s / K, dec_kms))
+
+    if rank != 0:
+        return
+    value = world * C * K * SF_SECONDS / enc_s
+    oc = opcount()
+    roof = None
+    if oc:
+        ach = oc["W_enc_per_sf"] * C / (enc_kms / 1e3) / 1e12
+        tr = pmc_traffic()
+        roof = {"bound": "valu", "achieved": ach, "peak": PEAK_VALU_TOPS,
+                "unit": "T basic-ops/s (INT32 VALU lane-ops)", "frac": ach / PEAK_VALU_TOPS,
+                "traffic": tr[0] if tr else None,
+                "kernel": "k_encode", "kernel_ms": enc_kms,
+                "W_per_channel_superframe": oc["W_enc_per_sf"],
+                "algorithmic_hbm_bytes_per_launch": C * (2 * SF_SAMPLES * 2 + SF_BYTES)}
+        if dec:
+            dec["roofline_frac"] = oc["W_dec_per_sf"] * C / (dec["kernel_ms"] / 1e3) / 1e12 / PEAK_VALU_TOPS
+    base, parity = (None, None)
+    if world == 1:
+        base, parity = cpu_baseline(args, bits[:W + K, :args.cpu_sample_channels].cpu().numpy())
+    line = {
+        "metric": "MELPe-1200 channel-seconds encoded/sec (node)",
+        "value": value, "unit": "channel-s/s", "n_gpus": world, "steps": K, "warmup": W,
+        "ms_per_step": 1e3 * enc_s / K, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int16/int32 saturating fixed point",
+        "data": "synthetic (integer speech-like generator csrc/synth.h, run seed %d)" % RUN_SEED,
+        "config": {"workload": "config 4: %d channels per GPU, melpe_a per superframe "
+                               "(NPP x3 + MELPe-1200 analysis + 81-bit packing)" % C,
+                   "channels_per_gpu": C, "channels_total": world * C,
+                   "parallelism": "channel shards, %d GPU(s), no collective" % world},
+        "realtime_factor": value / (world * C),
+        "roofline": roof, "cpu_baseline": base, "decode": dec, "parity_spot_check": parity,
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

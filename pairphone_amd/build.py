@@ -77,6 +77,18 @@ def build_hostemu(force=False):
     return EMU
 
 
+def build_opcount(force=False):
+    """host build with the basic-op census compiled in (tools/opcount.py)"""
+    out = os.path.join(ROOT, "build", "libmelpe_opcount.so")
+    if not force and not _newer(out, _sources()):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    _run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-DMELPE_OPCOUNT", "-I" + CSRC,
+          os.path.join(CSRC, "hostemu.cpp"), "-o", out + ".tmp"])
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build_all(force=False):
     build_oracle()
     build_engine(force)

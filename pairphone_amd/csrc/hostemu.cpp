@@ -25,6 +25,13 @@ struct emu_engine {
 
 static NppScratch g_npp_scratch;
 
+#if defined(MELPE_OPCOUNT)
+extern "C" {
+uint64_t melpe_opcount[64];
+int melpe_opdepth;
+}
+#endif
+
 extern "C" {
 
 int emu_load_tables(const char *path)
@@ -140,6 +147,28 @@ int emu_dec_params(emu_engine *e, int c, int16_t *out)
 {
 	memcpy(out, e->dec[c].par, sizeof(e->dec[c].par));
 	return 90;
+}
+
+/* basic-op census (count build only): copies and clears the counters;
+ * returns the number of ops, or -1 in a normal build */
+int emu_opcount(uint64_t *out, int n)
+{
+#if defined(MELPE_OPCOUNT)
+	for (int i = 0; i < n && i < 64; i++) {
+		out[i] = melpe_opcount[i];
+		melpe_opcount[i] = 0;
+	}
+	return 37;
+#else
+	(void) out;
+	(void) n;
+	return -1;
+#endif
+}
+
+const char *emu_op_names(void)
+{
+	return MELPE_OP_NAMES;
 }
 
 }  // extern "C"

@@ -35,6 +35,22 @@
 #define MDEV_CONST
 #endif
 
+/* Basic-op census for the roofline figure (host count build only, see
+ * tools/opcount.py): OPC(k) counts op k when it is entered from codec code,
+ * not from inside another op -- the SURVEY.md 8(d) rule. */
+#if defined(MELPE_OPCOUNT) && !defined(__HIP__)
+extern "C" uint64_t melpe_opcount[64];
+extern "C" int melpe_opdepth;
+struct OpScope {
+	explicit OpScope(int k) { if (!melpe_opdepth++) melpe_opcount[k]++; }
+	~OpScope() { melpe_opdepth--; }
+};
+#define OPC(k) OpScope op_scope_(k)
+#else
+#define OPC(k)
+#endif
+#define MELPE_OP_NAMES "add sub L_add L_sub L_mult extract_h extract_l L_deposit_h L_deposit_l mult L_mac L_msu r_ound msu_r negate L_negate abs_s L_abs shl shr L_shr L_shl shift_r L_shift_r norm_l norm_s divide_s L40_add L40_sub L40_mac L40_msu L40_shl L40_shr L40_negate norm32 L_sat32 L_mpy_ls"
+
 typedef int16_t Word16;
 typedef int32_t Word32;
 typedef int64_t Word40;
@@ -71,12 +87,13 @@ MD Word32 sat_sub32(Word32 a, Word32 b)
 #endif
 }
 
-MD Word16 add(Word16 a, Word16 b) { return sat16((Word32) a + b); }
-MD Word16 sub(Word16 a, Word16 b) { return sat16((Word32) a - b); }
-MD Word32 L_add(Word32 a, Word32 b) { return sat_add32(a, b); }
+MD Word16 add(Word16 a, Word16 b) { OPC(0); return sat16((Word32) a + b); }
+MD Word16 sub(Word16 a, Word16 b) { OPC(1); return sat16((Word32) a - b); }
+MD Word32 L_add(Word32 a, Word32 b) { OPC(2); return sat_add32(a, b); }
 
 MD Word32 L_sub(Word32 a, Word32 b)
 {
+	OPC(3);
 	/* reference quirk: with a == 0 no overflow check is made and
 	 * 0 - MIN32 wraps to MIN32 (mathhalf_i.h:724-729) */
 	if (a == 0 && b == LW_MIN_)
@@ -86,31 +103,33 @@ MD Word32 L_sub(Word32 a, Word32 b)
 
 MD Word32 L_mult(Word16 a, Word16 b)
 {
+	OPC(4);
 	Word32 p = (Word32) a * (Word32) b;
 	return sat_add32(p, p);
 }
 
-MD Word16 extract_h(Word32 x) { return (Word16) (x >> 16); }
-MD Word16 extract_l(Word32 x) { return (Word16) x; }
-MD Word32 L_deposit_h(Word16 a) { return (Word32) ((uint32_t) (int32_t) a << 16); }
-MD Word32 L_deposit_l(Word16 a) { return (Word32) a; }
+MD Word16 extract_h(Word32 x) { OPC(5); return (Word16) (x >> 16); }
+MD Word16 extract_l(Word32 x) { OPC(6); return (Word16) x; }
+MD Word32 L_deposit_h(Word16 a) { OPC(7); return (Word32) ((uint32_t) (int32_t) a << 16); }
+MD Word32 L_deposit_l(Word16 a) { OPC(8); return (Word32) a; }
 
-MD Word16 mult(Word16 a, Word16 b) { return extract_h(L_mult(a, b)); }
-MD Word32 L_mac(Word32 acc, Word16 a, Word16 b) { return sat_add32(acc, L_mult(a, b)); }
+MD Word16 mult(Word16 a, Word16 b) { OPC(9); return extract_h(L_mult(a, b)); }
+MD Word32 L_mac(Word32 acc, Word16 a, Word16 b) { OPC(10); return sat_add32(acc, L_mult(a, b)); }
 /* L_mult never returns MIN32, so L_sub's quirk cannot trigger here */
-MD Word32 L_msu(Word32 acc, Word16 a, Word16 b) { return sat_sub32(acc, L_mult(a, b)); }
-MD Word16 r_ound(Word32 x) { return extract_h(sat_add32(x, 0x8000)); }
-MD Word16 msu_r(Word32 acc, Word16 a, Word16 b) { return r_ound(L_msu(acc, a, b)); }
+MD Word32 L_msu(Word32 acc, Word16 a, Word16 b) { OPC(11); return sat_sub32(acc, L_mult(a, b)); }
+MD Word16 r_ound(Word32 x) { OPC(12); return extract_h(sat_add32(x, 0x8000)); }
+MD Word16 msu_r(Word32 acc, Word16 a, Word16 b) { OPC(13); return r_ound(L_msu(acc, a, b)); }
 
-MD Word16 negate(Word16 a) { return a == SW_MIN_ ? (Word16) SW_MAX_ : (Word16) -a; }
-MD Word32 L_negate(Word32 a) { return a == LW_MIN_ ? LW_MAX_ : -a; }
-MD Word16 abs_s(Word16 a) { return a == SW_MIN_ ? (Word16) SW_MAX_ : (Word16) (a < 0 ? -a : a); }
-MD Word32 L_abs(Word32 a) { return a == LW_MIN_ ? LW_MAX_ : (a < 0 ? -a : a); }
+MD Word16 negate(Word16 a) { OPC(14); return a == SW_MIN_ ? (Word16) SW_MAX_ : (Word16) -a; }
+MD Word32 L_negate(Word32 a) { OPC(15); return a == LW_MIN_ ? LW_MAX_ : -a; }
+MD Word16 abs_s(Word16 a) { OPC(16); return a == SW_MIN_ ? (Word16) SW_MAX_ : (Word16) (a < 0 ? -a : a); }
+MD Word32 L_abs(Word32 a) { OPC(17); return a == LW_MIN_ ? LW_MAX_ : (a < 0 ? -a : a); }
 
 /* shl/shr: mathhalf_i.h:781-935 */
 MD Word16 shr(Word16 a, Word16 n);
 MD Word16 shl(Word16 a, Word16 n)
 {
+	OPC(18);
 	if (n == 0 || a == 0)
 		return a;
 	if (n < 0) {
@@ -130,6 +149,7 @@ MD Word16 shl(Word16 a, Word16 n)
 
 MD Word16 shr(Word16 a, Word16 n)
 {
+	OPC(19);
 	if (n == 0 || a == 0)
 		return a;
 	if (n < 0) {
@@ -146,6 +166,7 @@ MD Word16 shr(Word16 a, Word16 n)
 MD Word32 L_shl(Word32 a, Word16 n);
 MD Word32 L_shr(Word32 a, Word16 n)
 {
+	OPC(20);
 	if (n == 0 || a == 0)
 		return a;
 	if (n < 0) {
@@ -160,6 +181,7 @@ MD Word32 L_shr(Word32 a, Word16 n)
 
 MD Word32 L_shl(Word32 a, Word16 n)
 {
+	OPC(21);
 	if (n == 0 || a == 0)
 		return a;
 	if (n < 0) {
@@ -182,6 +204,7 @@ MD Word32 L_shl(Word32 a, Word16 n)
 /* shift_r / L_shift_r: mathhalf_i.h:1108-1230 */
 MD Word16 shift_r(Word16 a, Word16 n)
 {
+	OPC(22);
 	if (n >= 0)
 		return shl(a, n);
 	if (n < -15)
@@ -191,6 +214,7 @@ MD Word16 shift_r(Word16 a, Word16 n)
 
 MD Word32 L_shift_r(Word32 a, Word16 n)
 {
+	OPC(23);
 	if (n < -31)
 		return 0;
 	if (n < 0)
@@ -200,6 +224,7 @@ MD Word32 L_shift_r(Word32 a, Word16 n)
 
 MD Word16 norm_l(Word32 x)
 {
+	OPC(24);
 	uint32_t u;
 	if (x == 0)
 		return 0;
@@ -213,10 +238,11 @@ MD Word16 norm_l(Word32 x)
 #endif
 }
 
-MD Word16 norm_s(Word16 a) { return norm_l(L_deposit_h(a)); }
+MD Word16 norm_s(Word16 a) { OPC(25); return norm_l(L_deposit_h(a)); }
 
 MD Word16 divide_s(Word16 num, Word16 den)
 {
+	OPC(26);
 	if (num < 0 || den < 0 || num > den)
 		return 0;
 	if (num == den)
@@ -226,13 +252,14 @@ MD Word16 divide_s(Word16 num, Word16 den)
 
 /* ---- 40-bit accumulator (mathhalf_i.h:1763-2168) ---- */
 MD Word40 clamp40(Word40 v) { return v > MAX40_ ? MAX40_ : (v < MIN40_ ? MIN40_ : v); }
-MD Word40 L40_add(Word40 acc, Word32 x) { return clamp40(acc + (Word40) x); }
-MD Word40 L40_sub(Word40 acc, Word32 x) { return clamp40(acc - (Word40) x); }
-MD Word40 L40_mac(Word40 acc, Word16 a, Word16 b) { return clamp40(acc + (Word40) a * (Word40) b * 2); }
-MD Word40 L40_msu(Word40 acc, Word16 a, Word16 b) { return clamp40(acc - (Word40) a * (Word40) b * 2); }
+MD Word40 L40_add(Word40 acc, Word32 x) { OPC(27); return clamp40(acc + (Word40) x); }
+MD Word40 L40_sub(Word40 acc, Word32 x) { OPC(28); return clamp40(acc - (Word40) x); }
+MD Word40 L40_mac(Word40 acc, Word16 a, Word16 b) { OPC(29); return clamp40(acc + (Word40) a * (Word40) b * 2); }
+MD Word40 L40_msu(Word40 acc, Word16 a, Word16 b) { OPC(30); return clamp40(acc - (Word40) a * (Word40) b * 2); }
 MD Word40 L40_shr(Word40 acc, Word16 n);
 MD Word40 L40_shl(Word40 acc, Word16 n)
 {
+	OPC(31);
 	if (n < 0)
 		return L40_shr(acc, (Word16) -n);
 	for (; n > 0; n--) {
@@ -246,17 +273,20 @@ MD Word40 L40_shl(Word40 acc, Word16 n)
 }
 MD Word40 L40_shr(Word40 acc, Word16 n)
 {
+	OPC(32);
 	if (n < 0)
 		return L40_shl(acc, (Word16) -n);
 	return acc >> (n > 62 ? 62 : n);	/* floor(acc/2) repeated */
 }
 MD Word40 L40_negate(Word40 acc)
 {
+	OPC(33);
 	acc = -acc;
 	return acc > MAX40_ ? MAX40_ : acc;
 }
 MD Word16 norm32(Word40 acc)
 {
+	OPC(34);
 	Word16 n = 0;
 	if (acc > 0) {
 		while (acc > (Word40) LW_MAX_) {
@@ -281,12 +311,14 @@ MD Word16 norm32(Word40 acc)
 }
 MD Word32 L_sat32(Word40 acc)
 {
+	OPC(35);
 	return (Word32) (acc > LW_MAX_ ? LW_MAX_ : (acc < LW_MIN_ ? LW_MIN_ : acc));
 }
 
 /* mathdp31.c:71-83 */
 MD Word32 L_mpy_ls(Word32 L_var2, Word16 var1)
 {
+	OPC(36);
 	Word16 lo = (Word16) (shr(extract_l(L_var2), 1) & 0x7fff);
 	Word32 out = L_shr(L_mult(var1, lo), 15);
 	return L_mac(out, var1, extract_h(L_var2));

@@ -1,0 +1,68 @@
+"""Basic-op census W (ops per channel-superframe) for the roofline figure.
+
+Runs the host count build of the device sources (build/libmelpe_opcount.so,
+-DMELPE_OPCOUNT) over the benchmark's own synthetic input (bench.py RUN_SEED,
+channels 0..N-1, 149 superframes each), counting every saturating basic op
+entered from codec code and not from inside another op.
+Encode = melpe_a (NPP x3 + analysis + packing); decode = melpe_s of the
+resulting bitstreams.  Writes profiles/opcount.json, which bench.py reads.
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main(channels=32, nsf=149):
+    from pairphone_amd.build import build_opcount
+    from pairphone_amd import synth_signal
+    import bench
+    lib = ctypes.CDLL(build_opcount())
+    lib.emu_create.restype = ctypes.c_void_p
+    lib.emu_create.argtypes = [ctypes.c_int]
+    for f in ("emu_encode", "emu_decode"):
+        getattr(lib, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.emu_opcount.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.emu_op_names.restype = ctypes.c_char_p
+    assert lib.emu_load_tables(os.path.join(ROOT, "pairphone_amd", "data", "melpe_tables.bin").encode()) == 0
+    names = lib.emu_op_names().decode().split()
+    cnt = np.zeros(64, np.uint64)
+    lib.emu_opcount(cnt.ctypes.data, 64)
+    x = np.stack([synth_signal(bench.RUN_SEED, c, nsf * 540) for c in range(channels)])
+    e = lib.emu_create(channels)
+    enc = np.zeros(64, np.uint64)
+    dec = np.zeros(64, np.uint64)
+    for k in range(nsf):
+        sp = np.ascontiguousarray(x[:, k * 540:(k + 1) * 540])
+        b = np.zeros((channels, 11), np.uint8)
+        lib.emu_encode(e, b.ctypes.data, sp.ctypes.data)
+        lib.emu_opcount(cnt.ctypes.data, 64)
+        enc += cnt
+        out = np.zeros((channels, 540), np.int16)
+        lib.emu_decode(e, out.ctypes.data, b.ctypes.data)
+        lib.emu_opcount(cnt.ctypes.data, 64)
+        dec += cnt
+    n = channels * nsf
+    res = {
+        "rule": "saturating basic ops entered from codec code (nested op calls not counted), "
+                "host count build of the device sources, SURVEY.md 8(d)",
+        "input": "bench.py synthetic signal, run seed %d, channels 0..%d, %d superframes each"
+                 % (bench.RUN_SEED, channels - 1, nsf),
+        "channel_superframes": n,
+        "W_enc_per_sf": float(enc.sum()) / n,
+        "W_dec_per_sf": float(dec.sum()) / n,
+        "enc_by_op": {names[i]: float(enc[i]) / n for i in np.argsort(-enc.astype(np.float64))[:len(names)] if enc[i]},
+        "dec_by_op": {names[i]: float(dec[i]) / n for i in np.argsort(-dec.astype(np.float64))[:len(names)] if dec[i]},
+    }
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    json.dump(res, open(os.path.join(ROOT, "profiles", "opcount.json"), "w"), indent=1)
+    print("W_enc %.0f  W_dec %.0f ops/superframe" % (res["W_enc_per_sf"], res["W_dec_per_sf"]))
+
+
+if __name__ == "__main__":
+    main(*[int(a) for a in sys.argv[1:]])
