@@ -81,6 +81,11 @@ double melpe_last_kernel_ms(const melpe_engine *e);
 
 const char *melpe_last_error(void);
 
+/* Diagnostics: per-stage wave-cycle totals of a profiling build
+ * (libmelpe_amd_prof.so, -DMELPE_PROF; tools/stage_prof.py), read and
+ * cleared.  Returns the number of slots, or an error in a normal build. */
+int melpe_prof_read(uint64_t *out, int n);
+
 /* Extension of the single-stream drop-in (include/melpe.h): return its one
  * instance to the state of a freshly started reference process (melpe_i
  * alone re-initialises only what melp_ana_init / melp_syn_init touch, as in

@@ -52,17 +52,24 @@ def build_oracle():
     _run([sys.executable, os.path.join(ROOT, "oracle", "dump_tables.py")])
 
 
-def build_engine(force=False):
+PROF_LIB = os.path.join(ROOT, "pairphone_amd", "libmelpe_amd_prof.so")
+
+
+def build_engine(force=False, prof=False, defs=(), out=None):
+    """hipcc build of the product library (prof=True: the stage-timer
+    diagnostics variant libmelpe_amd_prof.so, -DMELPE_PROF)"""
+    out = out or (PROF_LIB if prof else LIB)
     deps = _sources()
-    if not force and not _newer(LIB, deps):
-        return LIB
+    if not force and not _newer(out, deps):
+        return out
     blob = os.path.join(ROOT, "pairphone_amd", "data", "melpe_tables.bin")
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     _run([HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17", "-shared", "-fPIC",
-          "-Wno-unused-result", '-DMELPE_TABLES_BIN="%s"' % blob,
-          os.path.join(CSRC, "engine.hip"), "-o", tmp])
-    os.replace(tmp, LIB)
-    return LIB
+          "-Wno-unused-result", "-Wno-unused-value", '-DMELPE_TABLES_BIN="%s"' % blob]
+         + (["-DMELPE_PROF"] if prof else []) + ["-D" + d for d in defs]
+         + [os.path.join(CSRC, "engine.hip"), "-o", tmp])
+    os.replace(tmp, out)
+    return out
 
 
 def build_hostemu(force=False):

@@ -27,7 +27,7 @@ def load_library(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("MELPE_AMD_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise ImportError("libmelpe_amd.so not built (%s): run __graft_entry__.build()" % p)
     lib = ctypes.CDLL(p)
@@ -49,6 +49,7 @@ def load_library(path=None):
         "melpe_last_kernel_ms": (ctypes.c_double, [vp]),
         "melpe_last_error": (ctypes.c_char_p, []),
         "melpe_single_reset": (i32, []),
+        "melpe_prof_read": (i32, [vp, i32]),
         "melpe_i": (None, []),
         "melpe_a": (None, [vp, vp]),
         "melpe_s": (None, [vp, vp]),

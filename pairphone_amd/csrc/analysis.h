@@ -24,6 +24,7 @@ namespace mlp {
 MD void dc_rmv(const int16_t *in, int16_t *out, int16_t *din, int16_t *dhi,
 	       int16_t *dlo, int n)
 {
+	PROF_SCOPE(33);
 	v_copy(out, in, n);
 	for (int s = 0; s < DC_ORD / 2; s++)
 		iir_2nd_d(out, TB(dc_den) + s * 3, TB(dc_num) + s * 3, out, din + s * 2,
@@ -48,6 +49,7 @@ MN void remove_dc(const int16_t *in, int16_t *out, int16_t len)
 /* gain_ana :311 -- pitch-adaptive RMS in dB (Q8) */
 MN Word16 gain_ana(const int16_t *sig, Word16 pitch, Word16 minlen, Word16 maxlen)
 {
+	PROF_SCOPE(23);
 	int16_t tb[PITCHMAX * 2 + 8];
 	Word16 pq6 = shr(pitch, 1);
 	Word16 tmin = shl(minlen, 6);
@@ -171,6 +173,7 @@ MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 /* find_pitch :240 -- normalised autocorrelation lag search, lags upper..lower */
 MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upper, Word16 len)
 {
+	PROF_SCOPE(2);
 	Word16 ip = lower;
 	Word32 max_num = 0, max_den = 1;
 	bool even = true;
@@ -221,6 +224,7 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 range,
 		   Word16 pmin, Word16 pmax, Word16 pmin_q7, Word16 pmax_q7, Word16 lmin)
 {
+	PROF_SCOPE(3);
 	Word16 len, cb, ip, corr;
 	if (range > 0) {
 		ip = shift_r(fpitch, -7);
@@ -380,6 +384,7 @@ MD Word16 p_avg_update(EncState *E, Word16 pitch, Word16 pcorr, Word16 pthresh)
 MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Word16 pest,
 		    Word16 pavg, Word16 *pcorr2)
 {
+	PROF_SCOPE(7);
 	int16_t *sb = E->pa_sigbuf;
 	int16_t tdin[LPF_ORD], tdout[LPF_ORD];
 	Word16 pcorr, pitch, t, t2;
@@ -435,6 +440,7 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
 		 Word16 *pitch)
 {
+	PROF_SCOPE(4);
 	int16_t sb[BPF_ORD + PITCH_FR];
 	Word16 pcorr, t, sc;
 	const int16_t *bden = TB(bpf_den), *bnum = TB(bpf_num);
@@ -622,6 +628,7 @@ MD void norm40(Word40 *acc, Word16 *sh, Word32 *L)
 /* corPeak :216 */
 MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 {
+	PROF_SCOPE(32);
 	int16_t pb[PIT_COR_LEN];
 	int16_t index[MAXPITCH + 1], gp[MAXPITCH + 1], peak[MAXPITCH + 1], corx[NODE];
 	const int PW = PIT_COR_LEN - MAXPITCH;	/* 73 */
@@ -709,6 +716,7 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 /* pitchAuto :63 */
 MN void pitchAuto(EncState *E, const int16_t *in, PitTrack *pt, ClassParam *cs)
 {
+	PROF_SCOPE(5);
 	if (!E->pauto_started) {
 		v_zero(E->lpbuf, PIT_COR_LEN);
 		v_zero(E->ivbuf, PIT_COR_LEN);
@@ -871,6 +879,7 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
  * subframe; cs[-1] is the previous subframe's parameters */
 MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *ac)
 {
+	PROF_SCOPE(6);
 	int16_t sa[BPF_ORD / 3 + PIT_COR_LEN], sbb[BPF_ORD / 3 + PIT_COR_LEN];
 	int16_t insp[PIT_SUBFRAME];
 	int16_t *si, *so;
@@ -1031,6 +1040,7 @@ MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *
 /* ------------------------------------------------------------------ */
 MN void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, int len)
 {
+	PROF_SCOPE(12);
 	int16_t hb[1024];
 	Word32 Lm[NUM_HARM];
 	Word16 mx = 0;

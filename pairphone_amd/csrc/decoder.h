@@ -72,6 +72,7 @@ MN void noise_sup(int16_t *gain, Word16 ng, Word16 max_noise, Word16 max_att, Wo
  * SCALEOVER-sample cross-fade from the previous scale */
 MN void scale_adj(DecState *D, int16_t *sp, Word16 gain, int len, Word16 over, Word16 inv_over)
 {
+	PROF_SCOPE(21);
 	int16_t tb[PITCHMAX + 8];
 	Word16 sh = 4, t;
 	v_equ_shr(tb, sp, sh, len);
@@ -250,6 +251,7 @@ MD void rd_pitch_pattern(QuantParam *q, MelpParam *par, Word16 uuu_prot, Word16 
 
 MN Word16 low_rate_chn_read(DecState *D)
 {
+	PROF_SCOPE(17);
 	QuantParam *q = &D->qpar;
 	MelpParam *par = D->par;
 	const MelpParam *prev = &D->prev_par;
@@ -752,6 +754,7 @@ MD Word16 set_fc(int16_t *bpvc)
 /* harm_syn_pitch :192 */
 MN void harm_syn_pitch(DecState *D, const int16_t *amp, int16_t *sig, Word16 fc, Word16 len)
 {
+	PROF_SCOPE(19);
 	int16_t rnd[129], mag[129], phase[129];
 	Word16 fc1, fc2, factor;
 	v_zero(phase, 129);
@@ -842,6 +845,7 @@ MD Word16 pf_energy(const int16_t *sp, Word16 *sh_out)
 /* postfilt :60 */
 MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_t *cur_lsf)
 {
+	PROF_SCOPE(20);
 	const int16_t syn_inp[4] = {4096, 12288, 20480, 28672};
 	int16_t synLPC[LPC_ORD], inplsf[LPC_ORD], synhp[45], m1o[LPC_ORD], m2o[LPC_ORD];
 	int16_t nokori[20];
@@ -945,6 +949,7 @@ MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_
 /* ------------------------------------------------------------------ */
 MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 {
+	PROF_SCOPE(18);
 	const int BEGIN = DISP_ORD;	/* max(MIX_ORD, DISP_ORD) */
 	int16_t fs_real[PITCHMAX], refc[LPC_ORD], sb[BEGIN + PITCHMAX];
 	int16_t lsf[LPC_ORD], lpc[LPC_ORD + 1], ase_num[LPC_ORD + 1], ase_den[LPC_ORD];
@@ -1093,6 +1098,7 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 /* synthesis :110 -- melpe_s: D->chbuf (11 bytes) -> 540 samples */
 MN void decode_superframe(DecState *D, int16_t *out)
 {
+	PROF_SCOPE(22);
 	/* syn_begin < PITCHMAX <= BLOCK always, so the reference's "impossible"
 	 * syn_begin > frameSize branch (melp_syn.c:120-125) is not restated */
 	if (D->syn_begin > 0)

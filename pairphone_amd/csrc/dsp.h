@@ -74,20 +74,24 @@ MD void v_scale_shl(int16_t *a, int16_t sc, int n, int16_t sh)	/* :462 */
 		a[i] = extract_h(L_shl(L_mult(a[i], sc), sh));
 }
 
-/* L_v_inner :293 -- sum of products, then shift to the output Q */
-MN Word32 L_v_inner(const int16_t *a, const int16_t *b, int n,
+/* L_v_inner :293 -- sum of products, then shift to the output Q.  The
+ * unrolled body issues a batch of loads before the saturating (order
+ * dependent, so strictly sequential) accumulation consumes them. */
+MN Word32 L_v_inner(const int16_t *__restrict__ a, const int16_t *__restrict__ b, int n,
 		    int16_t qa, int16_t qb, int16_t qout)
 {
 	Word32 acc = 0;
+#pragma unroll 8
 	for (int i = 0; i < n; i++)
 		acc = L_mac(acc, a[i], b[i]);
 	return L_shl(acc, sub(qout, add(add(qa, qb), 1)));
 }
 
 /* L_v_magsq :352 */
-MN Word32 L_v_magsq(const int16_t *a, int n, int16_t qa, int16_t qout)
+MN Word32 L_v_magsq(const int16_t *__restrict__ a, int n, int16_t qa, int16_t qout)
 {
 	Word32 acc = 0;
+#pragma unroll 8
 	for (int i = 0; i < n; i++)
 		acc = L_mac(acc, a[i], a[i]);
 	return L_shl(acc, sub(sub(qout, shl(qa, 1)), 1));
@@ -496,11 +500,57 @@ MD void window_Q(const int16_t *in, const int16_t *w, int16_t *out, int n, Word1
 }
 
 /* zerflt :569 / zerflt_Q :591 -- FIR over in[-order..n-1], run backwards so
- * that in == out is allowed */
+ * that in == out is allowed.  Coefficients live in registers and four
+ * outputs share one sliding window of inputs (each output's sum is still
+ * accumulated in the reference's tap order). */
+template <int ORDER>
+MD void zerflt_q_fixed(const int16_t *in, const int16_t *c, int16_t *out, int n, Word16 sc)
+{
+	Word16 cf[ORDER + 1];
+#pragma unroll
+	for (int j = 0; j <= ORDER; j++)
+		cf[j] = c[j];
+	int i = n - 1;
+	for (; i >= 3; i -= 4) {
+		Word16 x[ORDER + 4];	/* x[k] = in[i - k] */
+#pragma unroll
+		for (int k = 0; k < ORDER + 4; k++)
+			x[k] = in[i - k];
+		Word32 a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll
+		for (int j = 0; j <= ORDER; j++) {
+			a0 = L_mac(a0, x[j], cf[j]);
+			a1 = L_mac(a1, x[j + 1], cf[j]);
+			a2 = L_mac(a2, x[j + 2], cf[j]);
+			a3 = L_mac(a3, x[j + 3], cf[j]);
+		}
+		out[i] = r_ound(L_shl(a0, sc));
+		out[i - 1] = r_ound(L_shl(a1, sc));
+		out[i - 2] = r_ound(L_shl(a2, sc));
+		out[i - 3] = r_ound(L_shl(a3, sc));
+	}
+	for (; i >= 0; i--) {
+		Word32 acc = 0;
+#pragma unroll
+		for (int j = 0; j <= ORDER; j++)
+			acc = L_mac(acc, in[i - j], cf[j]);
+		out[i] = r_ound(L_shl(acc, sc));
+	}
+}
+
 MN void zerflt_Q(const int16_t *in, const int16_t *c, int16_t *out, int order,
 		 int n, Word16 qc)
 {
+	PROF_SCOPE(28);
 	Word16 sc = sub(15, qc);
+	if (order == 10) {
+		zerflt_q_fixed<10>(in, c, out, n, sc);
+		return;
+	}
+	if (order == 1) {
+		zerflt_q_fixed<1>(in, c, out, n, sc);
+		return;
+	}
 	for (int i = n - 1; i >= 0; i--) {
 		Word32 acc = 0;
 		for (int j = 0; j <= order; j++)
@@ -514,50 +564,67 @@ MD void zerflt(const int16_t *in, const int16_t *c, int16_t *out, int order, int
 	zerflt_Q(in, c, out, order, n, 12);
 }
 
-/* iir_2nd_d :615 -- biquad with a double-precision (hi/lo) output memory */
+/* iir_2nd_d :615 -- biquad with a double-precision (hi/lo) output memory;
+ * coefficients and memories held in registers across the block */
 MN void iir_2nd_d(const int16_t *in, const int16_t *den, const int16_t *num,
 		  int16_t *out, int16_t *din, int16_t *dhi, int16_t *dlo, int n)
 {
+	PROF_SCOPE(26);
+	const Word16 d1 = den[1], d2 = den[2], n0 = num[0], n1 = num[1], n2 = num[2];
+	Word16 i0 = din[0], i1 = din[1], h0 = dhi[0], h1 = dhi[1], l0 = dlo[0], l1 = dlo[1];
 	for (int i = 0; i < n; i++) {
 		Word16 x = shr(in[i], 1);
-		Word32 acc = L_mult(dlo[0], den[1]);
-		acc = L_mac(acc, dlo[1], den[2]);
+		Word32 acc = L_mult(l0, d1);
+		acc = L_mac(acc, l1, d2);
 		acc = L_shr(acc, 14);
-		acc = L_mac(acc, dhi[0], den[1]);
-		acc = L_mac(acc, dhi[1], den[2]);
-		acc = L_mac(acc, x, num[0]);
-		acc = L_mac(acc, din[0], num[1]);
-		acc = L_mac(acc, din[1], num[2]);
+		acc = L_mac(acc, h0, d1);
+		acc = L_mac(acc, h1, d2);
+		acc = L_mac(acc, x, n0);
+		acc = L_mac(acc, i0, n1);
+		acc = L_mac(acc, i1, n2);
 		acc = L_shl(acc, 2);
-		din[1] = din[0];
-		din[0] = x;
-		dhi[1] = dhi[0];
-		dlo[1] = dlo[0];
-		dhi[0] = extract_h(acc);
-		dlo[0] = (Word16) (shr(extract_l(acc), 2) & 0x3FFF);
+		i1 = i0;
+		i0 = x;
+		h1 = h0;
+		l1 = l0;
+		h0 = extract_h(acc);
+		l0 = (Word16) (shr(extract_l(acc), 2) & 0x3FFF);
 		out[i] = r_ound(L_shl(acc, 1));
 	}
+	din[0] = i0;
+	din[1] = i1;
+	dhi[0] = h0;
+	dhi[1] = h1;
+	dlo[0] = l0;
+	dlo[1] = l1;
 }
 
 /* iir_2nd_s :660 -- biquad, single precision memories */
 MN void iir_2nd_s(const int16_t *in, const int16_t *den, const int16_t *num,
 		  int16_t *out, int16_t *din, int16_t *dout, int n)
 {
+	PROF_SCOPE(27);
+	const Word16 d1 = den[1], d2 = den[2], n0 = num[0], n1 = num[1], n2 = num[2];
+	Word16 i0 = din[0], i1 = din[1], o0 = dout[0], o1 = dout[1];
 	for (int i = 0; i < n; i++) {
 		Word16 x = in[i];
-		Word32 acc = L_mult(x, num[0]);
-		acc = L_mac(acc, din[0], num[1]);
-		acc = L_mac(acc, din[1], num[2]);
-		acc = L_mac(acc, dout[0], den[1]);
-		acc = L_mac(acc, dout[1], den[2]);
+		Word32 acc = L_mult(x, n0);
+		acc = L_mac(acc, i0, n1);
+		acc = L_mac(acc, i1, n2);
+		acc = L_mac(acc, o0, d1);
+		acc = L_mac(acc, o1, d2);
 		acc = L_shl(acc, 2);
-		din[1] = din[0];
-		din[0] = x;
+		i1 = i0;
+		i0 = x;
 		Word16 y = r_ound(acc);
 		out[i] = y;
-		dout[1] = dout[0];
-		dout[0] = y;
+		o1 = o0;
+		o0 = y;
 	}
+	din[0] = i0;
+	din[1] = i1;
+	dout[0] = o0;
+	dout[1] = o1;
 }
 
 /* ------------------------------------------------------------------ */
@@ -568,6 +635,7 @@ MN void iir_2nd_s(const int16_t *in, const int16_t *den, const int16_t *num,
 MN void lpc_acor(const int16_t *in, const int16_t *win, int16_t *r,
 		 Word16 hf_corr, int order, int n)
 {
+	PROF_SCOPE(24);
 	const int16_t *lagw = TB(lagw_cof);
 	int16_t w[200];
 	Word16 nv, sf;
@@ -792,6 +860,7 @@ MN void lsp_to_freq(const int16_t *lsp, int16_t *freq, int order)
 /* lpc_pred2lsp :566 */
 MN void lpc_pred2lsp(const int16_t *lpc, int16_t *lsf, int order)
 {
+	PROF_SCOPE(25);
 	Word32 Lp[6], Lq[6];
 	int16_t pc[6], qc[6], pf[6], qf[6];
 	Word16 p2 = shr((Word16) order, 1);
@@ -882,9 +951,32 @@ MN void lpc_lsp2pred(int16_t *lsf, int16_t *lpc, int order)
 	}
 }
 
-/* lpc_syn :922 -- all-pole synthesis, y[-order..-1] is the memory */
+/* lpc_syn :922 -- all-pole synthesis, y[-order..-1] is the memory; the
+ * order-10 case keeps coefficients and the output history in registers */
 MD void lpc_syn(const int16_t *x, int16_t *y, const int16_t *a, int order, int n)
 {
+	PROF_SCOPE(29);
+	if (order == 10) {
+		Word16 c[10], h[10];	/* h[k] = y[j - 1 - k] */
+#pragma unroll
+		for (int k = 0; k < 10; k++) {
+			c[k] = a[k];
+			h[k] = y[-1 - k];
+		}
+		for (int j = 0; j < n; j++) {
+			Word32 acc = L_shr(L_deposit_h(x[j]), 3);
+#pragma unroll
+			for (int i = 10; i > 0; i--)
+				acc = L_msu(acc, h[i - 1], c[i - 1]);
+			Word16 v = r_ound(L_shl(acc, 3));
+			y[j] = v;
+#pragma unroll
+			for (int k = 9; k > 0; k--)
+				h[k] = h[k - 1];
+			h[0] = v;
+		}
+		return;
+	}
 	for (int j = 0; j < n; j++) {
 		Word32 acc = L_shr(L_deposit_h(x[j]), 3);
 		for (int i = order; i > 0; i--)
@@ -913,6 +1005,7 @@ MD Word16 block_max(const int16_t *d, int n)
  * with per-stage block floating point; returns the number of halvings. */
 MN Word16 cfft(int16_t *d0, Word16 nn)
 {
+	PROF_SCOPE(30);
 	const int16_t *wrt = g_der.wr, *wit = g_der.wi;
 	int16_t *d = d0 - 1;	/* 1-based view, as the reference */
 	Word16 g = 0;
@@ -1029,6 +1122,7 @@ MD Word16 fft_npp(int16_t *d, Word16 dir)
  * d must hold 2n shorts */
 MN void rfft(int16_t *d, Word16 n)
 {
+	PROF_SCOPE(31);
 	const int16_t *wrt = g_der.wr, *wit = g_der.wi;
 	Word16 n2 = shr(n, 1);
 	cfft(d, n2);

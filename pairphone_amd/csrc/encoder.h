@@ -17,6 +17,7 @@ namespace mlp {
  * hpspeech[i*FRAME] (the window spans speech[0 .. FRAME_END+PITCHMAX]) */
 MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 {
+	PROF_SCOPE(1);
 	int16_t *sb = E->sigbuf;
 	int16_t ac[17], lpc[LPC_ORD + 1], tdin[LPF_ORD], tdout[LPF_ORD];
 	Word16 sub_pitch, t, dontcare, pcorr;
@@ -125,6 +126,7 @@ MN void sc_track_fix(PitTrack *pt, int16_t *pitch, Word16 prev_pitch)
 /* sc_ana :522 -- superframe pitch smoothing and bpvc smoothing */
 MN void sc_ana(EncState *E, MelpParam *par)
 {
+	PROF_SCOPE(8);
 	ClassParam *cs = E->classStat;
 	PitTrack *pt = E->pitTrack;
 	int16_t bpc[NUM_BANDS], sbp[NF + 1], uv[NF + 1];
@@ -337,6 +339,7 @@ MN void sc_ana(EncState *E, MelpParam *par)
 /* analysis :119 -- 540 NPP-processed samples -> quantised params + chbuf */
 MN void analysis(EncState *E, const int16_t *sp_in)
 {
+	PROF_SCOPE(15);
 	MelpParam *par = E->par;
 	int16_t lpc[LPC_ORD + 1];
 	for (int i = 0; i < NF; i++) {
@@ -424,6 +427,7 @@ MN void analysis_upto(EncState *E, const int16_t *sp_in, int upto)
  * frame is left in E->chbuf */
 MN void encode_superframe(EncState *E, NppScratch *w, int16_t *sp)
 {
+	PROF_SCOPE(16);
 	npp_frame(&E->npp, w, sp, sp);
 	npp_frame(&E->npp, w, sp + FRAME, sp + FRAME);
 	npp_frame(&E->npp, w, sp + 2 * FRAME, sp + 2 * FRAME);

@@ -42,6 +42,18 @@ extern "C" const unsigned char melpe_tables_blob[];
 extern "C" const unsigned char melpe_tables_blob_end[];
 
 #define WAVE 64
+/* minimum resident waves per SIMD the encoder / decoder kernels are compiled
+ * for (caps VGPRs at 512 / n) */
+#ifndef MELPE_ENC_WAVES
+#define MELPE_ENC_WAVES 2
+#endif
+#ifndef MELPE_DEC_WAVES
+#define MELPE_DEC_WAVES 4
+#endif
+
+#if defined(MELPE_PROF)
+__device__ unsigned long long g_prof[64];
+#endif
 
 /* ------------------------------------------------------------------ */
 /* kernels                                                            */
@@ -93,7 +105,7 @@ struct DecLane {
 #define PIN_FRAME(obj) __asm__ volatile("" : : "v"(&(obj)) : "memory")
 
 /* melpe_n on `frames` frames per channel (melpe/melpe.c:63-67) */
-__global__ __launch_bounds__(WAVE) void k_npp(EncState *enc, int16_t *sp, int frames,
+__global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_npp(EncState *enc, int16_t *sp, int frames,
 					       int stride, const uint8_t *active, int n,
 					       int rate1200)
 {
@@ -109,7 +121,7 @@ __global__ __launch_bounds__(WAVE) void k_npp(EncState *enc, int16_t *sp, int fr
 
 /* melpe_a on every active channel (melpe/melpe.c:91-99): one lane per
  * channel, sp (C x 540) in place, bits (C x 11) out */
-__global__ __launch_bounds__(WAVE) void k_encode(EncState *enc, int16_t *sp, uint8_t *bits,
+__global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_encode(EncState *enc, int16_t *sp, uint8_t *bits,
 						  const uint8_t *active, int n)
 {
 	int c = blockIdx.x * WAVE + threadIdx.x;
@@ -124,7 +136,7 @@ __global__ __launch_bounds__(WAVE) void k_encode(EncState *enc, int16_t *sp, uin
 }
 
 /* debug aid: encode with the pipeline cut after `upto` stages (0 = NPP only) */
-__global__ __launch_bounds__(WAVE) void k_encode_dbg(EncState *enc, int16_t *sp, int n, int upto)
+__global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_encode_dbg(EncState *enc, int16_t *sp, int n, int upto)
 {
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (c >= n)
@@ -142,7 +154,7 @@ __global__ __launch_bounds__(WAVE) void k_encode_dbg(EncState *enc, int16_t *sp,
 
 /* melpe_s on every active channel (melpe/melpe.c:102-107): bits (C x 11) in,
  * sp (C x 540) out */
-__global__ __launch_bounds__(WAVE) void k_decode(DecState *dec, int16_t *sp,
+__global__ __launch_bounds__(WAVE, MELPE_DEC_WAVES) void k_decode(DecState *dec, int16_t *sp,
 						  const uint8_t *bits, const uint8_t *active, int n)
 {
 	int c = blockIdx.x * WAVE + threadIdx.x;
@@ -552,6 +564,24 @@ int melpe_debug_encode_stage(melpe_engine *e, void *d_sp, int upto)
 	HIPCHK(hipGetLastError());
 	HIPCHK(hipStreamSynchronize(e->stream));
 	return 0;
+}
+
+int melpe_prof_read(uint64_t *out, int n)
+{
+#if defined(MELPE_PROF)
+	unsigned long long h[64];
+	HIPCHK(hipDeviceSynchronize());
+	HIPCHK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof(h)));
+	for (int i = 0; i < n && i < 64; i++)
+		out[i] = h[i];
+	memset(h, 0, sizeof(h));
+	HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), h, sizeof(h)));
+	return 64;
+#else
+	(void) out;
+	(void) n;
+	return fail_msg("not a profiling build (-DMELPE_PROF)");
+#endif
 }
 
 double melpe_last_kernel_ms(const melpe_engine *ce)

@@ -989,6 +989,7 @@ MN void npp_process_frame(NppState *s, NppScratch *w, const int16_t *in, int16_t
 MN void npp_frame(NppState *s, NppScratch *w, const int16_t *sp_in, int16_t *sp_out,
 		  bool rate1200 = true)
 {
+	PROF_SCOPE(0);
 	int16_t outbuf[NPP_WIN];
 	if (!s->started) {
 		int16_t noise[NPP_WIN];

@@ -28,11 +28,15 @@
 /* big routines stay out of line: bounded compile time and register use */
 #define MN __device__ __noinline__
 #define MDEV_CONST __device__
+/* read-only after the one-time upload: constant address space, so uniform
+ * reads become scalar loads */
+#define MDEV_TAB __constant__
 #else
 #define MD static inline
 #define MF static
 #define MN static
 #define MDEV_CONST
+#define MDEV_TAB
 #endif
 
 /* Basic-op census for the roofline figure (host count build only, see
@@ -48,6 +52,26 @@ struct OpScope {
 #define OPC(k) OpScope op_scope_(k)
 #else
 #define OPC(k)
+#endif
+/* Stage timer (profiling build only, -DMELPE_PROF): PROF_SCOPE(k) adds the
+ * wave's s_memtime ticks spent in the enclosing function to g_prof[k]
+ * (inclusive of callees; first active lane records).  tools/stage_prof.py. */
+#if defined(MELPE_PROF) && defined(__HIP_DEVICE_COMPILE__)
+extern __device__ unsigned long long g_prof[64];
+struct ProfScope {
+	int k;
+	unsigned long long t0;
+	__device__ explicit ProfScope(int kk) : k(kk), t0(__builtin_amdgcn_s_memtime()) {}
+	__device__ ~ProfScope()
+	{
+		unsigned long long dt = __builtin_amdgcn_s_memtime() - t0;
+		if (__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x)
+			atomicAdd(&g_prof[k], dt);
+	}
+};
+#define PROF_SCOPE(k) ProfScope prof_scope_(k)
+#else
+#define PROF_SCOPE(k)
 #endif
 #define MELPE_OP_NAMES "add sub L_add L_sub L_mult extract_h extract_l L_deposit_h L_deposit_l mult L_mac L_msu r_ound msu_r negate L_negate abs_s L_abs shl shr L_shr L_shl shift_r L_shift_r norm_l norm_s divide_s L40_add L40_sub L40_mac L40_msu L40_shl L40_shr L40_negate norm32 L_sat32 L_mpy_ls"
 

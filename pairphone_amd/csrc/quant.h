@@ -129,6 +129,7 @@ MN int16_t wvq2(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int di
 /* pitch_vq :75 */
 MN void pitch_vq(EncState *E, MelpParam *par)
 {
+	PROF_SCOPE(10);
 	QuantParam *q = &E->qpar;
 	int16_t tgt[NF], deltp[NF], deltw[NF], wt[NF];
 	int16_t dcb[PITCH_VQ_CAND * NF], il[PITCH_VQ_CAND];
@@ -205,6 +206,7 @@ MN void pitch_vq(EncState *E, MelpParam *par)
 /* gain_vq :368 -- 1024 x 6 full search with the reference's early skip */
 MN void gain_vq(EncState *E, MelpParam *par)
 {
+	PROF_SCOPE(11);
 	const int16_t *cb = TB(gain_vq_cb);
 	int16_t tg[NF * NUM_GAINFR];
 	for (int i = 0; i < NF; i++)
@@ -383,6 +385,7 @@ MD Word32 lsf_werr(Word32 acc, Word16 w)
 /* lsf_vq :895 */
 MN void lsf_vq(EncState *E, MelpParam *par)
 {
+	PROF_SCOPE(9);
 	QuantParam *q = &E->qpar;
 	const int16_t melp_cb_size[4] = {256, 64, 32, 32};
 	const int16_t res_cb_size[4] = {256, 64, 64, 64};
@@ -538,6 +541,7 @@ MN void quant_jitter(EncState *E, MelpParam *par)
 /* quant_fsmag :1277 */
 MN void quant_fsmag(EncState *E, MelpParam *par)
 {
+	PROF_SCOPE(13);
 	int16_t qmag[NUM_HARM];
 	int cnt = 0, last = -1;
 	for (int i = 0; i < NF; i++) {
@@ -673,6 +677,7 @@ MD Word16 parity(Word16 x, int len)	/* melp_chn.c:1367 */
 /* low_rate_chn_write :262 -- 81-bit superframe into chbuf (11 bytes) */
 MN void low_rate_chn_write(EncState *E)
 {
+	PROF_SCOPE(14);
 	QuantParam *q = &E->qpar;
 	unsigned char bb[81];
 	BitCursor bc = {bb, 0};

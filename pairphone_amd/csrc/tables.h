@@ -16,7 +16,7 @@
 #include "ops.h"
 #include "tables_gen.h"
 
-MDEV_CONST int16_t g_tab[MELPE_TABLE_WORDS];
+MDEV_TAB int16_t g_tab[MELPE_TABLE_WORDS];
 #define TB(name) ((const int16_t *) (g_tab + TOFF_##name))
 
 struct DerivedTables {
