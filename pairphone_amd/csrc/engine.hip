@@ -101,6 +101,23 @@ struct DecLane {
 	int16_t out[BLOCK];
 };
 
+struct EncLanePriv {
+	uint8_t guard[FLAT_GUARD_BYTES];
+	NppScratch w;
+	EncState S;
+	int16_t x[BLOCK];
+};
+
+/* per-lane copy between a channel's HBM record and the lane's private
+ * segment, 4 bytes at a time (sizes are multiples of 4) */
+__device__ __forceinline__ void lane_copy(void *dst, const void *src, size_t bytes)
+{
+	uint32_t *d = (uint32_t *) dst;
+	const uint32_t *s = (const uint32_t *) src;
+	for (size_t i = 0; i < bytes / 4; i++)
+		d[i] = s[i];
+}
+
 /* keep the guard alive: the compiler may not drop or shrink the object */
 #define PIN_FRAME(obj) __asm__ volatile("" : : "v"(&(obj)) : "memory")
 
@@ -127,12 +144,25 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_encode(EncState *enc,
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (c >= n || (active && !active[c]))
 		return;
+#if defined(MELPE_PRIVATE_STATE)
+	EncLanePriv L;
+	PIN_FRAME(L);
+	lane_copy(&L.S, &enc[c], sizeof(EncState));
+	int16_t *x = sp + (size_t) c * BLOCK;
+	lane_copy(L.x, x, sizeof(L.x));
+	encode_superframe(&L.S, &L.w, L.x);
+	lane_copy(&enc[c], &L.S, sizeof(EncState));
+	lane_copy(x, L.x, sizeof(L.x));
+	for (int k = 0; k < 11; k++)
+		bits[(size_t) c * 11 + k] = L.S.chbuf[k];
+#else
 	NppLane L;
 	PIN_FRAME(L);
 	EncState *E = &enc[c];
 	encode_superframe(E, &L.w, sp + (size_t) c * BLOCK);
 	for (int k = 0; k < 11; k++)
 		bits[(size_t) c * 11 + k] = E->chbuf[k];
+#endif
 }
 
 /* debug aid: encode with the pipeline cut after `upto` stages (0 = NPP only) */

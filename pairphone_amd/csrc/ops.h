@@ -26,7 +26,11 @@
 #define MD __device__ __attribute__((always_inline)) inline
 #define MF __device__
 /* big routines stay out of line: bounded compile time and register use */
+#if defined(MELPE_INLINE_ALL)
+#define MN __device__ __attribute__((always_inline)) inline
+#else
 #define MN __device__ __noinline__
+#endif
 #define MDEV_CONST __device__
 /* read-only after the one-time upload: constant address space, so uniform
  * reads become scalar loads */

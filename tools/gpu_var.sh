@@ -1,7 +1,9 @@
+# A/B of engine variants (build/var/*.so) against the default build: encode
+# parity tests per variant, then a short bench line each.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out &&
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 &&
-B="bench.py --steps 3 --warmup 1 --no-cpu-baseline" &&
-timeout -k 10 300 python $B > gpurun_out/v1.json 2> gpurun_out/v1.err &&
-MELPE_AMD_LIB=build/var/enc2.so timeout -k 10 300 python $B > gpurun_out/v2.json 2> gpurun_out/v2.err &&
-MELPE_AMD_LIB=build/var/enc4.so timeout -k 10 300 python $B > gpurun_out/v4.json 2> gpurun_out/v4.err &&
-timeout -k 10 300 python tools/stage_prof.py 65536 3 > gpurun_out/stage_prof.txt 2>&1
+B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-decode" &&
+timeout -k 10 300 python $B > gpurun_out/v_base.json 2> gpurun_out/v_base.err &&
+for v in "$@"; do
+  MELPE_AMD_LIB=build/var/$v.so timeout -k 10 300 python -u -m pytest tests/test_encode.py -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/t_$v.log 2>&1 &&
+  MELPE_AMD_LIB=build/var/$v.so timeout -k 10 300 python $B > gpurun_out/v_$v.json 2> gpurun_out/v_$v.err || exit 1
+done

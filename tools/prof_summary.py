@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output databases (rocpd SQLite) into profiles/.
+
+  python tools/prof_summary.py <gpurun_out dir> <tag>
+
+Reads   <dir>/prof_kt/*_results.db        (--kernel-trace --stats pass)
+        <dir>/pmc_*/*_results.db          (one --pmc pass each)
+Writes  profiles/<tag>_kernel_stats.txt   per-kernel calls / total / average
+        profiles/<tag>_pmc.txt            per-kernel counter means per dispatch
+        profiles/pmc_latest.json          HBM bytes per k_encode / k_decode
+                                          launch (read by bench.py)
+
+FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters in KiB per dispatch
+(TCC_EA0_RDREQ / _WRREQ x request size).  MI355X_MICROARCH.md: on gfx950
+FETCH_SIZE under-reports wide (16 B/lane) coalesced streaming reads by 2x;
+the codec's accesses are 2-4 B per lane, an uncalibrated width, so the raw
+value is reported and the correction is noted, not applied.
+"""
+import collections
+import glob
+import json
+import os
+import sqlite3
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")
+
+
+def kernel_stats(db):
+    c = sqlite3.connect(db)
+    rows = list(c.execute("select name,total_calls,total_duration,average,percentage "
+                          "from top_kernels"))
+    return rows
+
+
+def pmc_means(db):
+    c = sqlite3.connect(db)
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    for name, disp, cn, cv in c.execute(
+            "select name,dispatch_id,counter_name,counter_value from pmc_events"):
+        per[(short(name), disp)][cn] += cv
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for (k, _), v in per.items():
+        for cn, cv in v.items():
+            agg[k][cn].append(cv)
+    return {k: {cn: sum(v) / len(v) for cn, v in d.items()} for k, d in agg.items()}
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    prof = os.path.join(ROOT, "profiles")
+    kt = glob.glob(os.path.join(src, "prof_kt", "*_results.db"))
+    if kt:
+        rows = kernel_stats(kt[0])
+        with open(os.path.join(prof, tag + "_kernel_stats.txt"), "w") as f:
+            f.write("# rocprofv3 --kernel-trace --stats (%s); durations in ms (rocpd top_kernels, us / 1e3)\n" % tag)
+            f.write("%-14s %6s %14s %12s %7s\n" % ("kernel", "calls", "total_ms", "avg_ms", "pct"))
+            for n, calls, tot, avg, pct in rows:
+                f.write("%-14s %6d %14.1f %12.1f %7.2f\n" % (short(n)[:14], calls, tot / 1e3,
+                                                           avg / 1e3, pct))
+    pm = {}
+    for db in sorted(glob.glob(os.path.join(src, "pmc_*", "*_results.db"))):
+        for k, d in pmc_means(db).items():
+            pm.setdefault(k, {}).update(d)
+    if pm:
+        with open(os.path.join(prof, tag + "_pmc.txt"), "w") as f:
+            f.write("# rocprofv3 --pmc passes (%s): mean counter value per dispatch\n" % tag)
+            for k in ("k_encode", "k_decode"):
+                if k not in pm:
+                    continue
+                f.write("[%s]\n" % k)
+                for cn in sorted(pm[k]):
+                    f.write("  %-22s %20.1f\n" % (cn, pm[k][cn]))
+                d = pm[k]
+                if "SQ_WAVE_CYCLES" in d and "SQ_WAIT_ANY" in d:
+                    f.write("  wait_any/wave_cycles   %20.3f\n" % (d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]))
+                if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d:
+                    f.write("  valu_insts_per_wave    %20.1f\n" % (d["SQ_INSTS_VALU"] / d["SQ_WAVES"]))
+        out = {"source": "profiles/%s_pmc.txt" % tag}
+        for k, key in (("k_encode", "encode"), ("k_decode", "decode")):
+            d = pm.get(k, {})
+            if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+                out[key + "_bytes_per_launch"] = (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
+                out[key + "_fetch_bytes"] = d["FETCH_SIZE"] * 1024.0
+                out[key + "_write_bytes"] = d["WRITE_SIZE"] * 1024.0
+        json.dump(out, open(os.path.join(prof, "pmc_latest.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
