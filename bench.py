@@ -171,6 +171,16 @@ def main():
 
     enc_s, enc_kms = timed(lambda s: eng.encode_dev(bits[s].data_ptr(), pcm[s].data_ptr(), None, sptr))
     log("encode: %.1f ms/step (kernel %.1f ms)" % (1e3 * enc_s / K, enc_kms))
+    # end-of-run bitstream gather (the only collective, outside the timed
+    # region): every rank's K x C x 11 bytes to every rank, rank 0 keeps them
+    from pairphone_amd.shard import gather_bitstreams
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    allbits = gather_bitstreams(bits[W:], world * C)
+    torch.cuda.synchronize(dev)
+    gather_ms = 1e3 * (time.perf_counter() - t0)
+    gathered = {"bytes": int(allbits.numel()), "ms": gather_ms,
+                "collective": "all_gather" if world > 1 else "none (1 rank)"}
     dec = None
     if not args.no_decode:
         out = torch.empty((W + K, C, SF_SAMPLES), dtype=torch.int16, device=dev)
@@ -210,6 +220,7 @@ def main():
                    "parallelism": "channel shards, %d GPU(s), no collective" % world},
         "realtime_factor": value / (world * C),
         "roofline": roof, "cpu_baseline": base, "decode": dec, "parity_spot_check": parity,
+        "bitstream_gather": gathered,
     }
     print(json.dumps(line), flush=True)
 

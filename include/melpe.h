@@ -11,10 +11,11 @@
  *                                reference (melpe/melpe.c:94-96)
  *   melpe_s   melpe/melpe.c:102  11 bytes -> 540 samples
  *
- * Differences that are deliberate and documented: the encoder and decoder
- * keep separate parameter state (the reference shares melp_par/quant_par
- * between them inside one process, melpe/global.c:28-37; standalone
- * melpe/encoder.c and melpe/decoder.c semantics are reproduced exactly).
+ * As in the reference, the encoder and decoder of the one process-global
+ * instance share melp_par / quant_par / chbuf (melpe/global.c:28-37), so an
+ * interleaved melpe_a / melpe_s sequence (PairPhone's duplex pp) decodes as
+ * the reference does.  The batched ABI (melpe_batch.h) keeps them separate
+ * per channel, i.e. standalone melpe_enc / melpe_dec semantics.
  * The functions compute on the GPU; with no usable GPU they print an error
  * and abort() -- there is no CPU fallback.
  */

@@ -55,7 +55,18 @@ def build_oracle():
 PROF_LIB = os.path.join(ROOT, "pairphone_amd", "libmelpe_amd_prof.so")
 
 
-def build_engine(force=False, prof=False, defs=(), out=None):
+TUS = ("engine", "k_npp", "k_ana", "k_dec")
+# the codec TUs compile their whole call tree inline, so every access to a
+# lane's private state is a scratch_/global_ instruction with counted waits
+# instead of a generic FLAT access; this is what costs compile
+# time, hence one TU per kernel, compiled in parallel
+# (k_npp stays out of line: its fully inlined build computes frame 2 of a
+# superframe wrong -- an unresolved miscompile or latent UB that ASan/UBSan
+# on the host build does not show; tools/gpu_diag_enc.py reproduces it)
+HOT_TUS = ("k_ana", "k_dec")
+
+
+def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=HOT_TUS):
     """hipcc build of the product library (prof=True: the stage-timer
     diagnostics variant libmelpe_amd_prof.so, -DMELPE_PROF)"""
     out = out or (PROF_LIB if prof else LIB)
@@ -63,11 +74,27 @@ def build_engine(force=False, prof=False, defs=(), out=None):
     if not force and not _newer(out, deps):
         return out
     blob = os.path.join(ROOT, "pairphone_amd", "data", "melpe_tables.bin")
+    tag = os.path.splitext(os.path.basename(out))[0]
+    objdir = os.path.join(ROOT, "build", "obj", tag)
+    os.makedirs(objdir, exist_ok=True)
+    common = [HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-c",
+              "-Wno-unused-result", "-Wno-unused-value", '-DMELPE_TABLES_BIN="%s"' % blob] \
+        + (["-DMELPE_PROF"] if prof else []) + ["-D" + d for d in defs]
+    procs, objs = [], []
+    for tu in TUS:
+        o = os.path.join(objdir, tu + ".o")
+        objs.append(o)
+        extra = ["-DMELPE_INLINE_ALL"] if tu in hot else []
+        if tus_defs and tu in tus_defs:
+            extra += ["-D" + d for d in tus_defs[tu]]
+        cmd = common + extra + [os.path.join(CSRC, tu + ".hip"), "-o", o]
+        print("+", " ".join(cmd), flush=True)
+        procs.append((tu, subprocess.Popen(cmd)))
+    bad = [tu for tu, p in procs if p.wait() != 0]
+    if bad:
+        raise RuntimeError("hipcc failed for " + ", ".join(bad))
     tmp = out + ".tmp"
-    _run([HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17", "-shared", "-fPIC",
-          "-Wno-unused-result", "-Wno-unused-value", '-DMELPE_TABLES_BIN="%s"' % blob]
-         + (["-DMELPE_PROF"] if prof else []) + ["-D" + d for d in defs]
-         + [os.path.join(CSRC, "engine.hip"), "-o", tmp])
+    _run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", tmp])
     os.replace(tmp, out)
     return out
 

@@ -1,13 +1,17 @@
 /*
- * engine.hip -- the MI355X MELPe-1200 engine: HIP kernels + the C ABI
- * (include/melpe.h drop-in, include/melpe_batch.h batched).
+ * engine.hip -- host side of the MI355X MELPe-1200 engine: the C ABI
+ * (include/melpe.h drop-in, include/melpe_batch.h batched), device table
+ * upload, and the small kernels (reset, init, parameter sharing, the
+ * synthetic test-signal generator).
  *
- * Execution model: one lane per channel.  A channel-superframe is strictly
- * sequential (every stage carries state into the next and the reference's
- * saturating arithmetic is order dependent), so the parallelism is across
- * channels: a wave processes 64 channels in lock-step, a launch processes
- * every active channel of the engine.  Per-channel state lives in HBM
- * (EncState / DecState), the codebooks in g_tab (uploaded once per device).
+ * The codec kernels live in their own translation units, compiled in
+ * parallel (pairphone_amd/build.py) and linked into libmelpe_amd.so:
+ *   k_npp.hip  melpe_n, and the NPP half of melpe_a (melpe/melpe.c:94-96)
+ *   k_ana.hip  the analysis half of melpe_a (melpe/melpe.c:97-98)
+ *   k_dec.hip  melpe_s (melpe/melpe.c:102-107)
+ * Execution model: one lane per channel (kern.h).  Per-channel
+ * state lives in HBM (EncState / DecState), the codebooks in each TU's
+ * constant tables (uploaded once per device).
  */
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -17,13 +21,11 @@
 #include <string>
 #include <mutex>
 
-#include "codec.h"
+#include "kern.h"
 #define SYN_FN __host__ __device__ static inline
 #include "synth.h"
 #include "../../include/melpe.h"
 #include "../../include/melpe_batch.h"
-
-using namespace mlp;
 
 /* ------------------------------------------------------------------ */
 /* embedded constant tables (oracle/dump_tables.py output)            */
@@ -41,30 +43,29 @@ __asm__(".section .rodata\n"
 extern "C" const unsigned char melpe_tables_blob[];
 extern "C" const unsigned char melpe_tables_blob_end[];
 
-#define WAVE 64
-/* minimum resident waves per SIMD the encoder / decoder kernels are compiled
- * for (caps VGPRs at 512 / n) */
-#ifndef MELPE_ENC_WAVES
-#define MELPE_ENC_WAVES 2
-#endif
-#ifndef MELPE_DEC_WAVES
-#define MELPE_DEC_WAVES 4
-#endif
+MELPE_TU(eng)
 
-#if defined(MELPE_PROF)
-__device__ unsigned long long g_prof[64];
-#endif
-
-/* ------------------------------------------------------------------ */
-/* kernels                                                            */
-/* ------------------------------------------------------------------ */
-
-__global__ void k_init_tables()
-{
-	if (threadIdx.x == 0 && blockIdx.x == 0) {
-		derive_all(&g_der);
-	}
+/* kernels of the other translation units (k_npp.hip, k_ana.hip, k_dec.hip) */
+extern "C" {
+int melpe_tu_npp_upload(const void *blob, size_t bytes);
+int melpe_tu_ana_upload(const void *blob, size_t bytes);
+int melpe_tu_dec_upload(const void *blob, size_t bytes);
+int melpe_tu_npp_prof(uint64_t *acc);
+int melpe_tu_ana_prof(uint64_t *acc);
+int melpe_tu_dec_prof(uint64_t *acc);
+int kl_npp(EncState *enc, int16_t *sp, int frames, int stride, const uint8_t *active, int n,
+	   int rate1200, hipStream_t s);
+int kl_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active, int n, hipStream_t s);
+int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
+	       hipStream_t s);
+int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto, hipStream_t s);
+int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
+	      hipStream_t s);
 }
+
+/* ------------------------------------------------------------------ */
+/* small kernels: reset, init, parameter sharing, test-signal synth   */
+/* ------------------------------------------------------------------ */
 
 __global__ __launch_bounds__(WAVE) void k_reset(EncState *enc, DecState *dec,
 						 const uint8_t *mask, int n, int which)
@@ -76,129 +77,6 @@ __global__ __launch_bounds__(WAVE) void k_reset(EncState *enc, DecState *dec,
 		enc_reset(&enc[c]);
 	if (which & 2)
 		dec_reset(&dec[c]);
-}
-
-/*
- * Private-segment guard.  On gfx950 a FLAT load/store is aperture-checked on
- * its base register BEFORE the unsigned immediate offset is added.  Code that
- * only sees a generic pointer (every __noinline__ callee) may fold p[i - k]
- * into (p - k)[i] + offset:k, so a private object lying within 4 KiB of the
- * bottom of the lane's private segment faults with MEMORY_APERTURE_VIOLATION
- * (tools/exp/flat_private.hip, mode 2, reproduces it).  Every kernel that
- * calls into the codec therefore owns exactly one private object whose first
- * member is this guard; callee frames sit above the kernel frame, so no
- * private object the codec touches starts below FLAT_GUARD_BYTES.
- */
-#define FLAT_GUARD_BYTES 4608
-
-struct NppLane {
-	uint8_t guard[FLAT_GUARD_BYTES];
-	NppScratch w;
-};
-
-struct DecLane {
-	uint8_t guard[FLAT_GUARD_BYTES];
-	int16_t out[BLOCK];
-};
-
-struct EncLanePriv {
-	uint8_t guard[FLAT_GUARD_BYTES];
-	NppScratch w;
-	EncState S;
-	int16_t x[BLOCK];
-};
-
-/* per-lane copy between a channel's HBM record and the lane's private
- * segment, 4 bytes at a time (sizes are multiples of 4) */
-__device__ __forceinline__ void lane_copy(void *dst, const void *src, size_t bytes)
-{
-	uint32_t *d = (uint32_t *) dst;
-	const uint32_t *s = (const uint32_t *) src;
-	for (size_t i = 0; i < bytes / 4; i++)
-		d[i] = s[i];
-}
-
-/* keep the guard alive: the compiler may not drop or shrink the object */
-#define PIN_FRAME(obj) __asm__ volatile("" : : "v"(&(obj)) : "memory")
-
-/* melpe_n on `frames` frames per channel (melpe/melpe.c:63-67) */
-__global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_npp(EncState *enc, int16_t *sp, int frames,
-					       int stride, const uint8_t *active, int n,
-					       int rate1200)
-{
-	int c = blockIdx.x * WAVE + threadIdx.x;
-	if (c >= n || (active && !active[c]))
-		return;
-	NppLane L;
-	PIN_FRAME(L);
-	int16_t *x = sp + (size_t) c * stride;
-	for (int f = 0; f < frames; f++)
-		npp_frame(&enc[c].npp, &L.w, x + f * NPP_HOP, x + f * NPP_HOP, rate1200 != 0);
-}
-
-/* melpe_a on every active channel (melpe/melpe.c:91-99): one lane per
- * channel, sp (C x 540) in place, bits (C x 11) out */
-__global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_encode(EncState *enc, int16_t *sp, uint8_t *bits,
-						  const uint8_t *active, int n)
-{
-	int c = blockIdx.x * WAVE + threadIdx.x;
-	if (c >= n || (active && !active[c]))
-		return;
-#if defined(MELPE_PRIVATE_STATE)
-	EncLanePriv L;
-	PIN_FRAME(L);
-	lane_copy(&L.S, &enc[c], sizeof(EncState));
-	int16_t *x = sp + (size_t) c * BLOCK;
-	lane_copy(L.x, x, sizeof(L.x));
-	encode_superframe(&L.S, &L.w, L.x);
-	lane_copy(&enc[c], &L.S, sizeof(EncState));
-	lane_copy(x, L.x, sizeof(L.x));
-	for (int k = 0; k < 11; k++)
-		bits[(size_t) c * 11 + k] = L.S.chbuf[k];
-#else
-	NppLane L;
-	PIN_FRAME(L);
-	EncState *E = &enc[c];
-	encode_superframe(E, &L.w, sp + (size_t) c * BLOCK);
-	for (int k = 0; k < 11; k++)
-		bits[(size_t) c * 11 + k] = E->chbuf[k];
-#endif
-}
-
-/* debug aid: encode with the pipeline cut after `upto` stages (0 = NPP only) */
-__global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_encode_dbg(EncState *enc, int16_t *sp, int n, int upto)
-{
-	int c = blockIdx.x * WAVE + threadIdx.x;
-	if (c >= n)
-		return;
-	NppLane L;
-	PIN_FRAME(L);
-	EncState *E = &enc[c];
-	int16_t *x = sp + (size_t) c * BLOCK;
-	npp_frame(&E->npp, &L.w, x, x);
-	npp_frame(&E->npp, &L.w, x + FRAME, x + FRAME);
-	npp_frame(&E->npp, &L.w, x + 2 * FRAME, x + 2 * FRAME);
-	if (upto > 0)
-		analysis_upto(E, x, upto);
-}
-
-/* melpe_s on every active channel (melpe/melpe.c:102-107): bits (C x 11) in,
- * sp (C x 540) out */
-__global__ __launch_bounds__(WAVE, MELPE_DEC_WAVES) void k_decode(DecState *dec, int16_t *sp,
-						  const uint8_t *bits, const uint8_t *active, int n)
-{
-	int c = blockIdx.x * WAVE + threadIdx.x;
-	if (c >= n || (active && !active[c]))
-		return;
-	DecLane L;
-	PIN_FRAME(L);
-	DecState *D = &dec[c];
-	for (int k = 0; k < 11; k++)
-		D->chbuf[k] = bits[(size_t) c * 11 + k];
-	decode_superframe(D, L.out);
-	int16_t *o = sp + (size_t) c * BLOCK;
-	for (int i = 0; i < BLOCK; i++)
-		o[i] = L.out[i];
 }
 
 /* melpe_i on channel 0 of the single-stream engine: melp_ana_init +
@@ -299,17 +177,13 @@ static int ensure_device_tables(int dev)
 	if (bytes != sizeof(int16_t) * MELPE_TABLE_WORDS)
 		return fail_msg("embedded table blob has the wrong size");
 	HIPCHK(hipSetDevice(dev));
-	HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_tab), melpe_tables_blob, bytes));
-	k_init_tables<<<1, WAVE>>>();
-	HIPCHK(hipGetLastError());
-	HIPCHK(hipDeviceSynchronize());
+	int (*up[])(const void *, size_t) = {melpe_tu_eng_upload, melpe_tu_npp_upload,
+					     melpe_tu_ana_upload, melpe_tu_dec_upload};
+	for (auto f : up)
+		if (int rc = f(melpe_tables_blob, bytes))
+			return fail("table upload", (hipError_t) rc);
 	g_dev_ready[dev] = true;
 	return 0;
-}
-
-static inline unsigned grid_for(int n)
-{
-	return (unsigned) ((n + WAVE - 1) / WAVE);
 }
 
 static void ev_begin(melpe_engine *e, hipStream_t s)
@@ -426,9 +300,7 @@ static int npp_launch(melpe_engine *e, int16_t *d_sp, int frames, int stride,
 		return fail_msg("melpe_npp: bad frames/stride");
 	HIPCHK(hipSetDevice(e->device));
 	ev_begin(e, s);
-	k_npp<<<grid_for(e->channels), WAVE, 0, s>>>(e->d_enc, d_sp, frames, stride, d_act,
-						       e->channels, rate1200);
-	HIPCHK(hipGetLastError());
+	HIPCHK((hipError_t) kl_npp(e->d_enc, d_sp, frames, stride, d_act, e->channels, rate1200, s));
 	ev_end(e, s, sync);
 	return 0;
 }
@@ -472,9 +344,8 @@ static int encode_launch(melpe_engine *e, unsigned char *d_bits, int16_t *d_sp,
 {
 	HIPCHK(hipSetDevice(e->device));
 	ev_begin(e, s);
-	k_encode<<<grid_for(e->channels), WAVE, 0, s>>>(e->d_enc, d_sp, d_bits, d_act,
-							  e->channels);
-	HIPCHK(hipGetLastError());
+	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, d_sp, d_act, e->channels, s));
+	HIPCHK((hipError_t) kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, s));
 	ev_end(e, s, sync);
 	return 0;
 }
@@ -516,9 +387,7 @@ static int decode_launch(melpe_engine *e, int16_t *d_sp, const unsigned char *d_
 {
 	HIPCHK(hipSetDevice(e->device));
 	ev_begin(e, s);
-	k_decode<<<grid_for(e->channels), WAVE, 0, s>>>(e->d_dec, d_sp, d_bits, d_act,
-							  e->channels);
-	HIPCHK(hipGetLastError());
+	HIPCHK((hipError_t) kl_decode(e->d_dec, d_sp, d_bits, d_act, e->channels, s));
 	ev_end(e, s, sync);
 	return 0;
 }
@@ -589,29 +458,25 @@ int melpe_synth_host(uint32_t run_seed, uint32_t channel, int16_t *out, int samp
 int melpe_debug_encode_stage(melpe_engine *e, void *d_sp, int upto)
 {
 	HIPCHK(hipSetDevice(e->device));
-	k_encode_dbg<<<grid_for(e->channels), WAVE, 0, e->stream>>>(e->d_enc, (int16_t *) d_sp,
-								      e->channels, upto);
-	HIPCHK(hipGetLastError());
+	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, (int16_t *) d_sp, nullptr, e->channels, e->stream));
+	if (upto > 0)
+		HIPCHK((hipError_t) kl_enc_ana_dbg(e->d_enc, (int16_t *) d_sp, e->channels, upto,
+						   e->stream));
 	HIPCHK(hipStreamSynchronize(e->stream));
 	return 0;
 }
 
 int melpe_prof_read(uint64_t *out, int n)
 {
-#if defined(MELPE_PROF)
-	unsigned long long h[64];
-	HIPCHK(hipDeviceSynchronize());
-	HIPCHK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof(h)));
+	uint64_t acc[64] = {0};
+	int (*rd[])(uint64_t *) = {melpe_tu_eng_prof, melpe_tu_npp_prof, melpe_tu_ana_prof,
+				   melpe_tu_dec_prof};
+	for (auto f : rd)
+		if (f(acc))
+			return fail_msg("not a profiling build (-DMELPE_PROF)");
 	for (int i = 0; i < n && i < 64; i++)
-		out[i] = h[i];
-	memset(h, 0, sizeof(h));
-	HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), h, sizeof(h)));
+		out[i] = acc[i];
 	return 64;
-#else
-	(void) out;
-	(void) n;
-	return fail_msg("not a profiling build (-DMELPE_PROF)");
-#endif
 }
 
 double melpe_last_kernel_ms(const melpe_engine *ce)

@@ -28,6 +28,8 @@ static NppScratch g_npp_scratch;
 #if defined(MELPE_OPCOUNT)
 extern "C" {
 uint64_t melpe_opcount[64];
+uint64_t melpe_stagecount[64];
+int melpe_opstage;
 int melpe_opdepth;
 }
 #endif
@@ -159,6 +161,23 @@ int emu_opcount(uint64_t *out, int n)
 		melpe_opcount[i] = 0;
 	}
 	return 37;
+#else
+	(void) out;
+	(void) n;
+	return -1;
+#endif
+}
+
+/* per-stage census (count build only): ops attributed to the innermost
+ * PROF_SCOPE stage (index k+1; 0 = outside any stage); copies and clears */
+int emu_stagecount(uint64_t *out, int n)
+{
+#if defined(MELPE_OPCOUNT)
+	for (int i = 0; i < n && i < 64; i++) {
+		out[i] = melpe_stagecount[i];
+		melpe_stagecount[i] = 0;
+	}
+	return 64;
 #else
 	(void) out;
 	(void) n;

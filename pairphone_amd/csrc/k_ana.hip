@@ -1,0 +1,58 @@
+/*
+ * k_ana.hip -- the analysis half of melpe_a (melpe/melpe.c:97-98:
+ * analysis() + the 11-byte frame): dc removal, melp_ana per frame, sc_ana,
+ * the quantisers and channel packing, one lane per channel, reading the
+ * NPP output k_enc_npp left in the caller's PCM.
+ */
+#include "kern.h"
+
+MELPE_TU(ana)
+
+struct AnaLane {
+	uint8_t guard[FLAT_GUARD_BYTES];
+	EncState S;	/* only the part after the NPP state is live */
+	int16_t x[BLOCK];
+};
+
+__global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits,
+						  const uint8_t *active, int n)
+{
+	int c = blockIdx.x * WAVE + threadIdx.x;
+	if (c >= n || (active && !active[c]))
+		return;
+	AnaLane L;
+	PIN_FRAME(L);
+	lane_copy((char *) &L.S + ENC_ANA_OFF, (const char *) &enc[c] + ENC_ANA_OFF, ENC_ANA_BYTES);
+	lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
+	analysis(&L.S, L.x);
+	lane_copy((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, ENC_ANA_BYTES);
+	for (int k = 0; k < 11; k++)
+		bits[(size_t) c * 11 + k] = L.S.chbuf[k];
+}
+
+/* debug aid: analysis cut after `upto` stages (0 = nothing) */
+__global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto)
+{
+	int c = blockIdx.x * WAVE + threadIdx.x;
+	if (c >= n || upto <= 0)
+		return;
+	AnaLane L;
+	PIN_FRAME(L);
+	lane_copy((char *) &L.S + ENC_ANA_OFF, (const char *) &enc[c] + ENC_ANA_OFF, ENC_ANA_BYTES);
+	lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
+	analysis_upto(&L.S, L.x, upto);
+	lane_copy((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, ENC_ANA_BYTES);
+}
+
+extern "C" int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
+			  int n, hipStream_t s)
+{
+	k_enc_ana<<<grid_for(n), WAVE, 0, s>>>(enc, sp, bits, active, n);
+	return (int) hipGetLastError();
+}
+
+extern "C" int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto, hipStream_t s)
+{
+	k_enc_ana_dbg<<<grid_for(n), WAVE, 0, s>>>(enc, sp, n, upto);
+	return (int) hipGetLastError();
+}

@@ -1,0 +1,119 @@
+/*
+ * kern.h -- shared by the kernel translation units (k_npp.hip, k_ana.hip,
+ * k_dec.hip, engine.hip).
+ *
+ * Each TU is compiled separately (in parallel) into its own code object, so
+ * each has its own copy of the constant tables (g_tab, g_der: tables.h) and
+ * exports an upload function, MELPE_TU(name) -> melpe_tu_<name>_upload(),
+ * that engine.hip calls once per device.  Kernels are launched through
+ * extern "C" wrappers defined next to them (a kernel can only be launched
+ * from its own TU without relocatable device code).
+ *
+ * Execution model: one lane per channel.  A kernel copies the
+ * part of the channel's state it uses from its HBM record into the lane's
+ * private segment, runs, and copies it back.  The private segment is
+ * swizzled per dword across the wave (lane l's dword d at (d*64+l)*4), so
+ * the codec's same-index accesses of the 64 channels of a wave coalesce,
+ * while the HBM record stays a plain per-channel struct.
+ */
+#ifndef MELPE_KERN_H
+#define MELPE_KERN_H
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "codec.h"
+
+using namespace mlp;
+
+#define WAVE 64
+/* minimum resident waves per SIMD the encoder / decoder kernels are compiled
+ * for (caps VGPRs at 512 / n) */
+#ifndef MELPE_ENC_WAVES
+#define MELPE_ENC_WAVES 2
+#endif
+#ifndef MELPE_DEC_WAVES
+#define MELPE_DEC_WAVES 4
+#endif
+
+/*
+ * Private-segment guard.  On gfx950 a FLAT load/store is aperture-checked on
+ * its base register BEFORE the unsigned immediate offset is added.  Code that
+ * only sees a generic pointer (any out-of-line callee) may fold p[i - k]
+ * into (p - k)[i] + offset:k, so a private object lying within 4 KiB of the
+ * bottom of the lane's private segment faults with MEMORY_APERTURE_VIOLATION
+ * (tools/exp/flat_private.hip, mode 2, reproduces it).  Every kernel that
+ * calls into the codec therefore owns exactly one private object whose first
+ * member is this guard; callee frames sit above the kernel frame, so no
+ * private object the codec touches starts below FLAT_GUARD_BYTES.
+ */
+#define FLAT_GUARD_BYTES 4608
+
+/* keep the guard alive: the compiler may not drop or shrink the object */
+#define PIN_FRAME(obj) __asm__ volatile("" : : "v"(&(obj)) : "memory")
+
+/* per-lane copy between a channel's HBM record and the lane's private
+ * segment, 4 bytes at a time (sizes and offsets are multiples of 4) */
+__device__ __forceinline__ void lane_copy(void *dst, const void *src, size_t bytes)
+{
+	uint32_t *d = (uint32_t *) dst;
+	const uint32_t *s = (const uint32_t *) src;
+#pragma unroll 8
+	for (size_t i = 0; i < bytes / 4; i++)
+		d[i] = s[i];
+}
+
+#define MELPE_CHK(expr) do { hipError_t _e = (expr); if (_e != hipSuccess) return (int) _e; } while (0)
+
+/* per-TU table upload (+ derivation of g_der) and stage-timer readout */
+#define MELPE_TU(name)                                                          \
+	__global__ void k_derive_##name()                                       \
+	{                                                                       \
+		if (threadIdx.x == 0 && blockIdx.x == 0)                        \
+			derive_all(&g_der);                                     \
+	}                                                                       \
+	extern "C" int melpe_tu_##name##_upload(const void *blob, size_t bytes) \
+	{                                                                       \
+		if (bytes != sizeof(int16_t) * MELPE_TABLE_WORDS)               \
+			return -1;                                              \
+		MELPE_CHK(hipMemcpyToSymbol(HIP_SYMBOL(g_tab), blob, bytes));   \
+		k_derive_##name<<<1, WAVE>>>();                                 \
+		MELPE_CHK(hipGetLastError());                                   \
+		MELPE_CHK(hipDeviceSynchronize());                              \
+		return 0;                                                       \
+	}                                                                       \
+	MELPE_TU_PROF(name)
+
+#if defined(MELPE_PROF)
+#define MELPE_TU_PROF(name)                                                     \
+	extern "C" int melpe_tu_##name##_prof(uint64_t *acc)                    \
+	{                                                                       \
+		unsigned long long h[64];                                       \
+		MELPE_CHK(hipDeviceSynchronize());                              \
+		MELPE_CHK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof(h))); \
+		for (int i = 0; i < 64; i++)                                    \
+			acc[i] += h[i];                                         \
+		memset(h, 0, sizeof(h));                                        \
+		MELPE_CHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), h, sizeof(h))); \
+		return 0;                                                       \
+	}
+#else
+#define MELPE_TU_PROF(name)                                                     \
+	extern "C" int melpe_tu_##name##_prof(uint64_t *acc)                    \
+	{                                                                       \
+		(void) acc;                                                     \
+		return -1;                                                      \
+	}
+#endif
+
+static inline unsigned grid_for(int n)
+{
+	return (unsigned) ((n + WAVE - 1) / WAVE);
+}
+
+/* the encoder state after the NPP part: what analysis() touches */
+#define ENC_ANA_OFF offsetof(EncState, hpspeech)
+#define ENC_ANA_BYTES (sizeof(EncState) - ENC_ANA_OFF)
+
+#endif

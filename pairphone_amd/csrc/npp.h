@@ -48,6 +48,7 @@ struct NppState {
 	int16_t circb[NPP_NMINWIN][NPP_NB], circb_shift[NPP_NMINWIN][NPP_NB];
 	int16_t speech_in[NPP_WIN];
 	int16_t overlap[NPP_OVL];
+	int16_t pad_;	/* size multiple of 4: kernels copy state by dwords */
 };
 
 /* per-frame scratch that the reference keeps in file statics but rewrites

@@ -31,16 +31,18 @@
 #else
 #define MN __device__ __noinline__
 #endif
-#define MDEV_CONST __device__
+/* per translation unit: every kernel TU is its own code object and uploads
+ * its own copy (kern.h MELPE_TU) */
+#define MDEV_CONST static __device__
 /* read-only after the one-time upload: constant address space, so uniform
  * reads become scalar loads */
-#define MDEV_TAB __constant__
+#define MDEV_TAB static __constant__
 #else
 #define MD static inline
 #define MF static
 #define MN static
-#define MDEV_CONST
-#define MDEV_TAB
+#define MDEV_CONST static
+#define MDEV_TAB static
 #endif
 
 /* Basic-op census for the roofline figure (host count build only, see
@@ -49,9 +51,23 @@
 #if defined(MELPE_OPCOUNT) && !defined(__HIP__)
 extern "C" uint64_t melpe_opcount[64];
 extern "C" int melpe_opdepth;
+extern "C" uint64_t melpe_stagecount[64];
+extern "C" int melpe_opstage;
 struct OpScope {
-	explicit OpScope(int k) { if (!melpe_opdepth++) melpe_opcount[k]++; }
+	explicit OpScope(int k)
+	{
+		if (!melpe_opdepth++) {
+			melpe_opcount[k]++;
+			melpe_stagecount[melpe_opstage]++;
+		}
+	}
 	~OpScope() { melpe_opdepth--; }
+};
+/* exclusive attribution of ops to the innermost PROF_SCOPE stage */
+struct StageScope {
+	int prev;
+	explicit StageScope(int k) : prev(melpe_opstage) { melpe_opstage = k + 1; }
+	~StageScope() { melpe_opstage = prev; }
 };
 #define OPC(k) OpScope op_scope_(k)
 #else
@@ -60,8 +76,12 @@ struct OpScope {
 /* Stage timer (profiling build only, -DMELPE_PROF): PROF_SCOPE(k) adds the
  * wave's s_memtime ticks spent in the enclosing function to g_prof[k]
  * (inclusive of callees; first active lane records).  tools/stage_prof.py. */
+#if defined(MELPE_PROF) && defined(__HIP__)
+/* one counter block per kernel translation unit (each TU is its own code
+ * object; melpe_prof_read sums them) */
+static __device__ unsigned long long g_prof[64];
+#endif
 #if defined(MELPE_PROF) && defined(__HIP_DEVICE_COMPILE__)
-extern __device__ unsigned long long g_prof[64];
 struct ProfScope {
 	int k;
 	unsigned long long t0;
@@ -74,6 +94,8 @@ struct ProfScope {
 	}
 };
 #define PROF_SCOPE(k) ProfScope prof_scope_(k)
+#elif defined(MELPE_OPCOUNT) && !defined(__HIP__)
+#define PROF_SCOPE(k) StageScope stage_scope_(k)
 #else
 #define PROF_SCOPE(k)
 #endif
