@@ -60,10 +60,7 @@ TUS = ("engine", "k_npp", "k_ana", "k_dec")
 # lane's private state is a scratch_/global_ instruction with counted waits
 # instead of a generic FLAT access; this is what costs compile
 # time, hence one TU per kernel, compiled in parallel
-# (k_npp stays out of line: its fully inlined build computes frame 2 of a
-# superframe wrong -- an unresolved miscompile or latent UB that ASan/UBSan
-# on the host build does not show; tools/gpu_diag_enc.py reproduces it)
-HOT_TUS = ("k_ana", "k_dec")
+HOT_TUS = ("k_npp", "k_ana", "k_dec")
 
 
 def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=HOT_TUS):

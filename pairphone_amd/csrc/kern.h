@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "codec.h"
 

@@ -92,21 +92,31 @@ MD Word16 npp_norm_hi(Word32 v, Word16 *sh)
 	return extract_h(L_shl(v, *sh));
 }
 
-/* sum of a block-floating-point spectrum (npp.c:524-535 and 1316-1328) */
+/* term i of the sum of a block-floating-point spectrum (npp.c:524-535 and
+ * 1316-1328); the end bins count half.  Every term is non-negative and at
+ * most 2^23 (mantissa < 2^15, shift <= 8 since maxs >= vs[i]), so the
+ * reference's saturating L_add chain over 129 terms never saturates and any
+ * summation order gives the same value. */
+MD Word32 npp_spec_term(const int16_t *v, const int16_t *vs, Word16 maxs, int i)
+{
+	Word16 half = (i == 0 || i == NPP_NB - 1) ? 7 : 8;
+	return L_shl(L_deposit_l(v[i]), sub(half, sub(maxs, vs[i])));
+}
+
 MD Word32 npp_spec_sum(const int16_t *v, const int16_t *vs, Word16 maxs)
 {
-	Word32 s = L_shl(L_deposit_l(v[0]), sub(7, sub(maxs, vs[0])));
-	s = L_add(s, L_shl(L_deposit_l(v[NPP_NB - 1]), sub(7, sub(maxs, vs[NPP_NB - 1]))));
+	Word32 s = npp_spec_term(v, vs, maxs, 0);
+	s = L_add(s, npp_spec_term(v, vs, maxs, NPP_NB - 1));
 	for (int i = 1; i < NPP_NB - 1; i++)
-		s = L_add(s, L_shl(L_deposit_l(v[i]), sub(8, sub(maxs, vs[i]))));
+		s = L_add(s, npp_spec_term(v, vs, maxs, i));
 	return s;
 }
 
 /* gain_mod :211 -- speech-presence-uncertainty modification of the gain */
-MN void npp_gain_mod(const NppState *s, const NppScratch *w, const int16_t *qk,
-		     int16_t *GainD, int m)
+MD void npp_gain_mod_bin(const NppState *s, const NppScratch *w, const int16_t *qk,
+			 int16_t *GainD, int i)
 {
-	for (int i = 0; i < m; i++) {
+	{
 		Word16 t = sub(SW_MAX_, qk[i]);
 		if (t == 0)
 			t = 1;
@@ -156,26 +166,39 @@ MN void npp_gain_mod(const NppState *s, const NppScratch *w, const int16_t *qk,
 	}
 }
 
+MN void npp_gain_mod(const NppState *s, const NppScratch *w, const int16_t *qk,
+		     int16_t *GainD, int m)
+{
+	for (int i = 0; i < m; i++)
+		npp_gain_mod_bin(s, w, qk, GainD, i);
+}
+
 /* compute_qk :289 -- a-priori speech absence probability */
+MD void npp_compute_qk_bin(NppState *s, int16_t *qk, const int16_t *gk, const int16_t *gks,
+			   Word16 thr, bool first, int i)
+{
+	if (first)
+		s->qla[i] = 16384;
+	s->qla[i] = mult(s->qla[i], 30597);
+	if (cmp_shift(gk[i], gks[i], thr, 0) < 0)
+		s->qla[i] = add(s->qla[i], 2171);
+	qk[i] = s->qla[i];
+}
+
 MN void npp_compute_qk(NppState *s, int16_t *qk, const int16_t *gk, const int16_t *gks,
 		       Word16 thr)
 {
-	if (!s->qk_started) {
-		v_set(s->qla, 16384, NPP_NB);
-		s->qk_started = 1;
-	}
-	v_scale(s->qla, 30597, NPP_NB);
+	bool first = !s->qk_started;
 	for (int i = 0; i < NPP_NB; i++)
-		if (cmp_shift(gk[i], gks[i], thr, 0) < 0)
-			s->qla[i] = add(s->qla[i], 2171);
-	v_copy(qk, s->qla, NPP_NB);
+		npp_compute_qk_bin(s, qk, gk, gks, thr, first, i);
+	s->qk_started = 1;
 }
 
 /* gain_log_mmse :319 */
-MN void npp_gain_log_mmse(NppState *s, NppScratch *w, const int16_t *qk, int16_t *Gain,
-			  const int16_t *gk, const int16_t *gks, int m)
+MD void npp_gain_log_mmse_bin(NppState *s, NppScratch *w, const int16_t *qk, int16_t *Gain,
+			      const int16_t *gk, const int16_t *gks, int i)
 {
-	for (int i = 0; i < m; i++) {
+	{
 		Word16 t1 = sub(SW_MAX_, qk[i]);
 		Word16 sh = norm_s(t1);
 		t1 = shl(t1, sh);
@@ -231,7 +254,7 @@ MN void npp_gain_log_mmse(NppState *s, NppScratch *w, const int16_t *qk, int16_t
 		sh = shr(extract_h(L), 8);
 		if (cmp_shift(kv, sh, 32767, 0) > 0) {
 			Gain[i] = 32767;
-			continue;
+			return;
 		}
 		t1 = extract_l(L_shr(L, 9));
 		t1 = (Word16) (t1 & 0x7fff);
@@ -244,6 +267,13 @@ MN void npp_gain_log_mmse(NppState *s, NppScratch *w, const int16_t *qk, int16_t
 		else
 			Gain[i] = extract_h(L_shl(L, 1));
 	}
+}
+
+MN void npp_gain_log_mmse(NppState *s, NppScratch *w, const int16_t *qk, int16_t *Gain,
+			  const int16_t *gk, const int16_t *gks, int m)
+{
+	for (int i = 0; i < m; i++)
+		npp_gain_log_mmse_bin(s, w, qk, Gain, gk, gks, i);
 }
 
 /* ksi_min_adapt :428 */
@@ -290,14 +320,12 @@ MD void npp_smoothing_win(int16_t *x)
 	v_zero(&x[32], NPP_WIN - 64 + 1);
 }
 
-/* smoothed_periodogram :511 -- optimal recursive smoothing of |Y|^2 */
-MN void npp_smoothed_periodogram(NppState *s, NppScratch *w, Word16 YY_av, Word16 yy_shift)
+/* smoothed_periodogram :511 -- optimal recursive smoothing of |Y|^2.
+ * Scalar part: the smoothing-parameter correction (alphacorr) from the
+ * spectrum sum, and the lower bound amin; returns anum. */
+MD Word16 npp_sm_period_scalars(NppState *s, Word16 maxs, Word32 L, Word16 YY_av, Word16 yy_shift,
+				Word16 *amin_out)
 {
-	Word16 maxs = SW_MIN_;
-	for (int i = 0; i < NPP_NB; i++)
-		if (s->sm_shift[i] > maxs)
-			maxs = s->sm_shift[i];
-	Word32 L = npp_spec_sum(s->smoothedspect, s->sm_shift, maxs);
 	if (L == 0)
 		L = 1;
 	Word16 t = sub(norm_l(L), 1);
@@ -344,128 +372,147 @@ MN void npp_smoothed_periodogram(NppState *s, NppScratch *w, Word16 YY_av, Word1
 		amin = 9830;
 	else if (amin < 1638)
 		amin = 1638;
-	Word16 anum = mult(30802, s->alphacorr);
-
-	for (int i = 0; i < NPP_NB; i++) {
-		Word16 ns = s->noisespect[i];
-		Word32 Lt;
-		sh = sub(s->sm_shift[i], s->noise_shift[i]);
-		if (sh > 0) {
-			Lt = L_sub(L_deposit_h(s->smoothedspect[i]),
-				   L_shr(L_deposit_h(s->noisespect[i]), sh));
-			sh = s->sm_shift[i];
-		} else {
-			Lt = L_sub(L_shr(L_deposit_h(s->smoothedspect[i]), abs_s(sh)),
-				   L_deposit_h(ns));
-			sh = s->noise_shift[i];
-		}
-		Word16 t1 = norm_l(Lt);
-		t = extract_h(L_shl(Lt, t1));
-		sh = sub(sh, t1);
-		L = L_mult(ns, ns);
-		Word16 nsh = norm_l(L);
-		ns = extract_h(L_shl(L, nsh));
-		Word16 nssh = sub(shl(s->noise_shift[i], 1), nsh);
-		w->noisespect2[i] = ns;
-		w->noise2_shift[i] = nssh;
-		if (t == SW_MIN_)
-			L = 0x7fffffff;
-		else
-			L = L_mult(t, t);
-		nsh = norm_l(L);
-		t = extract_h(L_shl(L, nsh));
-		Word16 tsh = (t == 0) ? (Word16) -20 : sub(shl(sh, 1), nsh);
-		t1 = sub(tsh, nssh);
-		if (t1 > 0) {
-			t = shr(t, 1);
-			ns = shr(ns, add(t1, 1));
-		} else {
-			ns = shr(ns, 1);
-			t = shl(t, sub(t1, 1));
-		}
-		Word16 ta = divide_s(ns, add(t, ns));
-		ta = mult(ta, anum);
-		if (ta < amin)
-			ta = amin;
-		t = sub(SW_MAX_, ta);
-		w->alpha_var[i] = ta;
-		Word16 ds = sub(w->YY_shift[i], s->sm_shift[i]);
-		if (ds > 0) {
-			L = L_shr(L_mult(ta, s->smoothedspect[i]), ds);
-			L = L_add(L, L_mult(t, w->YY[i]));
-			s->sm_shift[i] = w->YY_shift[i];
-		} else {
-			L = L_mult(ta, s->smoothedspect[i]);
-			L = L_add(L, L_shl(L_mult(t, w->YY[i]), ds));
-		}
-		if (L < 1)
-			L = 1;
-		sh = norm_l(L);
-		s->smoothedspect[i] = extract_h(L_shl(L, sh));
-		s->sm_shift[i] = sub(s->sm_shift[i], sh);
-	}
+	*amin_out = amin;
+	return mult(30802, s->alphacorr);
 }
 
-/* bias_compensation :695 */
-MN void npp_bias_compensation(NppState *s, NppScratch *w, int16_t *bsp, int16_t *bsh,
-			      int16_t *bsub, int16_t *bsubsh)
+/* per-bin part of smoothed_periodogram */
+MD void npp_sm_period_bin(NppState *s, NppScratch *w, Word16 anum, Word16 amin, int i)
 {
-	Word32 vsum = 0;
-	for (int i = 0; i < NPP_NB; i++) {
-		Word16 beta = mult(w->alpha_var[i], w->alpha_var[i]);
-		if (beta > 26214)
-			beta = 26214;
-		Word32 L = L_mult(sub(SW_MAX_, beta), s->smoothedspect[i]);
-		Word16 ds = sub(s->sm_shift[i], s->av_shift[i]);
-		Word32 m1;
-		if (ds > 0) {
-			m1 = L_add(L_shr(L_mult(beta, s->var_sp_av[i]), ds), L);
-			s->av_shift[i] = s->sm_shift[i];
-		} else {
-			m1 = L_add(L_mult(beta, s->var_sp_av[i]), L_shl(L, ds));
-		}
-		if (m1 < 1)
-			m1 = 1;
-		Word16 s1 = norm_l(m1);
-		s->var_sp_av[i] = extract_h(L_shl(m1, s1));
-		s->av_shift[i] = sub(s->av_shift[i], s1);
-		Word16 ds2 = sub(shl(s->sm_shift[i], 1), s->av2_shift[i]);
-		Word32 m2;
-		if (ds2 > 0) {
-			m2 = L_add(L_shr(L_mult(beta, s->var_sp_2[i]), ds2),
-				   L_mpy_ls(L, s->smoothedspect[i]));
-			s->av2_shift[i] = shl(s->sm_shift[i], 1);
-		} else {
-			m2 = L_add(L_mult(beta, s->var_sp_2[i]),
-				   L_shl(L_mpy_ls(L, s->smoothedspect[i]), ds2));
-		}
-		if (m2 < 1)
-			m2 = 1;
-		s1 = norm_l(m2);
-		s->var_sp_2[i] = extract_h(L_shl(m2, s1));
-		s->av2_shift[i] = sub(s->av2_shift[i], s1);
-		L = L_mult(s->var_sp_av[i], s->var_sp_av[i]);
-		Word16 s3 = sub(s->av2_shift[i], shl(s->av_shift[i], 1));
-		Word16 s4;
-		if (s3 > 0) {
-			L = L_sub(L_deposit_h(s->var_sp_2[i]), L_shr(L, s3));
-			s4 = s->av2_shift[i];
-		} else {
-			L = L_sub(L_shl(L_deposit_h(s->var_sp_2[i]), s3), L);
-			s4 = shl(s->av_shift[i], 1);
-		}
-		s1 = sub(norm_l(L), 1);
-		Word16 t1 = extract_h(L_shl(L, s1));
-		Word16 t = sub(sub(s4, s1), w->noise2_shift[i]);
-		w->var_rel[i] = divide_s(t1, w->noisespect2[i]);
-		if (cmp_shift(w->var_rel[i], t, 16384, 0) > 0)
-			w->var_rel[i] = 16384;
-		else
-			w->var_rel[i] = shl(w->var_rel[i], t);
-		if (w->var_rel[i] < 0)
-			w->var_rel[i] = 0;
-		vsum = L_add(vsum, L_deposit_l(w->var_rel[i]));
+	Word16 ns = s->noisespect[i];
+	Word32 Lt, L;
+	Word16 sh = sub(s->sm_shift[i], s->noise_shift[i]);
+	if (sh > 0) {
+		Lt = L_sub(L_deposit_h(s->smoothedspect[i]),
+			   L_shr(L_deposit_h(s->noisespect[i]), sh));
+		sh = s->sm_shift[i];
+	} else {
+		Lt = L_sub(L_shr(L_deposit_h(s->smoothedspect[i]), abs_s(sh)),
+			   L_deposit_h(ns));
+		sh = s->noise_shift[i];
 	}
+	Word16 t1 = norm_l(Lt);
+	Word16 t = extract_h(L_shl(Lt, t1));
+	sh = sub(sh, t1);
+	L = L_mult(ns, ns);
+	Word16 nsh = norm_l(L);
+	ns = extract_h(L_shl(L, nsh));
+	Word16 nssh = sub(shl(s->noise_shift[i], 1), nsh);
+	w->noisespect2[i] = ns;
+	w->noise2_shift[i] = nssh;
+	if (t == SW_MIN_)
+		L = 0x7fffffff;
+	else
+		L = L_mult(t, t);
+	nsh = norm_l(L);
+	t = extract_h(L_shl(L, nsh));
+	Word16 tsh = (t == 0) ? (Word16) -20 : sub(shl(sh, 1), nsh);
+	t1 = sub(tsh, nssh);
+	if (t1 > 0) {
+		t = shr(t, 1);
+		ns = shr(ns, add(t1, 1));
+	} else {
+		ns = shr(ns, 1);
+		t = shl(t, sub(t1, 1));
+	}
+	Word16 ta = divide_s(ns, add(t, ns));
+	ta = mult(ta, anum);
+	if (ta < amin)
+		ta = amin;
+	t = sub(SW_MAX_, ta);
+	w->alpha_var[i] = ta;
+	Word16 ds = sub(w->YY_shift[i], s->sm_shift[i]);
+	if (ds > 0) {
+		L = L_shr(L_mult(ta, s->smoothedspect[i]), ds);
+		L = L_add(L, L_mult(t, w->YY[i]));
+		s->sm_shift[i] = w->YY_shift[i];
+	} else {
+		L = L_mult(ta, s->smoothedspect[i]);
+		L = L_add(L, L_shl(L_mult(t, w->YY[i]), ds));
+	}
+	if (L < 1)
+		L = 1;
+	sh = norm_l(L);
+	s->smoothedspect[i] = extract_h(L_shl(L, sh));
+	s->sm_shift[i] = sub(s->sm_shift[i], sh);
+}
+
+MN void npp_smoothed_periodogram(NppState *s, NppScratch *w, Word16 YY_av, Word16 yy_shift)
+{
+	Word16 maxs = SW_MIN_;
+	for (int i = 0; i < NPP_NB; i++)
+		if (s->sm_shift[i] > maxs)
+			maxs = s->sm_shift[i];
+	Word32 L = npp_spec_sum(s->smoothedspect, s->sm_shift, maxs);
+	Word16 amin;
+	Word16 anum = npp_sm_period_scalars(s, maxs, L, YY_av, yy_shift, &amin);
+	for (int i = 0; i < NPP_NB; i++)
+		npp_sm_period_bin(s, w, anum, amin, i);
+}
+
+/* bias_compensation :695, first per-bin pass: the variance estimates and
+ * the relative variance var_rel[i] (0..16384) */
+MD void npp_bias1_bin(NppState *s, NppScratch *w, int i)
+{
+	Word16 beta = mult(w->alpha_var[i], w->alpha_var[i]);
+	if (beta > 26214)
+		beta = 26214;
+	Word32 L = L_mult(sub(SW_MAX_, beta), s->smoothedspect[i]);
+	Word16 ds = sub(s->sm_shift[i], s->av_shift[i]);
+	Word32 m1;
+	if (ds > 0) {
+		m1 = L_add(L_shr(L_mult(beta, s->var_sp_av[i]), ds), L);
+		s->av_shift[i] = s->sm_shift[i];
+	} else {
+		m1 = L_add(L_mult(beta, s->var_sp_av[i]), L_shl(L, ds));
+	}
+	if (m1 < 1)
+		m1 = 1;
+	Word16 s1 = norm_l(m1);
+	s->var_sp_av[i] = extract_h(L_shl(m1, s1));
+	s->av_shift[i] = sub(s->av_shift[i], s1);
+	Word16 ds2 = sub(shl(s->sm_shift[i], 1), s->av2_shift[i]);
+	Word32 m2;
+	if (ds2 > 0) {
+		m2 = L_add(L_shr(L_mult(beta, s->var_sp_2[i]), ds2),
+			   L_mpy_ls(L, s->smoothedspect[i]));
+		s->av2_shift[i] = shl(s->sm_shift[i], 1);
+	} else {
+		m2 = L_add(L_mult(beta, s->var_sp_2[i]),
+			   L_shl(L_mpy_ls(L, s->smoothedspect[i]), ds2));
+	}
+	if (m2 < 1)
+		m2 = 1;
+	s1 = norm_l(m2);
+	s->var_sp_2[i] = extract_h(L_shl(m2, s1));
+	s->av2_shift[i] = sub(s->av2_shift[i], s1);
+	L = L_mult(s->var_sp_av[i], s->var_sp_av[i]);
+	Word16 s3 = sub(s->av2_shift[i], shl(s->av_shift[i], 1));
+	Word16 s4;
+	if (s3 > 0) {
+		L = L_sub(L_deposit_h(s->var_sp_2[i]), L_shr(L, s3));
+		s4 = s->av2_shift[i];
+	} else {
+		L = L_sub(L_shl(L_deposit_h(s->var_sp_2[i]), s3), L);
+		s4 = shl(s->av_shift[i], 1);
+	}
+	s1 = sub(norm_l(L), 1);
+	Word16 t1 = extract_h(L_shl(L, s1));
+	Word16 t = sub(sub(s4, s1), w->noise2_shift[i]);
+	w->var_rel[i] = divide_s(t1, w->noisespect2[i]);
+	if (cmp_shift(w->var_rel[i], t, 16384, 0) > 0)
+		w->var_rel[i] = 16384;
+	else
+		w->var_rel[i] = shl(w->var_rel[i], t);
+	if (w->var_rel[i] < 0)
+		w->var_rel[i] = 0;
+}
+
+/* the scalar middle of bias_compensation: vsum = sum of var_rel over the
+ * bins (each 0..16384, so the reference's L_add chain never saturates and
+ * any order gives the same sum); returns vsq, sets f1/f2 */
+MD Word16 npp_bias_scalars(NppState *s, const NppScratch *w, Word32 vsum, Word16 *f1, Word16 *f2)
+{
 	vsum = L_shl(vsum, 1);
 	vsum = L_sub(vsum, L_deposit_l(w->var_rel[0]));
 	vsum = L_sub(vsum, L_deposit_l(w->var_rel[NPP_NB - 1]));
@@ -474,31 +521,50 @@ MN void npp_bias_compensation(NppState *s, NppScratch *w, int16_t *bsp, int16_t 
 		s->var_rel_av = 0;
 	Word16 vsq = mult(12288, sqrt_Q15(s->var_rel_av));
 	vsq = add(8192, vsq);
-	Word16 f1 = extract_h(L_shl(L_mult(vsq, 16521), 1));
-	Word16 f2 = extract_h(L_shl(L_mult(vsq, 18643), 1));
+	*f1 = extract_h(L_shl(L_mult(vsq, 16521), 1));
+	*f2 = extract_h(L_shl(L_mult(vsq, 18643), 1));
+	return vsq;
+}
+
+/* second per-bin pass: the bias-compensated spectra for the minimum search */
+MD void npp_bias2_bin(const NppState *s, const NppScratch *w, int16_t *bsp, int16_t *bsh,
+		      int16_t *bsub, int16_t *bsubsh, Word16 vsq, Word16 f1, Word16 f2, int i)
+{
+	Word32 L3 = L_mult(vsq, s->smoothedspect[i]);
+	Word16 vr = w->var_rel[i];
+	Word32 L4 = L_mult(vr, s->smoothedspect[i]);
+	Word16 t = add(19543, shr(vr, 1));
+	t = add(11656, shr(mult(vr, t), 1));
+	Word32 L = L_mpy_ls(L_mpy_ls(L4, f1), t);
+	L = L_add(L_shr(L3, 6), L_shr(L, 1));
+	if (L < 1)
+		L = 1;
+	Word16 s1 = norm_l(L);
+	bsp[i] = extract_h(L_shl(L, s1));
+	bsh[i] = add(s->sm_shift[i], sub(8, s1));
+	t = add(13968, shr(vr, 2));
+	t = add(11909, shr(mult(vr, t), 1));
+	L = L_mpy_ls(L_mpy_ls(L4, f2), t);
+	L = L_add(L_shr(L3, 4), L_shr(L, 1));
+	if (L < 1)
+		L = 1;
+	s1 = norm_l(L);
+	bsub[i] = extract_h(L_shl(L, s1));
+	bsubsh[i] = add(s->sm_shift[i], sub(6, s1));
+}
+
+MN void npp_bias_compensation(NppState *s, NppScratch *w, int16_t *bsp, int16_t *bsh,
+			      int16_t *bsub, int16_t *bsubsh)
+{
+	Word32 vsum = 0;
 	for (int i = 0; i < NPP_NB; i++) {
-		Word32 L3 = L_mult(vsq, s->smoothedspect[i]);
-		Word16 vr = w->var_rel[i];
-		Word32 L4 = L_mult(vr, s->smoothedspect[i]);
-		Word16 t = add(19543, shr(vr, 1));
-		t = add(11656, shr(mult(vr, t), 1));
-		Word32 L = L_mpy_ls(L_mpy_ls(L4, f1), t);
-		L = L_add(L_shr(L3, 6), L_shr(L, 1));
-		if (L < 1)
-			L = 1;
-		Word16 s1 = norm_l(L);
-		bsp[i] = extract_h(L_shl(L, s1));
-		bsh[i] = add(s->sm_shift[i], sub(8, s1));
-		t = add(13968, shr(vr, 2));
-		t = add(11909, shr(mult(vr, t), 1));
-		L = L_mpy_ls(L_mpy_ls(L4, f2), t);
-		L = L_add(L_shr(L3, 4), L_shr(L, 1));
-		if (L < 1)
-			L = 1;
-		s1 = norm_l(L);
-		bsub[i] = extract_h(L_shl(L, s1));
-		bsubsh[i] = add(s->sm_shift[i], sub(6, s1));
+		npp_bias1_bin(s, w, i);
+		vsum = L_add(vsum, L_deposit_l(w->var_rel[i]));
 	}
+	Word16 f1, f2;
+	Word16 vsq = npp_bias_scalars(s, w, vsum, &f1, &f2);
+	for (int i = 0; i < NPP_NB; i++)
+		npp_bias2_bin(s, w, bsp, bsh, bsub, bsubsh, vsq, f1, f2, i);
 }
 
 /* noise_slope :843 */
@@ -515,87 +581,94 @@ MD Word16 npp_noise_slope(const NppState *s)
 	return 2703;
 }
 
-/* min_search :889 -- minimum tracking over 8 windows of 9 frames */
-MN void npp_min_search(NppState *s, const int16_t *bsp, const int16_t *bsh,
-		       const int16_t *bsub, const int16_t *bsubsh)
+/* min_search :889 -- minimum tracking over 8 windows of 9 frames.  Every
+ * loop of the reference touches bin i only, so the per-bin part runs each
+ * bin through the whole branch; the counters advance afterwards. */
+MD void npp_min_search_bin(NppState *s, const int16_t *bsp, const int16_t *bsh,
+			   const int16_t *bsub, const int16_t *bsubsh, Word16 slope, int i)
 {
 	if (s->minspec_counter == 0) {
-		Word16 slope = npp_noise_slope(s);
-		for (int i = 0; i < NPP_NB; i++)
-			if (cmp_shift(bsp[i], bsh[i], s->act_min[i], s->act_min_shift[i]) < 0) {
-				s->act_min[i] = bsp[i];
-				s->act_min_shift[i] = bsh[i];
-				s->act_min_sub[i] = bsub[i];
-				s->act_min_sub_shift[i] = bsubsh[i];
-				s->localflag[i] = 0;
-			}
-		v_copy(s->circb[s->circb_index], s->act_min, NPP_NB);
-		v_copy(s->circb_shift[s->circb_index], s->act_min_shift, NPP_NB);
-		for (int i = 0; i < NPP_NB; i++) {
-			Word16 t1 = s->circb[0][i], t2 = s->circb_shift[0][i];
-			for (int k = 1; k < NPP_NMINWIN; k++)
-				if (cmp_shift(s->circb[k][i], s->circb_shift[k][i], t1, t2) < 0) {
-					t1 = s->circb[k][i];
-					t2 = s->circb_shift[k][i];
-				}
-			s->circb_min[i] = t1;
-			s->circb_min_shift[i] = t2;
+		if (cmp_shift(bsp[i], bsh[i], s->act_min[i], s->act_min_shift[i]) < 0) {
+			s->act_min[i] = bsp[i];
+			s->act_min_shift[i] = bsh[i];
+			s->act_min_sub[i] = bsub[i];
+			s->act_min_sub_shift[i] = bsubsh[i];
+			s->localflag[i] = 0;
 		}
-		for (int i = 0; i < NPP_NB; i++) {
-			Word16 t = mult(slope, s->circb_min[i]);
-			Word16 ts = add(s->circb_min_shift[i], 4);
-			if (s->localflag[i] &&
-			    cmp_shift(s->act_min_sub[i], s->act_min_sub_shift[i],
-				      s->circb_min[i], s->circb_min_shift[i]) > 0 &&
-			    cmp_shift(s->act_min_sub[i], s->act_min_sub_shift[i], t, ts) < 0) {
-				s->circb_min[i] = s->act_min_sub[i];
-				s->circb_min_shift[i] = s->act_min_sub_shift[i];
-				for (int k = 0; k < NPP_NMINWIN; k++) {
-					s->circb[k][i] = s->circb_min[i];
-					s->circb_shift[k][i] = s->circb_min_shift[i];
-				}
+		s->circb[s->circb_index][i] = s->act_min[i];
+		s->circb_shift[s->circb_index][i] = s->act_min_shift[i];
+		Word16 t1 = s->circb[0][i], t2 = s->circb_shift[0][i];
+		for (int k = 1; k < NPP_NMINWIN; k++)
+			if (cmp_shift(s->circb[k][i], s->circb_shift[k][i], t1, t2) < 0) {
+				t1 = s->circb[k][i];
+				t2 = s->circb_shift[k][i];
+			}
+		s->circb_min[i] = t1;
+		s->circb_min_shift[i] = t2;
+		Word16 t = mult(slope, s->circb_min[i]);
+		Word16 ts = add(s->circb_min_shift[i], 4);
+		if (s->localflag[i] &&
+		    cmp_shift(s->act_min_sub[i], s->act_min_sub_shift[i],
+			      s->circb_min[i], s->circb_min_shift[i]) > 0 &&
+		    cmp_shift(s->act_min_sub[i], s->act_min_sub_shift[i], t, ts) < 0) {
+			s->circb_min[i] = s->act_min_sub[i];
+			s->circb_min_shift[i] = s->act_min_sub_shift[i];
+			for (int k = 0; k < NPP_NMINWIN; k++) {
+				s->circb[k][i] = s->circb_min[i];
+				s->circb_shift[k][i] = s->circb_min_shift[i];
 			}
 		}
-		v_zero(s->localflag, NPP_NB);
+		s->localflag[i] = 0;
+	} else if (s->minspec_counter == 1) {
+		s->act_min[i] = bsp[i];
+		s->act_min_shift[i] = bsh[i];
+		s->act_min_sub[i] = bsub[i];
+		s->act_min_sub_shift[i] = bsubsh[i];
+	} else {
+		if (cmp_shift(bsp[i], bsh[i], s->act_min[i], s->act_min_shift[i]) < 0) {
+			s->act_min[i] = bsp[i];
+			s->act_min_shift[i] = bsh[i];
+			s->act_min_sub[i] = bsub[i];
+			s->act_min_sub_shift[i] = bsubsh[i];
+			s->localflag[i] = 1;
+		}
+		if (cmp_shift(s->act_min_sub[i], s->act_min_sub_shift[i],
+			      s->circb_min[i], s->circb_min_shift[i]) < 0) {
+			s->circb_min[i] = s->act_min_sub[i];
+			s->circb_min_shift[i] = s->act_min_sub_shift[i];
+		}
+		s->noisespect[i] = s->circb_min[i];
+		s->noise_shift[i] = s->circb_min_shift[i];
+		Word32 L = L_mult(NOISE_BIAS, s->noisespect[i]);
+		if (L < 0x40000000L) {
+			L = L_shl(L, 1);
+			s->lambdaD_shift[i] = s->noise_shift[i];
+		} else {
+			s->lambdaD_shift[i] = add(s->noise_shift[i], 1);
+		}
+		s->lambdaD[i] = extract_h(L);
+	}
+}
+
+MD void npp_min_search_post(NppState *s)
+{
+	if (s->minspec_counter == 0) {
 		s->circb_index = add(s->circb_index, 1);
 		if (s->circb_index == NPP_NMINWIN)
 			s->circb_index = 0;
-	} else if (s->minspec_counter == 1) {
-		v_copy(s->act_min, bsp, NPP_NB);
-		v_copy(s->act_min_shift, bsh, NPP_NB);
-		v_copy(s->act_min_sub, bsub, NPP_NB);
-		v_copy(s->act_min_sub_shift, bsubsh, NPP_NB);
-	} else {
-		for (int i = 0; i < NPP_NB; i++)
-			if (cmp_shift(bsp[i], bsh[i], s->act_min[i], s->act_min_shift[i]) < 0) {
-				s->act_min[i] = bsp[i];
-				s->act_min_shift[i] = bsh[i];
-				s->act_min_sub[i] = bsub[i];
-				s->act_min_sub_shift[i] = bsubsh[i];
-				s->localflag[i] = 1;
-			}
-		for (int i = 0; i < NPP_NB; i++)
-			if (cmp_shift(s->act_min_sub[i], s->act_min_sub_shift[i],
-				      s->circb_min[i], s->circb_min_shift[i]) < 0) {
-				s->circb_min[i] = s->act_min_sub[i];
-				s->circb_min_shift[i] = s->act_min_sub_shift[i];
-			}
-		v_copy(s->noisespect, s->circb_min, NPP_NB);
-		v_copy(s->noise_shift, s->circb_min_shift, NPP_NB);
-		for (int i = 0; i < NPP_NB; i++) {
-			Word32 L = L_mult(NOISE_BIAS, s->noisespect[i]);
-			if (L < 0x40000000L) {
-				L = L_shl(L, 1);
-				s->lambdaD_shift[i] = s->noise_shift[i];
-			} else {
-				s->lambdaD_shift[i] = add(s->noise_shift[i], 1);
-			}
-			s->lambdaD[i] = extract_h(L);
-		}
 	}
 	s->minspec_counter = add(s->minspec_counter, 1);
 	if (s->minspec_counter == NPP_LMINWIN)
 		s->minspec_counter = 0;
+}
+
+MN void npp_min_search(NppState *s, const int16_t *bsp, const int16_t *bsh,
+		       const int16_t *bsub, const int16_t *bsubsh)
+{
+	Word16 slope = npp_noise_slope(s);
+	for (int i = 0; i < NPP_NB; i++)
+		npp_min_search_bin(s, bsp, bsh, bsub, bsubsh, slope, i);
+	npp_min_search_post(s);
 }
 
 /* minstat_init :1164 */
@@ -710,6 +783,41 @@ MN void npp_enh_init(NppState *s, NppScratch *w, int16_t *noise)
 	s->SN_LT = divide_s(14648, s->n_pwr);
 	s->SN_LT_shift = sub(22, s->n_pwr_shift);
 	npp_minstat_init(s);
+}
+
+/* a-priori SNR (decision-directed) of bin i, npp.c:1420-1465 */
+MD void npp_ksi_bin(NppState *s, const int16_t *gk, const int16_t *gks, int i)
+{
+	Word32 L = L_mpy_ls(L_mult(s->agal[i], s->agal[i]), 30474);
+	if (L < 1)
+		L = 1;
+	Word16 sh = norm_l(L);
+	Word16 t1 = extract_h(L_shl(L, sh));
+	Word16 t2 = sub(shl(s->agal_shift[i], 1), add(sh, 8));
+	Word16 t3 = s->lambdaD[i];
+	Word16 t4 = s->lambdaD_shift[i];
+	if (sub(t3, t1) < 0) {
+		t1 = shr(t1, 1);
+		t2 = (Word16) (t2 + 1);
+	}
+	s->ksi[i] = divide_s(t1, t3);
+	s->ksi_shift[i] = sub(t2, t4);
+	if (cmp_shift(gk[i], gks[i], NOISE_BIAS, 0) > 0) {
+		L = L_shr(L_deposit_h(NOISE_BIAS), gks[i]);
+		L = L_sub(L_deposit_h(gk[i]), L);
+		sh = norm_l(L);
+		t1 = extract_h(L_shl(L, sh));
+		t1 = mult(t1, 18350);
+		t2 = sub(gks[i], add(sh, 3));
+		sh = sub(s->ksi_shift[i], t2);
+		if (sh > 0) {
+			s->ksi[i] = add(shr(s->ksi[i], 1), shr(t1, (Word16) (sh + 1)));
+			s->ksi_shift[i] = add(s->ksi_shift[i], 1);
+		} else {
+			s->ksi[i] = add(shl(s->ksi[i], (Word16) (sh - 1)), shr(t1, 1));
+			s->ksi_shift[i] = add(t2, 1);
+		}
+	}
 }
 
 /* process_frame :1212 -- one 256-sample analysis/synthesis frame */
@@ -850,38 +958,8 @@ MN void npp_process_frame(NppState *s, NppScratch *w, const int16_t *in, int16_t
 			s->agal_shift[i] = sub(Ymag_shift[i], sh);
 		}
 	} else {
-		for (int i = 0; i < NPP_NB; i++) {
-			L = L_mpy_ls(L_mult(s->agal[i], s->agal[i]), 30474);
-			if (L < 1)
-				L = 1;
-			sh = norm_l(L);
-			t1 = extract_h(L_shl(L, sh));
-			t2 = sub(shl(s->agal_shift[i], 1), add(sh, 8));
-			t3 = s->lambdaD[i];
-			t4 = s->lambdaD_shift[i];
-			if (sub(t3, t1) < 0) {
-				t1 = shr(t1, 1);
-				t2 = (Word16) (t2 + 1);
-			}
-			s->ksi[i] = divide_s(t1, t3);
-			s->ksi_shift[i] = sub(t2, t4);
-			if (cmp_shift(gk[i], gks[i], NOISE_BIAS, 0) > 0) {
-				L = L_shr(L_deposit_h(NOISE_BIAS), gks[i]);
-				L = L_sub(L_deposit_h(gk[i]), L);
-				sh = norm_l(L);
-				t1 = extract_h(L_shl(L, sh));
-				t1 = mult(t1, 18350);
-				t2 = sub(gks[i], add(sh, 3));
-				sh = sub(s->ksi_shift[i], t2);
-				if (sh > 0) {
-					s->ksi[i] = add(shr(s->ksi[i], 1), shr(t1, (Word16) (sh + 1)));
-					s->ksi_shift[i] = add(s->ksi_shift[i], 1);
-				} else {
-					s->ksi[i] = add(shl(s->ksi[i], (Word16) (sh - 1)), shr(t1, 1));
-					s->ksi_shift[i] = add(t2, 1);
-				}
-			}
-		}
+		for (int i = 0; i < NPP_NB; i++)
+			npp_ksi_bin(s, gk, gks, i);
 		t1 = mult(29491, s->Ksi_min_var);
 		t2 = mult(3277, npp_ksi_min_adapt(nflag, GM_MIN, s->SN_LT, s->SN_LT_shift));
 		s->Ksi_min_var = add(t1, t2);

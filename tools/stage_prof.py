@@ -43,8 +43,9 @@ def main(C=65536, nsf=4):
     dec = np.zeros(64, np.uint64)
     lib.melpe_prof_read(dec.ctypes.data, 64)
     waves = C // 64
-    for title, v, tot in (("encode", enc, "encode_superframe"), ("decode", dec, "decode_superframe")):
-        t = float(v[names.index(tot)])
+    for title, v, tot in (("encode", enc, ("npp_frame", "analysis")),
+                          ("decode", dec, ("decode_superframe",))):
+        t = float(sum(v[names.index(n)] for n in tot))
         print("%s: %d channels, %d superframes; wave-cycles per superframe, inclusive" % (title, C, nsf))
         for i in np.argsort(-v.astype(np.float64)):
             if i < len(names) and v[i]:
