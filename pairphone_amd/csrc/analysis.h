@@ -170,6 +170,40 @@ MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 	return sc;
 }
 
+/* the 8 correlations of one lag block of find_pitch: lag n0+k (k = 0..7,
+ * n0 even) reads sig[cb + a_k + j] * sig[cb + upper - n0 - 7 + 3 + b_k + j]
+ * ... i.e. the a-offsets {0,1,1,2,2,3,3,4} and b-offsets {3,3,2,2,1,1,0,0}
+ * relative to the block's two bases (cb_n = cb0 + (n + 1) / 2, lag
+ * i_n = upper - n).  Each lag keeps its own saturating L_mac chain in j
+ * order, so the result is the reference's per-lag L_v_inner; the block only
+ * shares the sample loads (two per j instead of sixteen). */
+MD void fp_corr8(const int16_t *pa, const int16_t *pb, int len, Word32 *out)
+{
+	Word32 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	int16_t A0 = pa[0], A1 = pa[1], A2 = pa[2], A3 = pa[3];
+	int16_t B0 = pb[0], B1 = pb[1], B2 = pb[2];
+	for (int j = 0; j < len; j++) {
+		int16_t A4 = pa[j + 4], B3 = pb[j + 3];
+		acc[0] = L_mac(acc[0], A0, B3);
+		acc[1] = L_mac(acc[1], A1, B3);
+		acc[2] = L_mac(acc[2], A1, B2);
+		acc[3] = L_mac(acc[3], A2, B2);
+		acc[4] = L_mac(acc[4], A2, B1);
+		acc[5] = L_mac(acc[5], A3, B1);
+		acc[6] = L_mac(acc[6], A3, B0);
+		acc[7] = L_mac(acc[7], A4, B0);
+		A0 = A1;
+		A1 = A2;
+		A2 = A3;
+		A3 = A4;
+		B0 = B1;
+		B1 = B2;
+		B2 = B3;
+	}
+	for (int k = 0; k < 8; k++)
+		out[k] = acc[k];
+}
+
 /* find_pitch :240 -- normalised autocorrelation lag search, lags upper..lower */
 MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upper, Word16 len)
 {
@@ -178,10 +212,24 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 	Word32 max_num = 0, max_den = 1;
 	bool even = true;
 	Word16 cb = negate(shr(add(len, upper), 1));
+	const Word16 cb0 = cb;
 	Word32 c00 = L_v_magsq(&sig[cb], len, 0, 1);
 	Word32 cTT = L_v_magsq(&sig[cb + upper], len, 0, 1);
+	Word32 blk[8];
+	int nlags = upper - lower + 1;
 	for (Word16 i = upper; i >= lower; i--) {
-		Word32 corr = L_v_inner(&sig[cb], &sig[cb + i], len, 0, 0, 1);
+		int n = upper - i;
+		Word32 corr;
+		if ((n & 7) == 0 && n + 8 <= nlags) {
+			/* the block's bases: a at cb_n0, b at cb_(n0+7) + i_(n0+7) */
+			int c_n0 = cb0 + (n + 1) / 2;
+			int b0 = cb0 + (n + 8) / 2 + upper - n - 7;
+			fp_corr8(&sig[c_n0], &sig[b0], len, blk);
+		}
+		if (n < (nlags & ~7))
+			corr = blk[n & 7];
+		else
+			corr = L_v_inner(&sig[cb], &sig[cb + i], len, 0, 0, 1);
 		Word16 s1a = norm_s(extract_h(c00));
 		Word16 s1b = norm_s(extract_h(cTT));
 		Word16 s = add(s1a, s1b);
@@ -248,25 +296,56 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 	if (len < lmin)
 		len = lmin;
 	cb = negate(shr(add(len, ip), 1));
-	Word32 msq = L_v_magsq(&sig[cb], len, 0, 1);
+	/* All nine sums of the reference's separate L_v_magsq / L_v_inner calls
+	 * in one pass over the samples: a_j = sig[cb + j], b_j = sig[cb + ip -
+	 * 1 + j].  Each sum keeps its own saturating L_mac chain in j order, so
+	 * each equals the call it replaces; the candidates for both outcomes of
+	 * the ip-1 test are formed (cTT of one outcome is cT1T1 of the other, and
+	 * cTT of the ip-1 outcome is the len-prefix of the (len+2)-term magsq). */
+	Word32 msq = 0, m2 = 0, cm1 = 0, c0 = 0, c1 = 0, tt1 = 0, tt = 0, t1t1 = 0, tt1m = 0;
+	{
+		const int16_t *pa = &sig[cb], *pb = &sig[cb + ip - 1];
+		int16_t b0 = pb[0], b1 = pb[1];
+		for (int j = 0; j < len; j++) {
+			int16_t a = pa[j], b2 = pb[j + 2];
+			msq = L_mac(msq, a, a);
+			m2 = L_mac(m2, b0, b0);
+			cm1 = L_mac(cm1, a, b0);
+			c0 = L_mac(c0, a, b1);
+			c1 = L_mac(c1, a, b2);
+			tt1 = L_mac(tt1, b1, b2);
+			tt = L_mac(tt, b1, b1);
+			t1t1 = L_mac(t1t1, b2, b2);
+			tt1m = L_mac(tt1m, b0, b1);
+			b0 = b1;
+			b1 = b2;
+		}
+	}
+	Word32 ttm = m2;	/* sum of b_j^2, j < len */
+	m2 = L_mac(m2, sig[cb + ip - 1 + len], sig[cb + ip - 1 + len]);
+	m2 = L_mac(m2, sig[cb + ip + len], sig[cb + ip + len]);
 	Word16 s1a = norm_s(extract_h(msq));
-	Word16 s1b = norm_s(extract_h(L_v_magsq(&sig[cb + ip - 1], (Word16) (len + 2), 0, 1)));
+	Word16 s1b = norm_s(extract_h(m2));
 	Word16 s = add(s1a, s1b);
 	Word16 s2 = shr(s, 1);
 	if (shl(s2, 1) != s)
 		s1a = sub(s1a, 1);
 	Word16 c00 = extract_h(L_shl(msq, s1a));
-	Word16 c0T = extract_h(L_shl(L_v_inner(&sig[cb], &sig[cb + ip], len, 0, 0, 1), s2));
-	Word16 c0T1 = extract_h(L_shl(L_v_inner(&sig[cb], &sig[cb + ip + 1], len, 0, 0, 1), s2));
-	Word16 c0Tm1 = extract_h(L_shl(L_v_inner(&sig[cb], &sig[cb + ip - 1], len, 0, 0, 1), s2));
+	Word16 c0T = extract_h(L_shl(c0, s2));
+	Word16 c0T1 = extract_h(L_shl(c1, s2));
+	Word16 c0Tm1 = extract_h(L_shl(cm1, s2));
+	Word32 rTT1 = tt1, rTT = tt, rT1T1 = t1t1;
 	if (c0Tm1 > c0T1) {
 		c0T1 = c0T;
 		c0T = c0Tm1;
 		ip = sub(ip, 1);
+		rTT1 = tt1m;
+		rTT = ttm;
+		rT1T1 = tt;
 	}
-	Word16 cTT1 = extract_h(L_shl(L_v_inner(&sig[cb + ip], &sig[cb + ip + 1], len, 0, 0, 1), s1b));
-	Word16 cTT = extract_h(L_shl(L_v_inner(&sig[cb + ip], &sig[cb + ip], len, 0, 0, 1), s1b));
-	Word16 cT1T1 = extract_h(L_shl(L_v_inner(&sig[cb + ip + 1], &sig[cb + ip + 1], len, 0, 0, 1), s1b));
+	Word16 cTT1 = extract_h(L_shl(rTT1, s1b));
+	Word16 cTT = extract_h(L_shl(rTT, s1b));
+	Word16 cT1T1 = extract_h(L_shl(rT1T1, s1b));
 	Word32 den = L_add(L_mult(c0T1, sub(shr(cTT, 1), shr(cTT1, 1))),
 			   L_mult(c0T, sub(shr(cT1T1, 1), shr(cTT1, 1))));
 	Word32 num = L_sub(L_shr(L_mult(c0T1, cTT), 1), L_shr(L_mult(c0T, cTT1), 1));
@@ -646,7 +725,42 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 		A = L40_mac(A, pb[i], pb[i + MAXPITCH]);
 	gp[MAXPITCH] = cor_gain(&Lr0, &r0s, rks, Lrk, A, true);
 	int lo = 0, hi = MAXPITCH;
+	/* The cross terms A of the lag loop are 73-term sums of 2*x*y with
+	 * |x*y| <= 2^30, so |A| < 2^37 and the 40-bit clamp of L40_mac never
+	 * acts: A is an exact integer sum, order-free.  Lags are taken in
+	 * blocks of 8 (lag 146 - n for n = n0..n0+7, n0 even; window start
+	 * lo = 1 + n/2) sharing the sample loads of one pass. */
+	const int NL = MAXPITCH - MINPITCH;	/* 127 lags 146..20 */
+	int64_t blk[8];
 	for (int i = MAXPITCH - 1; i >= MINPITCH; i--) {
+		int n = MAXPITCH - 1 - i;
+		if ((n & 7) == 0 && n + 8 <= NL) {
+			const int16_t *pa = &pb[1 + n / 2];
+			const int16_t *pq = &pb[143 - n / 2];
+			int64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+			int a0 = pa[0], a1 = pa[1], a2 = pa[2];
+			int q0 = pq[0], q1 = pq[1], q2 = pq[2], q3 = pq[3];
+			for (int t = 0; t < PW; t++) {
+				int a3 = pa[t + 3], q4 = pq[t + 4];
+				acc[0] += (int64_t) (a0 * q4);
+				acc[1] += (int64_t) (a0 * q3);
+				acc[2] += (int64_t) (a1 * q3);
+				acc[3] += (int64_t) (a1 * q2);
+				acc[4] += (int64_t) (a2 * q2);
+				acc[5] += (int64_t) (a2 * q1);
+				acc[6] += (int64_t) (a3 * q1);
+				acc[7] += (int64_t) (a3 * q0);
+				a0 = a1;
+				a1 = a2;
+				a2 = a3;
+				q0 = q1;
+				q1 = q2;
+				q2 = q3;
+				q3 = q4;
+			}
+			for (int k = 0; k < 8; k++)
+				blk[k] = 2 * acc[k];
+		}
 		if (i % 2 == 0) {
 			r0 = L40_shr((Word40) Lr0, r0s);
 			r0 = L40_msu(r0, pb[lo], pb[lo]);
@@ -660,9 +774,13 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 			rk = L40_msu(rk, pb[hi + PW], pb[hi + PW]);
 			norm40(&rk, &rks, &Lrk);
 		}
-		A = 0;
-		for (int j = lo; j < lo + PW; j++)
-			A = L40_mac(A, pb[j], pb[j + i]);
+		if (n < (NL & ~7)) {
+			A = blk[n & 7];
+		} else {
+			A = 0;
+			for (int j = lo; j < lo + PW; j++)
+				A = L40_mac(A, pb[j], pb[j + i]);
+		}
 		gp[i] = cor_gain(&Lr0, &r0s, rks, Lrk, A, true);
 	}
 	peak[MINPITCH] = (gp[MINPITCH + 1] < gp[MINPITCH]) ? gp[MINPITCH] : (int16_t) 0;
