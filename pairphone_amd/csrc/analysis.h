@@ -25,10 +25,7 @@ MD void dc_rmv(const int16_t *in, int16_t *out, int16_t *din, int16_t *dhi,
 	       int16_t *dlo, int n)
 {
 	PROF_SCOPE(33);
-	v_copy(out, in, n);
-	for (int s = 0; s < DC_ORD / 2; s++)
-		iir_2nd_d(out, TB(dc_den) + s * 3, TB(dc_num) + s * 3, out, din + s * 2,
-			  dhi + s * 2, dlo + s * 2, n);
+	iir3_d(in, out, TB(dc_den), TB(dc_num), din, dhi, dlo, n);
 }
 
 /* remove_dc :261 */
@@ -148,16 +145,31 @@ MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 {
 	Word16 sc = 0;
 	Word32 sum = 0, margin = LW_MAX_;
-	for (int i = 0; i < len; i++) {
+	bool ovf = false;
+	int i = 0;
+	for (; i + 4 <= len && !ovf; i += 4) {	/* samples in blocks of 4 */
+		int16_t v[4] = {in[i], in[i + 1], in[i + 2], in[i + 3]};
+		for (int k = 0; k < 4; k++) {
+			Word32 t = L_mult(v[k], v[k]);
+			if (!ovf && t <= margin) {
+				sum = L_add(sum, t);
+				margin = L_sub(margin, t);
+			} else {
+				ovf = true;
+			}
+		}
+	}
+	for (; i < len && !ovf; i++) {
 		Word32 t = L_mult(in[i], in[i]);
 		if (t <= margin) {
 			sum = L_add(sum, t);
 			margin = L_sub(margin, t);
 		} else {
-			margin = LW_MIN_;
-			break;
+			ovf = true;
 		}
 	}
+	if (ovf)
+		margin = LW_MIN_;
 	Word32 corr = sum;
 	if (margin == LW_MIN_) {
 		int16_t tb[PITCH_FR + 8];
@@ -465,7 +477,6 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 {
 	PROF_SCOPE(7);
 	int16_t *sb = E->pa_sigbuf;
-	int16_t tdin[LPF_ORD], tdout[LPF_ORD];
 	Word16 pcorr, pitch, t, t2;
 	if (!E->pana_started) {
 		v_zero(E->lpres_delin, LPF_ORD);
@@ -473,20 +484,8 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 		E->pana_started = 1;
 	}
 	v_copy(&sb[2], &resid[-PITCHMAX], PITCH_FR);
-	for (int s = 0; s < LPF_ORD / 2; s++) {
-		iir_2nd_s(&sb[2], TB(lpf_den) + s * 3, TB(lpf_num) + s * 3, &sb[2],
-			  &E->lpres_delin[s * 2], &E->lpres_delout[s * 2], FRAME);
-		for (int i = s * 2; i < s * 2 + 2; i++) {
-			tdin[i] = E->lpres_delin[i];
-			tdout[i] = E->lpres_delout[i];
-		}
-		iir_2nd_s(&sb[2 + FRAME], TB(lpf_den) + s * 3, TB(lpf_num) + s * 3, &sb[2 + FRAME],
-			  &E->lpres_delin[s * 2], &E->lpres_delout[s * 2], PITCH_FR - FRAME);
-		for (int i = s * 2; i < s * 2 + 2; i++) {
-			E->lpres_delin[i] = tdin[i];
-			E->lpres_delout[i] = tdout[i];
-		}
-	}
+	iir3_s(&sb[2], TB(lpf_den), TB(lpf_num), E->lpres_delin, E->lpres_delout, PITCH_FR,
+	       FRAME);
 	f_pitch_scale(&sb[2], &sb[2], PITCH_FR);
 	t = frac_pch(&sb[2 + PITCH_FR / 2], &pcorr, pest, 5, PITCHMIN, PITCHMAX,
 		     PITCHMIN_Q7, PITCHMAX_Q7, 160);
@@ -536,9 +535,7 @@ MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int1
 	const int NEW = BPF_ORD + PITCH_FR - FRAME;	/* 147 */
 	v_copy(&sb[BPF_ORD], E->bpfsp[0], PITCH_FR - FRAME);
 	v_copy(&sb[NEW], &speech[PITCH_FR - FRAME - PITCHMAX], FRAME);
-	for (int s = 0; s < BPF_ORD / 2; s++)
-		iir_2nd_s(&sb[NEW], bden + s * 3, bnum + s * 3, &sb[NEW], &E->bpfdelin[0][s * 2],
-			  &E->bpfdelout[0][s * 2], FRAME);
+	iir3_s(&sb[NEW], bden, bnum, E->bpfdelin[0], E->bpfdelout[0], FRAME, 0);
 	v_copy(E->bpfsp[0], &sb[BPF_ORD + FRAME], PITCH_FR - FRAME);
 	f_pitch_scale(&sb[BPF_ORD], &sb[BPF_ORD], PITCH_FR);
 	*pitch = frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[0], fpitch[0], 5, PITCHMIN, PITCHMAX,
@@ -554,11 +551,8 @@ MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int1
 	for (int i = 1; i < NUM_BANDS; i++) {
 		v_copy(&sb[BPF_ORD], E->bpfsp[i], PITCH_FR - FRAME);
 		v_copy(&sb[NEW], &speech[PITCH_FR - FRAME - PITCHMAX], FRAME);
-		for (int s = 0; s < BPF_ORD / 2; s++) {
-			int fi = i * (BPF_ORD / 2) * 3 + s * 3;
-			iir_2nd_s(&sb[NEW], bden + fi, bnum + fi, &sb[NEW], &E->bpfdelin[i][s * 2],
-				  &E->bpfdelout[i][s * 2], FRAME);
-		}
+		int fi = i * (BPF_ORD / 2) * 3;
+		iir3_s(&sb[NEW], bden + fi, bnum + fi, E->bpfdelin[i], E->bpfdelout[i], FRAME, 0);
 		v_copy(E->bpfsp[i], &sb[BPF_ORD + FRAME], PITCH_FR - FRAME);
 		sc = f_pitch_scale(&sb[BPF_ORD], &sb[BPF_ORD], PITCH_FR);
 		frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[i], *pitch, 0, PITCHMIN, PITCHMAX,

@@ -627,6 +627,147 @@ MN void iir_2nd_s(const int16_t *in, const int16_t *den, const int16_t *num,
 	dout[1] = o1;
 }
 
+/* One biquad step of iir_2nd_s (single-precision memories), the section
+ * state in registers. */
+struct Biq {
+	Word16 n0, n1, n2, d1, d2, i0, i1, o0, o1;
+};
+
+MD Word16 biq_step(Biq &b, Word16 x)
+{
+	Word32 acc = L_mult(x, b.n0);
+	acc = L_mac(acc, b.i0, b.n1);
+	acc = L_mac(acc, b.i1, b.n2);
+	acc = L_mac(acc, b.o0, b.d1);
+	acc = L_mac(acc, b.o1, b.d2);
+	acc = L_shl(acc, 2);
+	b.i1 = b.i0;
+	b.i0 = x;
+	Word16 y = r_ound(acc);
+	b.o1 = b.o0;
+	b.o0 = y;
+	return y;
+}
+
+/* Three cascaded iir_2nd_s sections (section s: den + 3s, num + 3s, memories
+ * din/dout[2s..2s+1]) run in place on x[0..n), sample by sample.  Section s
+ * at sample i depends only on section s-1 at samples <= i and on its own
+ * past, so this equals the reference's three sequential in-place calls.
+ * Samples move in blocks of 4 (loads issued together, one wait per block).
+ * snap > 0 (a multiple of 4): the memories left behind are those after
+ * sample snap-1 -- the reference's filter-then-save-then-restore around a
+ * two-part call (melp_ana.c:324-346, pit_lib.c:604-622). */
+MD void iir3_s(int16_t *x, const int16_t *den, const int16_t *num, int16_t *din, int16_t *dout,
+	       int n, int snap)
+{
+	Biq b[3];
+	for (int s = 0; s < 3; s++) {
+		b[s].n0 = num[3 * s];
+		b[s].n1 = num[3 * s + 1];
+		b[s].n2 = num[3 * s + 2];
+		b[s].d1 = den[3 * s + 1];
+		b[s].d2 = den[3 * s + 2];
+		b[s].i0 = din[2 * s];
+		b[s].i1 = din[2 * s + 1];
+		b[s].o0 = dout[2 * s];
+		b[s].o1 = dout[2 * s + 1];
+	}
+	Biq keep[3];
+	int i = 0;
+	for (; i + 4 <= n; i += 4) {
+		if (i == snap)
+			for (int s = 0; s < 3; s++)
+				keep[s] = b[s];
+		int16_t v0 = x[i], v1 = x[i + 1], v2 = x[i + 2], v3 = x[i + 3];
+		v0 = biq_step(b[2], biq_step(b[1], biq_step(b[0], v0)));
+		v1 = biq_step(b[2], biq_step(b[1], biq_step(b[0], v1)));
+		v2 = biq_step(b[2], biq_step(b[1], biq_step(b[0], v2)));
+		v3 = biq_step(b[2], biq_step(b[1], biq_step(b[0], v3)));
+		x[i] = v0;
+		x[i + 1] = v1;
+		x[i + 2] = v2;
+		x[i + 3] = v3;
+	}
+	if (i == snap)
+		for (int s = 0; s < 3; s++)
+			keep[s] = b[s];
+	for (; i < n; i++)
+		x[i] = biq_step(b[2], biq_step(b[1], biq_step(b[0], x[i])));
+	for (int s = 0; s < 3; s++) {
+		const Biq &o = snap > 0 ? keep[s] : b[s];
+		din[2 * s] = o.i0;
+		din[2 * s + 1] = o.i1;
+		dout[2 * s] = o.o0;
+		dout[2 * s + 1] = o.o1;
+	}
+}
+
+/* One step of iir_2nd_d (double-precision output memory hi/lo) */
+struct Biqd {
+	Word16 n0, n1, n2, d1, d2, i0, i1, h0, h1, l0, l1;
+};
+
+MD Word16 biqd_step(Biqd &b, Word16 in)
+{
+	Word16 x = shr(in, 1);
+	Word32 acc = L_mult(b.l0, b.d1);
+	acc = L_mac(acc, b.l1, b.d2);
+	acc = L_shr(acc, 14);
+	acc = L_mac(acc, b.h0, b.d1);
+	acc = L_mac(acc, b.h1, b.d2);
+	acc = L_mac(acc, x, b.n0);
+	acc = L_mac(acc, b.i0, b.n1);
+	acc = L_mac(acc, b.i1, b.n2);
+	acc = L_shl(acc, 2);
+	b.i1 = b.i0;
+	b.i0 = x;
+	b.h1 = b.h0;
+	b.l1 = b.l0;
+	b.h0 = extract_h(acc);
+	b.l0 = (Word16) (shr(extract_l(acc), 2) & 0x3FFF);
+	return r_ound(L_shl(acc, 1));
+}
+
+/* dc_rmv's three cascaded iir_2nd_d sections (melp_sub.c:211-245), in -> out,
+ * sample by sample (equal to the reference's three in-place passes),
+ * samples in blocks of 4 */
+MD void iir3_d(const int16_t *in, int16_t *out, const int16_t *den, const int16_t *num,
+	       int16_t *din, int16_t *dhi, int16_t *dlo, int n)
+{
+	Biqd b[3];
+	for (int s = 0; s < 3; s++) {
+		b[s].n0 = num[3 * s];
+		b[s].n1 = num[3 * s + 1];
+		b[s].n2 = num[3 * s + 2];
+		b[s].d1 = den[3 * s + 1];
+		b[s].d2 = den[3 * s + 2];
+		b[s].i0 = din[2 * s];
+		b[s].i1 = din[2 * s + 1];
+		b[s].h0 = dhi[2 * s];
+		b[s].h1 = dhi[2 * s + 1];
+		b[s].l0 = dlo[2 * s];
+		b[s].l1 = dlo[2 * s + 1];
+	}
+	int i = 0;
+	for (; i + 4 <= n; i += 4) {
+		int16_t v0 = in[i], v1 = in[i + 1], v2 = in[i + 2], v3 = in[i + 3];
+		out[i] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], v0)));
+		out[i + 1] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], v1)));
+		out[i + 2] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], v2)));
+		out[i + 3] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], v3)));
+	}
+	for (; i < n; i++)
+		out[i] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], in[i])));
+	for (int s = 0; s < 3; s++) {
+		din[2 * s] = b[s].i0;
+		din[2 * s + 1] = b[s].i1;
+		dhi[2 * s] = b[s].h0;
+		dhi[2 * s + 1] = b[s].h1;
+		dlo[2 * s] = b[s].l0;
+		dlo[2 * s + 1] = b[s].l1;
+	}
+}
+
 /* ------------------------------------------------------------------ */
 /* LPC: melpe/lpc_lib.c                                               */
 /* ------------------------------------------------------------------ */

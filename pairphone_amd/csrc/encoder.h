@@ -19,7 +19,7 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 {
 	PROF_SCOPE(1);
 	int16_t *sb = E->sigbuf;
-	int16_t ac[17], lpc[LPC_ORD + 1], tdin[LPF_ORD], tdout[LPF_ORD];
+	int16_t ac[17], lpc[LPC_ORD + 1];
 	Word16 sub_pitch, t, dontcare, pcorr;
 	if (!E->ana_started) {
 		v_zero(E->lpfsp_delin, LPF_ORD);
@@ -31,18 +31,8 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 	/* lowpass for the global pitch; the filter memory advances by FRAME only
 	 * (melp_ana.c:324-346) */
 	v_copy(&sb[LPF_ORD], &speech[PITCH_BEG], PITCH_FR);
-	for (int s = 0; s < LPF_ORD / 2; s++) {
-		for (int i = s * 2; i < s * 2 + 2; i++)
-			tdin[i] = sb[LPF_ORD + FRAME - 1 - i + s * 2];
-		iir_2nd_s(&sb[LPF_ORD], TB(lpf_den) + s * 3, TB(lpf_num) + s * 3, &sb[LPF_ORD],
-			  &E->lpfsp_delin[s * 2], &E->lpfsp_delout[s * 2], FRAME);
-		v_copy(&tdout[2 * s], &E->lpfsp_delout[2 * s], 2);
-		iir_2nd_s(&sb[LPF_ORD + FRAME], TB(lpf_den) + s * 3, TB(lpf_num) + s * 3,
-			  &sb[LPF_ORD + FRAME], &E->lpfsp_delin[s * 2], &E->lpfsp_delout[s * 2],
-			  PITCH_FR - FRAME);
-		v_copy(&E->lpfsp_delin[2 * s], &tdin[2 * s], 2);
-		v_copy(&E->lpfsp_delout[2 * s], &tdout[2 * s], 2);
-	}
+	iir3_s(&sb[LPF_ORD], TB(lpf_den), TB(lpf_num), E->lpfsp_delin, E->lpfsp_delout,
+	       PITCH_FR, FRAME);
 	f_pitch_scale(&sb[LPF_ORD], &sb[LPF_ORD], PITCH_FR);
 	E->fpitch[1] = find_pitch(&sb[LPF_ORD + PITCH_FR / 2], &dontcare, 2 * PITCHMIN,
 				  PITCHMAX, PITCHMAX);

@@ -307,19 +307,22 @@ MD Word40 L40_sub(Word40 acc, Word32 x) { OPC(28); return clamp40(acc - (Word40)
 MD Word40 L40_mac(Word40 acc, Word16 a, Word16 b) { OPC(29); return clamp40(acc + (Word40) a * (Word40) b * 2); }
 MD Word40 L40_msu(Word40 acc, Word16 a, Word16 b) { OPC(30); return clamp40(acc - (Word40) a * (Word40) b * 2); }
 MD Word40 L40_shr(Word40 acc, Word16 n);
+/* the reference doubles with a clamp test per step (mathhalf_i.h); as the
+ * magnitude only grows, that equals one clamp of acc * 2^n */
 MD Word40 L40_shl(Word40 acc, Word16 n)
 {
 	OPC(31);
 	if (n < 0)
 		return L40_shr(acc, (Word16) -n);
-	for (; n > 0; n--) {
-		acc *= 2;
-		if (acc > MAX40_)
-			return MAX40_;
-		if (acc < MIN40_)
-			return MIN40_;
-	}
-	return acc;
+	if (n == 0 || acc == 0)
+		return acc;
+	if (n >= 40)
+		return acc > 0 ? MAX40_ : MIN40_;
+	if (acc > (MAX40_ >> n))
+		return MAX40_;
+	if (acc < (MIN40_ >> n))
+		return MIN40_;
+	return acc * ((Word40) 1 << n);
 }
 MD Word40 L40_shr(Word40 acc, Word16 n)
 {
@@ -334,30 +337,32 @@ MD Word40 L40_negate(Word40 acc)
 	acc = -acc;
 	return acc > MAX40_ ? MAX40_ : acc;
 }
+/* norm32 (mathhalf_i.h:2108): the shift that brings acc into [2^30, 2^31)
+ * (positive) or [-2^31, -2^30) (negative) by the reference's halving /
+ * doubling loops, in closed form: 30 - floor(log2 acc) for acc > 0,
+ * 31 - ceil(log2 -acc) for acc < 0 */
 MD Word16 norm32(Word40 acc)
 {
 	OPC(34);
-	Word16 n = 0;
 	if (acc > 0) {
-		while (acc > (Word40) LW_MAX_) {
-			acc >>= 1;
-			n--;
-		}
-		while (acc < ((Word40) 1 << 30)) {
-			acc *= 2;
-			n++;
-		}
-	} else if (acc < 0) {
-		while (acc < (Word40) LW_MIN_) {
-			acc >>= 1;
-			n--;
-		}
-		while (acc >= -((Word40) 1 << 30)) {
-			acc *= 2;
-			n++;
-		}
+#if defined(__HIP__)
+		return (Word16) (30 - (63 - __clzll(acc)));
+#else
+		return (Word16) (30 - (63 - __builtin_clzll((unsigned long long) acc)));
+#endif
 	}
-	return n;
+	if (acc < 0) {
+		uint64_t m = (uint64_t) (-acc);
+		if (m == 1)
+			return 31;
+#if defined(__HIP__)
+		int cl = 64 - __clzll((long long) (m - 1));	/* ceil(log2 m) */
+#else
+		int cl = 64 - __builtin_clzll(m - 1);
+#endif
+		return (Word16) (31 - cl);
+	}
+	return 0;
 }
 MD Word32 L_sat32(Word40 acc)
 {

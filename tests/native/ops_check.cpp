@@ -67,6 +67,19 @@ int main(int argc, char **argv)
 		CHK("mult-edge", mult(a, -32768), ref_mult(a, -32768));
 		CHK("div-edge", divide_s(a, 32767), ref_divide_s(a, 32767));
 	}
+	// 40-bit edges: +-2^k, +-2^k +- 1 for every k, every shift in [-45, 45]
+	for (int k = 0; k <= 39; k++)
+		for (int d = -1; d <= 1; d++)
+			for (int sg = -1; sg <= 1; sg += 2) {
+				int64_t z = sg * (((int64_t) 1 << k) + d);
+				if (z > ((int64_t) 1 << 39) || z < -((int64_t) 1 << 39))
+					continue;	/* outside the 40-bit format: the reference exits */
+				CHK("norm32-edge", norm32(z), ref_norm32(z));
+				for (int n = -45; n <= 45; n++) {
+					CHK("L40_shl-edge", L40_shl(z, n), ref_L40_shl(z, n));
+					CHK("L40_shr-edge", L40_shr(z, n), ref_L40_shr(z, n));
+				}
+			}
 	for (long i = 0; i < nrand; i++) {
 		int32_t x = rnd32(), y = rnd32();
 		int16_t a = rnd16(), b = rnd16(), n = (int16_t) ((int) (rnd() % 81) - 40);
