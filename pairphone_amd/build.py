@@ -76,7 +76,8 @@ def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=
     os.makedirs(objdir, exist_ok=True)
     common = [HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-c",
               "-Wno-unused-result", "-Wno-unused-value", '-DMELPE_TABLES_BIN="%s"' % blob] \
-        + (["-DMELPE_PROF"] if prof else []) + ["-D" + d for d in defs]
+        + (["-DMELPE_PROF"] if prof else []) + ["-D" + d for d in defs] \
+        + os.environ.get("MELPE_EXTRA_FLAGS", "").split()
     procs, objs = [], []
     for tu in TUS:
         o = os.path.join(objdir, tu + ".o")

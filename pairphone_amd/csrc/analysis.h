@@ -726,6 +726,8 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 	 * lo = 1 + n/2) sharing the sample loads of one pass. */
 	const int NL = MAXPITCH - MINPITCH;	/* 127 lags 146..20 */
 	int64_t blk[8];
+	{
+	PROF_SCOPE(39);
 	for (int i = MAXPITCH - 1; i >= MINPITCH; i--) {
 		int n = MAXPITCH - 1 - i;
 		if ((n & 7) == 0 && n + 8 <= NL) {
@@ -777,6 +779,8 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 		}
 		gp[i] = cor_gain(&Lr0, &r0s, rks, Lrk, A, true);
 	}
+	}
+	PROF_SCOPE(40);
 	peak[MINPITCH] = (gp[MINPITCH + 1] < gp[MINPITCH]) ? gp[MINPITCH] : (int16_t) 0;
 	peak[MAXPITCH] = (gp[MAXPITCH] > gp[MAXPITCH - 1]) ? gp[MAXPITCH] : (int16_t) 0;
 	for (int i = MINPITCH + 1; i < MAXPITCH; i++)

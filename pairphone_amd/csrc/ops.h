@@ -73,6 +73,8 @@ struct StageScope {
 #else
 #define OPC(k)
 #endif
+#define PROF_CAT2(a, b) a##b
+#define PROF_CAT(a, b) PROF_CAT2(a, b)
 /* Stage timer (profiling build only, -DMELPE_PROF): PROF_SCOPE(k) adds the
  * wave's s_memtime ticks spent in the enclosing function to g_prof[k]
  * (inclusive of callees; first active lane records).  tools/stage_prof.py. */
@@ -93,9 +95,9 @@ struct ProfScope {
 			atomicAdd(&g_prof[k], dt);
 	}
 };
-#define PROF_SCOPE(k) ProfScope prof_scope_(k)
+#define PROF_SCOPE(k) ProfScope PROF_CAT(prof_scope_, __LINE__)(k)
 #elif defined(MELPE_OPCOUNT) && !defined(__HIP__)
-#define PROF_SCOPE(k) StageScope stage_scope_(k)
+#define PROF_SCOPE(k) StageScope PROF_CAT(stage_scope_, __LINE__)(k)
 #else
 #define PROF_SCOPE(k)
 #endif

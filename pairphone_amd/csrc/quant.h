@@ -29,15 +29,22 @@ MN void vq_lspw(int16_t *w, const int16_t *lsp, const int16_t *lpc, int order)
 }
 
 /* vq_enc, melpe/vq_lib.c:474 -- full search, first minimum wins */
-MN Word32 vq_enc(const int16_t *cb, const int16_t *u, int levels, int order, int16_t *uhat,
+template <int ORDER>
+MN Word32 vq_enc(const int16_t *cb, const int16_t *u_in, int levels, int16_t *uhat,
 		 int16_t *index)
 {
+	const int order = ORDER;
+	int16_t u[ORDER];	/* the target in registers for the codebook scan */
+#pragma unroll
+	for (int j = 0; j < ORDER; j++)
+		u[j] = u_in[j];
 	int16_t best = 0;
 	Word32 dmin = LW_MAX_;
 	const int16_t *p = cb;
 	for (int i = 0; i < levels; i++) {
 		Word32 d = 0;
-		for (int j = 0; j < order; j++) {
+#pragma unroll
+		for (int j = 0; j < ORDER; j++) {
 			Word16 t = sub(u[j], *p++);
 			d = L_mac(d, t, t);
 		}
@@ -72,9 +79,17 @@ MD void vq_fsw(int16_t *wfs, int nh, Word16 pitch)
 
 /* wvq1 :221 -- keeps `cand` best entries; a new entry replaces the slot
  * holding the current maximum, exactly as the reference's linear rescan */
-MN void wvq1(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int dim, int cbsize,
+template <int DIM>
+MN void wvq1(const int16_t *tgt_in, const int16_t *wt_in, const int16_t *cb, int cbsize,
 	     int16_t *index, Word32 *dist, int cand)
 {
+	const int dim = DIM;
+	int16_t tgt[DIM], wt[DIM];	/* in registers for the codebook scan */
+#pragma unroll
+	for (int j = 0; j < DIM; j++) {
+		tgt[j] = tgt_in[j];
+		wt[j] = wt_in[j];
+	}
 	for (int j = 0; j < cand; j++)
 		dist[j] = LW_MAX_;
 	Word32 maxd = LW_MAX_;
@@ -103,9 +118,17 @@ MN void wvq1(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int dim, 
 }
 
 /* wvq2 :302 */
-MN int16_t wvq2(const int16_t *tgt, const int16_t *wt, const int16_t *cb, int dim,
+template <int DIM>
+MN int16_t wvq2(const int16_t *tgt_in, const int16_t *wt_in, const int16_t *cb,
 		const int16_t *index, const Word32 *dist, int cand)
 {
+	const int dim = DIM;
+	int16_t tgt[DIM], wt[DIM];
+#pragma unroll
+	for (int j = 0; j < DIM; j++) {
+		tgt[j] = tgt_in[j];
+		wt[j] = wt_in[j];
+	}
 	Word32 mn = LW_MAX_;
 	int16_t ind = 0;
 	for (int i = 0; i < cand; i++) {
@@ -182,7 +205,7 @@ MN void pitch_vq(EncState *E, MelpParam *par)
 			cb = TB(pitch_vq_cb_uvv);
 			size = 512;
 		}
-		wvq1(tgt, wt, cb, NF, size, il, dl, PITCH_VQ_CAND);
+		wvq1<NF>(tgt, wt, cb, size, il, dl, PITCH_VQ_CAND);
 		Word16 k = 0;
 		for (int i = 0; i < PITCH_VQ_CAND; i++) {
 			Word16 t2 = extract_l(L_shr(L_mult(il[i], NF), 1));
@@ -191,7 +214,7 @@ MN void pitch_vq(EncState *E, MelpParam *par)
 			v_sub(&dcb[k + 1], &cb[t2], NF - 1);
 			k = add(k, NF);
 		}
-		int16_t pi = wvq2(deltp, deltw, dcb, NF, il, dl, PITCH_VQ_CAND);
+		int16_t pi = wvq2<NF>(deltp, deltw, dcb, il, dl, PITCH_VQ_CAND);
 		if (par[NF - 1].uv_flag)
 			E->pvq_prev_qpitch = LOG_UV_PITCH_Q12;
 		else
@@ -286,13 +309,43 @@ MN Word16 InsertCand(int c1, int s1, int16_t *dMin, Word16 dist, int16_t entry,
 	return dMin[LSP_VQ_CAND - 1];
 }
 
-/* lspVQ :482 -- M-best multistage search; qout receives the ncPrev best
- * reconstructions (dim each), cb_index their stage indices (tos each) */
-MN void lspVQ(const int16_t *target, const int16_t *weight, int16_t *qout, const int16_t *cb,
-	      int tos, const int16_t *cb_size, int16_t *cb_index, int dim, bool flag)
+/* WeightedMSE for a compile-time dimension, target and weights in
+ * registers (same arithmetic and early exit as WeightedMSE) */
+template <int DIM>
+MD Word16 WeightedMSE_t(const int16_t *w, const int16_t *x, const int16_t *tgt, Word16 max_dmin)
 {
+	Word32 d = 0;
+#pragma unroll
+	for (int i = 0; i < DIM / 2; i++) {
+		Word16 t = sub(x[i], tgt[i]);
+		d = L_mac(d, w[i], mult(t, t));
+	}
+	if (r_ound(d) >= max_dmin)
+		return SW_MAX_;
+#pragma unroll
+	for (int i = DIM / 2; i < DIM; i++) {
+		Word16 t = sub(x[i], tgt[i]);
+		d = L_mac(d, w[i], mult(t, t));
+	}
+	return r_ound(d);
+}
+
+/* lspVQ :482 -- M-best multistage search; qout receives the ncPrev best
+ * reconstructions (dim each), cb_index their stage indices (tos each).
+ * Specialised per dimension (10: the LSF stages, 20: the interpolation
+ * residual) so the target and weights of the codebook scan stay in
+ * registers. */
+template <int DIM>
+MD void lspVQ_t(const int16_t *target, const int16_t *weight, int16_t *qout, const int16_t *cb,
+		int tos, const int16_t *cb_size, int16_t *cb_index, bool flag)
+{
+	const int dim = DIM;
 	int16_t index[LSP_VQ_CAND][LSP_VQ_STAGES], nextIndex[LSP_VQ_CAND][LSP_VQ_STAGES];
-	int16_t cand[LSP_VQ_CAND][2 * LPC_ORD], ct[2 * LPC_ORD], dMin[LSP_VQ_CAND];
+	int16_t cand[LSP_VQ_CAND][2 * LPC_ORD], dMin[LSP_VQ_CAND];
+	int16_t wr[DIM];
+#pragma unroll
+	for (int i = 0; i < DIM; i++)
+		wr[i] = weight[i];
 	for (int i = 0; i < LSP_VQ_CAND; i++) {
 		v_zero(cand[i], dim);
 		v_zero(index[i], LSP_VQ_STAGES);
@@ -306,10 +359,12 @@ MN void lspVQ(const int16_t *target, const int16_t *weight, int16_t *qout, const
 		Word16 maxd = SW_MAX_;
 		for (int c1 = 0; c1 < ncPrev; c1++) {
 			off = 0;
-			v_copy(ct, target, dim);
-			v_sub(ct, cand[c1], dim);
+			int16_t ct[DIM];
+#pragma unroll
+			for (int i = 0; i < DIM; i++)
+				ct[i] = sub(target[i], cand[c1][i]);
 			for (int e = 0; e < cb_size[s1]; e++) {
-				Word16 d = WeightedMSE(dim, weight, cbp + off, ct, maxd);
+				Word16 d = WeightedMSE_t<DIM>(wr, cbp + off, ct, maxd);
 				if (d < maxd)
 					maxd = InsertCand(c1, s1, dMin, d, (int16_t) e, nextIndex, index);
 				off = add(off, (Word16) dim);
@@ -338,6 +393,15 @@ MN void lspVQ(const int16_t *target, const int16_t *weight, int16_t *qout, const
 		v_copy(&cb_index[i * tos], index[i], tos);
 		v_copy(&qout[i * dim], cand[i], dim);
 	}
+}
+
+MN void lspVQ(const int16_t *target, const int16_t *weight, int16_t *qout, const int16_t *cb,
+	      int tos, const int16_t *cb_size, int16_t *cb_index, int dim, bool flag)
+{
+	if (dim == 2 * LPC_ORD)
+		lspVQ_t<2 * LPC_ORD>(target, weight, qout, cb, tos, cb_size, cb_index, flag);
+	else
+		lspVQ_t<LPC_ORD>(target, weight, qout, cb, tos, cb_size, cb_index, flag);
 }
 
 /* lspStable :805 (the reference also prints a warning when unstable) */
@@ -554,7 +618,7 @@ MN void quant_fsmag(EncState *E, MelpParam *par)
 		}
 	}
 	if (cnt > 0)
-		vq_enc(TB(fsvq_cb), par[last].fs_mag, 256, NUM_HARM, qmag, &E->qpar.fs_index);
+		vq_enc<NUM_HARM>(TB(fsvq_cb), par[last].fs_mag, 256, qmag, &E->qpar.fs_index);
 	if (cnt > 1) {
 		if (E->fsm_prev_uv || par[0].uv_flag) {
 			for (int i = 0; i <= last; i++)
