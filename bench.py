@@ -12,12 +12,18 @@ the device before the timed region, so every step's PCM is resident in HBM;
 bitstreams stay on the device.  The decode leg (melpe_s of the bits just
 produced) is timed the same way and reported beside the headline.
 
+A step is two kernels on one stream: k_enc_npp (noise pre-processor, one
+wavefront per channel) then k_enc_ana (analysis + packing, one lane per
+channel); both are timed with HIP events around each launch.
+
 Roofline: the codec is bit-exact saturating int16/int32 arithmetic with
 serial recursions per channel, so it is bounded by INT VALU issue, not HBM
-and not MFMA.  achieved = W (basic ops per channel-superframe,
+and not MFMA.  For the dominant kernel (k_enc_ana) achieved =
+W_ana (the reference's basic ops per channel-superframe of the analysis,
 profiles/opcount.json, counted by tools/opcount.py on this same input) x
-channels / average kernel duration (HIP events on the launch stream);
-peak = 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz = 78.6 T lane-ops/s.
+channels / its average launch duration; peak = 256 CUs x 4 SIMDs x 32
+lanes/clk x 2.4 GHz = 78.6 T lane-ops/s.  traffic = HBM bytes per launch
+from the committed rocprofv3 --pmc passes at this channel count.
 
 cpu_baseline: the reference codec itself (oracle/_ref/ref_tool, compiled
 from /root/reference by oracle/Makefile), one process per core on a bounded
@@ -67,14 +73,18 @@ def opcount():
     return json.load(open(p))
 
 
-def pmc_traffic():
-    """HBM bytes per encode launch from the committed rocprofv3 --pmc pass
-    (profiles/*_pmc.json, written by tools/pmc_summary.py), or None."""
+def pmc_traffic(kernel, channels):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
+    passes (profiles/pmc_latest.json, written by tools/prof_summary.py), if
+    they were taken at this channel count; else None."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(p):
         return None
     d = json.load(open(p))
-    return d.get("encode_bytes_per_launch"), d.get("source")
+    if d.get("channels") != channels:
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    return None if k is None else k["bytes_per_launch"]
 
 
 def cpu_baseline(args, gpu_bits):
@@ -145,32 +155,45 @@ def main():
         if world > 1:
             dist.barrier()
 
-    def timed(fn):
+    def timed(fns):
+        """W untimed steps, then K timed steps bracketed by barrier + sync;
+        each step runs the launches in `fns` (callables of the step index)
+        in order on `stream`, with a HIP event around each launch.  Returns
+        (wall seconds for K steps, max over ranks; mean ms per launch)."""
         for s in range(W):
-            fn(s)
+            for fn in fns:
+                fn(s)
         torch.cuda.synchronize(dev)
         barrier()
         torch.cuda.synchronize(dev)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(fns) + 1)]
               for _ in range(K)]
         t0 = time.perf_counter()
         for i in range(K):
             ev[i][0].record(stream)
-            fn(W + i)
-            ev[i][1].record(stream)
+            for j, fn in enumerate(fns):
+                fn(W + i)
+                ev[i][j + 1].record(stream)
         torch.cuda.synchronize(dev)
         barrier()
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
-        kms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        kms = [float(np.mean([ev[i][j].elapsed_time(ev[i][j + 1]) for i in range(K)]))
+               for j in range(len(fns))]
         if world > 1:
             t = torch.tensor([dt], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         return dt, kms
 
-    enc_s, enc_kms = timed(lambda s: eng.encode_dev(bits[s].data_ptr(), pcm[s].data_ptr(), None, sptr))
-    log("encode: %.1f ms/step (kernel %.1f ms)" % (1e3 * enc_s / K, enc_kms))
+    # one step = melpe_a on every channel = k_enc_npp then k_enc_ana
+    # (melpe_encode_npp_dev + melpe_encode_ana_dev == melpe_encode_dev)
+    enc_s, (npp_kms, ana_kms) = timed([
+        lambda s: eng.encode_npp_dev(pcm[s].data_ptr(), None, sptr),
+        lambda s: eng.encode_ana_dev(bits[s].data_ptr(), pcm[s].data_ptr(), None, sptr)])
+    enc_kms = npp_kms + ana_kms
+    log("encode: %.1f ms/step (k_enc_npp %.1f ms + k_enc_ana %.1f ms)"
+        % (1e3 * enc_s / K, npp_kms, ana_kms))
     # end-of-run bitstream gather (the only collective, outside the timed
     # region): every rank's K x C x 11 bytes to every rank, rank 0 keeps them
     from pairphone_amd.shard import gather_bitstreams
@@ -184,7 +207,8 @@ def main():
     dec = None
     if not args.no_decode:
         out = torch.empty((W + K, C, SF_SAMPLES), dtype=torch.int16, device=dev)
-        dec_s, dec_kms = timed(lambda s: eng.decode_dev(out[s].data_ptr(), bits[s].data_ptr(), None, sptr))
+        dec_s, (dec_kms,) = timed([lambda s: eng.decode_dev(out[s].data_ptr(), bits[s].data_ptr(),
+                                                            None, sptr)])
         dec = {"value": world * C * K * SF_SECONDS / dec_s, "unit": "channel-s/s decoded",
                "ms_per_step": 1e3 * dec_s / K, "kernel_ms": dec_kms}
         log("decode: %.1f ms/step (kernel %.1f ms)" % (1e3 * dec_s / K, dec_kms))
@@ -195,16 +219,30 @@ def main():
     oc = opcount()
     roof = None
     if oc:
-        ach = oc["W_enc_per_sf"] * C / (enc_kms / 1e3) / 1e12
-        tr = pmc_traffic()
-        roof = {"bound": "valu", "achieved": ach, "peak": PEAK_VALU_TOPS,
-                "unit": "T basic-ops/s (INT32 VALU lane-ops)", "frac": ach / PEAK_VALU_TOPS,
-                "traffic": tr[0] if tr else None,
-                "kernel": "k_encode", "kernel_ms": enc_kms,
-                "W_per_channel_superframe": oc["W_enc_per_sf"],
-                "algorithmic_hbm_bytes_per_launch": C * (2 * SF_SAMPLES * 2 + SF_BYTES)}
+        def kroof(kernel, W_sf, kms, in_b, out_b):
+            ach = W_sf * C / (kms / 1e3) / 1e12
+            return {"kernel": kernel, "kernel_ms": kms, "W_per_channel_superframe": W_sf,
+                    "achieved": ach, "frac": ach / PEAK_VALU_TOPS,
+                    "algorithmic_hbm_bytes_per_launch": C * (in_b + out_b),
+                    "traffic": pmc_traffic(kernel, C)}
+        # the dominant kernel of the step (analysis) carries the headline
+        # roofline; the NPP kernel and the whole step are listed beside it
+        ana = kroof("k_enc_ana", oc["W_enc_ana_per_sf"], ana_kms, 2 * SF_SAMPLES, SF_BYTES)
+        npp = kroof("k_enc_npp", oc["W_enc_npp_per_sf"], npp_kms, 2 * SF_SAMPLES, 2 * SF_SAMPLES)
+        step_ach = oc["W_enc_per_sf"] * C / (enc_kms / 1e3) / 1e12
+        roof = {"bound": "valu", "achieved": ana["achieved"], "peak": PEAK_VALU_TOPS,
+                "unit": "T basic-ops/s (INT32 VALU lane-ops)", "frac": ana["frac"],
+                "traffic": ana["traffic"], "kernel": "k_enc_ana", "kernel_ms": ana_kms,
+                "W_per_channel_superframe": ana["W_per_channel_superframe"],
+                "algorithmic_hbm_bytes_per_launch": ana["algorithmic_hbm_bytes_per_launch"],
+                "kernels": [ana, npp],
+                "encode_step": {"W_per_channel_superframe": oc["W_enc_per_sf"],
+                                "kernel_ms": enc_kms, "achieved": step_ach,
+                                "frac": step_ach / PEAK_VALU_TOPS}}
         if dec:
             dec["roofline_frac"] = oc["W_dec_per_sf"] * C / (dec["kernel_ms"] / 1e3) / 1e12 / PEAK_VALU_TOPS
+            dec["W_per_channel_superframe"] = oc["W_dec_per_sf"]
+            dec["traffic"] = pmc_traffic("k_decode", C)
     base, parity = (None, None)
     if world == 1:
         base, parity = cpu_baseline(args, bits[:W + K, :args.cpu_sample_channels].cpu().numpy())

@@ -50,6 +50,15 @@ int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp,
 int melpe_encode_dev(melpe_engine *e, void *d_bits, void *d_sp,
 		     const void *d_active, void *hip_stream);
 
+/* The two halves of melpe_encode_dev, enqueued separately (e.g. to time
+ * each kernel): the noise pre-processor on the superframe's three frames,
+ * in place (melpe/melpe.c:94-96), then analysis + packing
+ * (melpe/melpe.c:97-98).  encode_npp followed by encode_ana on the same
+ * buffers and stream is exactly melpe_encode_dev. */
+int melpe_encode_npp_dev(melpe_engine *e, void *d_sp, const void *d_active, void *hip_stream);
+int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const void *d_active,
+			 void *hip_stream);
+
 /* melpe_s on every active channel: bits (C x 11, in), sp (C x 540, out) */
 int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
 		      const uint8_t *active);

@@ -39,6 +39,8 @@ def load_library(path=None):
         "melpe_engine_reset": (i32, [vp, vp, i32]),
         "melpe_encode_host": (i32, [vp, vp, vp, vp]),
         "melpe_encode_dev": (i32, [vp, vp, vp, vp, vp]),
+        "melpe_encode_npp_dev": (i32, [vp, vp, vp, vp]),
+        "melpe_encode_ana_dev": (i32, [vp, vp, vp, vp, vp]),
         "melpe_decode_host": (i32, [vp, vp, vp, vp]),
         "melpe_decode_dev": (i32, [vp, vp, vp, vp, vp]),
         "melpe_npp_host": (i32, [vp, vp, i32, i32, vp]),
@@ -146,6 +148,12 @@ class MelpeEngine:
 
     def encode_dev(self, d_bits, d_sp, d_active=None, stream=None):
         _check(self.lib.melpe_encode_dev(self.h, d_bits, d_sp, d_active, stream))
+
+    def encode_npp_dev(self, d_sp, d_active=None, stream=None):
+        _check(self.lib.melpe_encode_npp_dev(self.h, d_sp, d_active, stream))
+
+    def encode_ana_dev(self, d_bits, d_sp, d_active=None, stream=None):
+        _check(self.lib.melpe_encode_ana_dev(self.h, d_bits, d_sp, d_active, stream))
 
     def decode_dev(self, d_sp, d_bits, d_active=None, stream=None):
         _check(self.lib.melpe_decode_dev(self.h, d_sp, d_bits, d_active, stream))

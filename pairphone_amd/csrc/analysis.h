@@ -238,9 +238,13 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 			int b0 = cb0 + (n + 8) / 2 + upper - n - 7;
 			fp_corr8(&sig[c_n0], &sig[b0], len, blk);
 		}
-		if (n < (nlags & ~7))
+		if (n < (nlags & ~7)) {
 			corr = blk[n & 7];
-		else
+			/* census: the reference's L_v_inner tail per lag */
+			OPC_ADD(OP_add, 2);
+			OPC_ADD(OP_sub, 1);
+			OPC_ADD(OP_L_shl, 1);
+		} else
 			corr = L_v_inner(&sig[cb], &sig[cb + i], len, 0, 0, 1);
 		Word16 s1a = norm_s(extract_h(c00));
 		Word16 s1b = norm_s(extract_h(cTT));
@@ -333,6 +337,12 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 			b1 = b2;
 		}
 	}
+	/* census: the reference's two L_v_magsq and six L_v_inner calls */
+	OPC_ADD(OP_L_mac, -len);
+	OPC_ADD(OP_shl, 2);
+	OPC_ADD(OP_sub, 10);
+	OPC_ADD(OP_add, 12);
+	OPC_ADD(OP_L_shl, 8);
 	Word32 ttm = m2;	/* sum of b_j^2, j < len */
 	m2 = L_mac(m2, sig[cb + ip - 1 + len], sig[cb + ip - 1 + len]);
 	m2 = L_mac(m2, sig[cb + ip + len], sig[cb + ip + len]);
@@ -772,6 +782,7 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 		}
 		if (n < (NL & ~7)) {
 			A = blk[n & 7];
+			OPC_ADD(OP_L40_mac, PW);	/* census: the reference's per-lag sum */
 		} else {
 			A = 0;
 			for (int j = lo; j < lo + PW; j++)

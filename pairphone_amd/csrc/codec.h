@@ -24,6 +24,7 @@ MD void derive_all(DerivedTables *d)
 	derive_fft_twiddles(d);
 	derive_lsp_cos(d);
 	derive_fs_weights(d);
+	derive_idft_cos(d);
 }
 
 }  // namespace mlp

@@ -687,20 +687,50 @@ MN Word16 low_rate_chn_read(DecState *D)
 /* harmonic excitation, melpe/harm.c                                   */
 /* ------------------------------------------------------------------ */
 
-/* realIDFT :63 -- direct real inverse DFT of one pitch period */
+/* realIDFT's cosine table entry i for period len (melpe/harm.c:70-80) */
+MD Word16 idft_cos_entry(Word16 len, int i)
+{
+	Word16 w = divide_s(16, len);	/* TWO_Q3 */
+	Word32 L = L_mult(w, (Word16) i);
+	if (L > 524288L)
+		L = L_sub(1048576L, L);
+	else if (L == 524288L)
+		L = L_sub(L, 1);
+	return cos_fxp(extract_l(L_shr(L, 4)));
+}
+
+MD void derive_idft_cos(DerivedTables *d)
+{
+	for (int len = 1; len <= PITCHMAX; len++)
+		for (int i = 0; i < len; i++)
+			d->idft_cos[len][i] = idft_cos_entry((Word16) len, i);
+}
+
+/* realIDFT :63 -- direct real inverse DFT of one pitch period.  The
+ * reference steps the cosine index k by adding phase[j], wrapping into
+ * [0, len), then subtracting phase[j] and adding i, so before harmonic j
+ * it is (j*i + phase[j]) mod len; that index is carried incrementally here
+ * (one conditional subtraction per step, phase[j] reduced mod len once).  The
+ * cosines come from the per-len table built at init. */
 MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 {
-	int16_t c[PITCHMAX];
 	Word16 len2 = add(shr(len, 1), 1);
 	Word16 w = divide_s(16, len);	/* TWO_Q3 */
-	for (int i = 0; i < len; i++) {
-		Word32 L = L_mult(w, (Word16) i);
-		if (L > 524288L)
-			L = L_sub(1048576L, L);
-		else if (L == 524288L)
-			L = L_sub(L, 1);
-		c[i] = cos_fxp(extract_l(L_shr(L, 4)));
+#if defined(MELPE_OPCOUNT)
+	/* census build: the reference's own sequence of basic ops (c[] built
+	 * per call, index stepped with add/sub wraps), same values */
+	int16_t cbuf[PITCHMAX];
+	for (int i = 0; i < len; i++)
+		cbuf[i] = idft_cos_entry(len, i);
+	const int16_t *c = cbuf;
+#else
+	const int16_t *c = g_der.idft_cos[len];
+	int16_t phm[PITCHMAX / 2 + 1];	/* phase[j] mod len, in [0, len) */
+	for (int j = 1; j < len2; j++) {
+		int p = phase[j] % len;
+		phm[j] = (int16_t) (p < 0 ? p + len : p);
 	}
+#endif
 	w = shr(w, 1);
 	Word16 w2 = shr(w, 1);
 	mag[0] = mult(mag[0], w2);
@@ -714,6 +744,7 @@ MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 		mag[i] = mult(mag[i], w);
 	for (i = 0; i < len; i++) {
 		Word32 L = L_deposit_h(mag[0]);
+#if defined(MELPE_OPCOUNT)
 		Word16 k = (Word16) i;
 		for (int j = 1; j < len2; j++) {
 			k = add(k, phase[j]);
@@ -725,6 +756,18 @@ MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 			k = sub(k, phase[j]);
 			k = add(k, (Word16) i);
 		}
+#else
+		int base = 0;	/* (j * i) mod len */
+		for (int j = 1; j < len2; j++) {
+			base += i;
+			if (base >= len)
+				base -= len;
+			int k = base + phm[j];
+			if (k >= len)
+				k -= len;
+			L = L_mac(L, mag[j], c[k]);
+		}
+#endif
 		sig[i] = r_ound(L);
 	}
 }

@@ -359,6 +359,28 @@ int melpe_encode_dev(melpe_engine *e, void *d_bits, void *d_sp, const void *d_ac
 			     (const uint8_t *) d_active, (hipStream_t) hip_stream, false);
 }
 
+int melpe_encode_npp_dev(melpe_engine *e, void *d_sp, const void *d_active, void *hip_stream)
+{
+	if (!e || !d_sp)
+		return fail_msg("melpe_encode_npp_dev: null argument");
+	HIPCHK(hipSetDevice(e->device));
+	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, (int16_t *) d_sp, (const uint8_t *) d_active,
+				       e->channels, (hipStream_t) hip_stream));
+	return 0;
+}
+
+int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const void *d_active,
+			 void *hip_stream)
+{
+	if (!e || !d_bits || !d_sp)
+		return fail_msg("melpe_encode_ana_dev: null argument");
+	HIPCHK(hipSetDevice(e->device));
+	HIPCHK((hipError_t) kl_enc_ana(e->d_enc, (const int16_t *) d_sp, (uint8_t *) d_bits,
+				       (const uint8_t *) d_active, e->channels,
+				       (hipStream_t) hip_stream));
+	return 0;
+}
+
 int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const uint8_t *active)
 {
 	if (!e || !bits || !sp)

@@ -88,6 +88,27 @@ int emu_encode(emu_engine *e, unsigned char *bits, int16_t *sp)
 	return 0;
 }
 
+/* the two halves of melpe_a, as the GPU runs them (k_enc_npp, k_enc_ana) */
+int emu_encode_npp(emu_engine *e, int16_t *sp)
+{
+	for (int c = 0; c < e->channels; c++) {
+		int16_t *x = sp + (size_t) c * BLOCK;
+		for (int f = 0; f < NF; f++)
+			npp_frame(&e->enc[c].npp, &g_npp_scratch, x + f * FRAME, x + f * FRAME);
+	}
+	return 0;
+}
+
+int emu_encode_ana(emu_engine *e, unsigned char *bits, const int16_t *sp)
+{
+	for (int c = 0; c < e->channels; c++) {
+		analysis(&e->enc[c], sp + (size_t) c * BLOCK);
+		for (int k = 0; k < 11; k++)
+			bits[c * 11 + k] = e->enc[c].chbuf[k];
+	}
+	return 0;
+}
+
 /* melpe_s on every channel: bits (C x 11) in, sp (C x 540) out */
 int emu_decode(emu_engine *e, int16_t *sp, const unsigned char *bits)
 {

@@ -70,9 +70,16 @@ struct StageScope {
 	~StageScope() { melpe_opstage = prev; }
 };
 #define OPC(k) OpScope op_scope_(k)
+/* n more (or, n < 0, fewer) top-level ops of kind k: keeps the census equal
+ * to the reference's op sequence where a code path computes the same values
+ * with fewer or different operations (blocked correlations, fused sums) */
+#define OPC_ADD(k, n) do { if (!melpe_opdepth) { melpe_opcount[k] += (uint64_t) (int64_t) (n); melpe_stagecount[melpe_opstage] += (uint64_t) (int64_t) (n); } } while (0)
 #else
 #define OPC(k)
+#define OPC_ADD(k, n) do { } while (0)
 #endif
+enum { OP_add = 0, OP_sub = 1, OP_L_sub = 3, OP_L_mult = 4, OP_extract_l = 6, OP_L_mac = 10, OP_shl = 18, OP_shr = 19,
+       OP_L_shr = 20, OP_L_shl = 21, OP_divide_s = 26, OP_L40_mac = 29 };
 #define PROF_CAT2(a, b) a##b
 #define PROF_CAT(a, b) PROF_CAT2(a, b)
 /* Stage timer (profiling build only, -DMELPE_PROF): PROF_SCOPE(k) adds the

@@ -314,6 +314,7 @@ MN Word16 InsertCand(int c1, int s1, int16_t *dMin, Word16 dist, int16_t entry,
 template <int DIM>
 MD Word16 WeightedMSE_t(const int16_t *w, const int16_t *x, const int16_t *tgt, Word16 max_dmin)
 {
+	OPC_ADD(OP_shr, 1);	/* census: the reference's shr(n, 1) */
 	Word32 d = 0;
 #pragma unroll
 	for (int i = 0; i < DIM / 2; i++) {

@@ -27,6 +27,9 @@ struct DerivedTables {
 	int16_t w_fs_inv[10];
 	int16_t pf_window[20];	/* postfilter gain cross-fade window */
 	int16_t pad[2];
+	/* realIDFT's cosine table for period len (melpe/harm.c:70-80): it
+	 * depends on len only, so it is built once for every len 1..160 */
+	int16_t idft_cos[161][160];
 };
 
 MDEV_CONST DerivedTables g_der;

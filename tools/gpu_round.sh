@@ -1,8 +1,8 @@
 # One GPU call: parity tests, the default bench line, the rocprofv3 kernel-trace
-# summary of the same bench command, and HBM-traffic PMC passes (one counter
-# group per pass).  Every GPU step has its own limit; steps chained with &&.
+# summary of the same bench command, and HBM-traffic / instruction PMC passes
+# (one counter group per pass, each its own run and limit); steps chained &&.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp &&
-timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 &&
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 &&
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err &&
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt -- python3 bench.py --no-cpu-baseline > gpurun_out/prof_kt.log 2>&1 &&
 B="bench.py --steps 2 --warmup 0 --no-cpu-baseline" &&

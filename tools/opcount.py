@@ -4,8 +4,9 @@ Runs the host count build of the device sources (build/libmelpe_opcount.so,
 -DMELPE_OPCOUNT) over the benchmark's own synthetic input (bench.py RUN_SEED,
 channels 0..N-1, 149 superframes each), counting every saturating basic op
 entered from codec code and not from inside another op.
-Encode = melpe_a (NPP x3 + analysis + packing); decode = melpe_s of the
-resulting bitstreams.  Writes profiles/opcount.json, which bench.py reads.
+Encode = melpe_a (NPP x3 + analysis + packing), split as the GPU runs it:
+W_enc_npp (k_enc_npp) and W_enc_ana (k_enc_ana); decode = melpe_s of the
+resulting bitstreams (k_decode).  Writes profiles/opcount.json, which bench.py reads.
 """
 import ctypes
 import json
@@ -37,10 +38,17 @@ def main(channels=32, nsf=149):
     e = lib.emu_create(channels)
     enc = np.zeros(64, np.uint64)
     dec = np.zeros(64, np.uint64)
+    lib.emu_encode_npp.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.emu_encode_ana.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    npp = np.zeros(64, np.uint64)
     for k in range(nsf):
         sp = np.ascontiguousarray(x[:, k * 540:(k + 1) * 540])
         b = np.zeros((channels, 11), np.uint8)
-        lib.emu_encode(e, b.ctypes.data, sp.ctypes.data)
+        lib.emu_encode_npp(e, sp.ctypes.data)
+        lib.emu_opcount(cnt.ctypes.data, 64)
+        npp += cnt
+        enc += cnt
+        lib.emu_encode_ana(e, b.ctypes.data, sp.ctypes.data)
         lib.emu_opcount(cnt.ctypes.data, 64)
         enc += cnt
         out = np.zeros((channels, 540), np.int16)
@@ -55,6 +63,8 @@ def main(channels=32, nsf=149):
                  % (bench.RUN_SEED, channels - 1, nsf),
         "channel_superframes": n,
         "W_enc_per_sf": float(enc.sum()) / n,
+        "W_enc_npp_per_sf": float(npp.sum()) / n,
+        "W_enc_ana_per_sf": float(enc.sum() - npp.sum()) / n,
         "W_dec_per_sf": float(dec.sum()) / n,
         "enc_by_op": {names[i]: float(enc[i]) / n for i in np.argsort(-enc.astype(np.float64))[:len(names)] if enc[i]},
         "dec_by_op": {names[i]: float(dec[i]) / n for i in np.argsort(-dec.astype(np.float64))[:len(names)] if dec[i]},

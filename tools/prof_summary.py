@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 output databases (rocpd SQLite) into profiles/.
 
-  python tools/prof_summary.py <gpurun_out dir> <tag>
+  python tools/prof_summary.py <gpurun_out dir> <tag> [channels]
 
 Reads   <dir>/prof_kt/*_results.db        (--kernel-trace --stats pass)
         <dir>/pmc_*/*_results.db          (one --pmc pass each)
@@ -69,8 +69,8 @@ def main():
     if pm:
         with open(os.path.join(prof, tag + "_pmc.txt"), "w") as f:
             f.write("# rocprofv3 --pmc passes (%s): mean counter value per dispatch\n" % tag)
-            for k in ("k_encode", "k_decode"):
-                if k not in pm:
+            for k in sorted(pm):
+                if not k.startswith("k_enc") and k != "k_decode":
                     continue
                 f.write("[%s]\n" % k)
                 for cn in sorted(pm[k]):
@@ -80,13 +80,13 @@ def main():
                     f.write("  wait_any/wave_cycles   %20.3f\n" % (d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]))
                 if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d:
                     f.write("  valu_insts_per_wave    %20.1f\n" % (d["SQ_INSTS_VALU"] / d["SQ_WAVES"]))
-        out = {"source": "profiles/%s_pmc.txt" % tag}
-        for k, key in (("k_encode", "encode"), ("k_decode", "decode")):
-            d = pm.get(k, {})
+        out = {"source": "profiles/%s_pmc.txt" % tag, "kernels": {},
+               "channels": int(sys.argv[3]) if len(sys.argv) > 3 else None}
+        for k, d in pm.items():
             if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
-                out[key + "_bytes_per_launch"] = (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
-                out[key + "_fetch_bytes"] = d["FETCH_SIZE"] * 1024.0
-                out[key + "_write_bytes"] = d["WRITE_SIZE"] * 1024.0
+                out["kernels"][k] = {"fetch_bytes": d["FETCH_SIZE"] * 1024.0,
+                                     "write_bytes": d["WRITE_SIZE"] * 1024.0,
+                                     "bytes_per_launch": (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0}
         json.dump(out, open(os.path.join(prof, "pmc_latest.json"), "w"), indent=1)
 
 
