@@ -194,6 +194,7 @@ MD void fp_corr8(const int16_t *pa, const int16_t *pb, int len, Word32 *out)
 	Word32 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	int16_t A0 = pa[0], A1 = pa[1], A2 = pa[2], A3 = pa[3];
 	int16_t B0 = pb[0], B1 = pb[1], B2 = pb[2];
+	#pragma unroll 4
 	for (int j = 0; j < len; j++) {
 		int16_t A4 = pa[j + 4], B3 = pb[j + 3];
 		acc[0] = L_mac(acc[0], A0, B3);
@@ -322,6 +323,7 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 	{
 		const int16_t *pa = &sig[cb], *pb = &sig[cb + ip - 1];
 		int16_t b0 = pb[0], b1 = pb[1];
+		#pragma unroll 4
 		for (int j = 0; j < len; j++) {
 			int16_t a = pa[j], b2 = pb[j + 2];
 			msq = L_mac(msq, a, a);
@@ -746,6 +748,7 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 			int64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 			int a0 = pa[0], a1 = pa[1], a2 = pa[2];
 			int q0 = pq[0], q1 = pq[1], q2 = pq[2], q3 = pq[3];
+			#pragma unroll 4
 			for (int t = 0; t < PW; t++) {
 				int a3 = pa[t + 3], q4 = pq[t + 4];
 				acc[0] += (int64_t) (a0 * q4);

@@ -327,16 +327,20 @@ MN void sc_ana(EncState *E, MelpParam *par)
 }
 
 /* analysis :119 -- 540 NPP-processed samples -> quantised params + chbuf */
-MN void analysis(EncState *E, const int16_t *sp_in)
+/* analysis() in the two parts the GPU runs as separate kernels:
+ * analysis_frame: dc removal and melp_ana of frame i (melp_ana.c:140-160);
+ * analysis_tail: sc_ana, the quantisers and channel packing (:162-265) */
+MD void analysis_frame(EncState *E, const int16_t *sp_in, int i)
 {
-	PROF_SCOPE(15);
+	dc_rmv(&sp_in[i * FRAME], &E->hpspeech[IN_BEG + i * FRAME], E->dcdelin,
+	       E->dcdelout_hi, E->dcdelout_lo, FRAME);
+	melp_ana(E, &E->hpspeech[i * FRAME], &E->par[i], i);
+}
+
+MN void analysis_tail(EncState *E)
+{
 	MelpParam *par = E->par;
 	int16_t lpc[LPC_ORD + 1];
-	for (int i = 0; i < NF; i++) {
-		dc_rmv(&sp_in[i * FRAME], &E->hpspeech[IN_BEG + i * FRAME], E->dcdelin,
-		       E->dcdelout_hi, E->dcdelout_lo, FRAME);
-		melp_ana(E, &E->hpspeech[i * FRAME], &par[i], i);
-	}
 	sc_ana(E, par);
 	lpc[0] = 4096;
 	lsf_vq(E, par);
@@ -362,6 +366,14 @@ MN void analysis(EncState *E, const int16_t *sp_in)
 		E->qpar.uv_flag[i] = par[i].uv_flag;
 	low_rate_chn_write(E);
 	v_copy(E->hpspeech, &E->hpspeech[NF * FRAME], IN_BEG);
+}
+
+MN void analysis(EncState *E, const int16_t *sp_in)
+{
+	PROF_SCOPE(15);
+	for (int i = 0; i < NF; i++)
+		analysis_frame(E, sp_in, i);
+	analysis_tail(E);
 }
 
 /* debug aid: analysis() stopped after `upto` of its stages (1 = dc_rmv +

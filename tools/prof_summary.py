@@ -63,6 +63,8 @@ def main():
                 f.write("%-14s %6d %14.1f %12.1f %7.2f\n" % (short(n)[:14], calls, tot / 1e3,
                                                            avg / 1e3, pct))
     pm = {}
+    if len(sys.argv) <= 3:	# PMC summaries only with the channel count they were taken at
+        return
     for db in sorted(glob.glob(os.path.join(src, "pmc_*", "*_results.db"))):
         for k, d in pmc_means(db).items():
             pm.setdefault(k, {}).update(d)
