@@ -32,7 +32,7 @@ using namespace mlp;
 /* minimum resident waves per SIMD the encoder / decoder kernels are compiled
  * for (caps VGPRs at 512 / n) */
 #ifndef MELPE_ENC_WAVES
-#define MELPE_ENC_WAVES 2
+#define MELPE_ENC_WAVES 4
 #endif
 #ifndef MELPE_DEC_WAVES
 #define MELPE_DEC_WAVES 4

@@ -460,7 +460,10 @@ MN void lsf_vq(EncState *E, MelpParam *par)
 	int16_t best0[LPC_ORD], best1[LPC_ORD], res[2 * LPC_ORD];
 	int16_t lcand[LSP_INP_CAND][LPC_ORD], lidx[LSP_INP_CAND * LSP_VQ_STAGES];
 	int16_t il0[LPC_ORD], il1[LPC_ORD];
-	int16_t *lsp[NF];
+	/* lsp(i) is par[i].lsf; written as a macro, not an array of pointers:
+	 * a pointer loaded back from memory loses its address space and turns
+	 * every access through it into a generic (FLAT) access */
+#define lsp(i) (par[i].lsf)
 	if (!E->lsf_started) {
 		Word16 t2 = shl(LPC_ORD, 10), t1 = 819;
 		for (int i = 0; i < LPC_ORD; i++) {
@@ -470,9 +473,8 @@ MN void lsf_vq(EncState *E, MelpParam *par)
 		E->lsf_started = 1;
 	}
 	for (int i = 0; i < NF; i++) {
-		lsp[i] = par[i].lsf;
-		lpc_lsp2pred(lsp[i], lpc, LPC_ORD);
-		vq_lspw(wgt[i], lsp[i], lpc, LPC_ORD);
+		lpc_lsp2pred(lsp(i), lpc, LPC_ORD);
+		vq_lspw(wgt[i], lsp(i), lpc, LPC_ORD);
 	}
 	Word16 uvc = 0;
 	for (int i = 0; i < NF; i++) {
@@ -490,20 +492,20 @@ MN void lsf_vq(EncState *E, MelpParam *par)
 		for (int i = 0; i < NF; i++) {
 			bool uv = (uvc >> (NF - 1 - i)) & 1;
 			if (uv)
-				lspVQ(lsp[i], wgt[i], lsp[i], cb_uv, 1, uv_cb_size, q->lsf_index[i],
+				lspVQ(lsp(i), wgt[i], lsp(i), cb_uv, 1, uv_cb_size, q->lsf_index[i],
 				      LPC_ORD, false);
 			else
-				lspVQ(lsp[i], wgt[i], lsp[i], cb_v, 4, melp_cb_size, q->lsf_index[i],
+				lspVQ(lsp(i), wgt[i], lsp(i), cb_v, 4, melp_cb_size, q->lsf_index[i],
 				      LPC_ORD, false);
 		}
 	} else {
 		int tos;
 		if (uvc == 1) {
 			tos = 1;
-			lspVQ(lsp[2], wgt[2], lcand[0], cb_uv, tos, uv_cb_size, lidx, LPC_ORD, true);
+			lspVQ(lsp(2), wgt[2], lcand[0], cb_uv, tos, uv_cb_size, lidx, LPC_ORD, true);
 		} else {
 			tos = 4;
-			lspVQ(lsp[2], wgt[2], lcand[0], cb_v, tos, melp_cb_size, lidx, LPC_ORD, true);
+			lspVQ(lsp(2), wgt[2], lcand[0], cb_v, tos, melp_cb_size, lidx, LPC_ORD, true);
 		}
 		Word32 minErr = LW_MAX_;
 		int cand = 0;
@@ -517,15 +519,15 @@ MN void lsf_vq(EncState *E, MelpParam *par)
 					Word32 acc = L_mult(f, E->qplsp[j]);
 					acc = L_mac(acc, sub(16384, f), lcand[k][j]);
 					il0[j] = extract_h(L_shl(acc, 1));
-					acc = L_sub(acc, L_shl(L_deposit_l(lsp[0][j]), 15));
+					acc = L_sub(acc, L_shl(L_deposit_l(lsp(0)[j]), 15));
 					f = ic[i * 20 + j + LPC_ORD];
 					Word32 bcc = L_mult(f, E->qplsp[j]);
 					bcc = L_mac(bcc, sub(16384, f), lcand[k][j]);
 					il1[j] = extract_h(L_shl(bcc, 1));
-					bcc = L_sub(bcc, L_shl(L_deposit_l(lsp[1][j]), 15));
+					bcc = L_sub(bcc, L_shl(L_deposit_l(lsp(1)[j]), 15));
 					err = L_add(err, lsf_werr(acc, wgt[0][j]));
 					err = L_add(err, lsf_werr(bcc, wgt[1][j]));
-					acc = L_shl(L_deposit_l(lsp[2][j]), 15);
+					acc = L_shl(L_deposit_l(lsp(2)[j]), 15);
 					acc = L_sub(acc, L_shl(L_deposit_l(lcand[k][j]), 15));
 					err = L_add(err, lsf_werr(acc, wgt[2][j]));
 				}
@@ -537,27 +539,28 @@ MN void lsf_vq(EncState *E, MelpParam *par)
 					v_copy(best1, il1, LPC_ORD);
 				}
 			}
-		v_copy(lsp[2], lcand[cand], LPC_ORD);
+		v_copy(lsp(2), lcand[cand], LPC_ORD);
 		v_copy(q->lsf_index[0], &lidx[cand * tos], tos);
 		q->lsf_index[1][0] = inp;
 		for (int i = 0; i < LPC_ORD; i++) {
-			res[i] = shl(sub(lsp[0][i], best0[i]), 2);
-			res[i + LPC_ORD] = shl(sub(lsp[1][i], best1[i]), 2);
+			res[i] = shl(sub(lsp(0)[i], best0[i]), 2);
+			res[i + LPC_ORD] = shl(sub(lsp(1)[i], best1[i]), 2);
 		}
 		v_copy(mwgt, wgt[0], LPC_ORD);
 		v_copy(mwgt + LPC_ORD, wgt[1], LPC_ORD);
 		lspVQ(res, mwgt, res, TB(res256x64x64x64), uvc == 1 ? 4 : 2, res_cb_size,
 		      q->lsf_index[2], 2 * LPC_ORD, false);
 		for (int i = 0; i < LPC_ORD; i++) {
-			lsp[0][i] = add(shr(res[i], 2), best0[i]);
-			lsp[1][i] = add(shr(res[i + LPC_ORD], 2), best1[i]);
+			lsp(0)[i] = add(shr(res[i], 2), best0[i]);
+			lsp(1)[i] = add(shr(res[i + LPC_ORD], 2), best1[i]);
 		}
 	}
-	lspStable(lsp[0], LPC_ORD);
-	lspStable(lsp[1], LPC_ORD);
-	if (!lspStable(lsp[2], LPC_ORD))
-		lspSort(lsp[2], LPC_ORD);
-	v_copy(E->qplsp, lsp[2], LPC_ORD);
+	lspStable(lsp(0), LPC_ORD);
+	lspStable(lsp(1), LPC_ORD);
+	if (!lspStable(lsp(2), LPC_ORD))
+		lspSort(lsp(2), LPC_ORD);
+	v_copy(E->qplsp, lsp(2), LPC_ORD);
+#undef lsp
 }
 
 /* quant_jitter :1198 */
