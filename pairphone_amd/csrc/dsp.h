@@ -538,11 +538,63 @@ MD void zerflt_q_fixed(const int16_t *in, const int16_t *c, int16_t *out, int n,
 	}
 }
 
+/* long FIR (the decoder's 65-tap dispersion filter): eight outputs share a
+ * sliding window of eight inputs, one new load per tap; each output keeps
+ * the reference's tap-order L_mac chain */
+MD void zerflt_q_long(const int16_t *in, const int16_t *c, int16_t *out, int order, int n,
+		      Word16 sc)
+{
+	int i = n - 1;
+	for (; i >= 7; i -= 8) {
+		Word16 w0 = in[i], w1 = in[i - 1], w2 = in[i - 2], w3 = in[i - 3];
+		Word16 w4 = in[i - 4], w5 = in[i - 5], w6 = in[i - 6], w7 = in[i - 7];
+		Word32 a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
+		for (int j = 0; j <= order; j++) {
+			Word16 cj = c[j];
+			a0 = L_mac(a0, w0, cj);
+			a1 = L_mac(a1, w1, cj);
+			a2 = L_mac(a2, w2, cj);
+			a3 = L_mac(a3, w3, cj);
+			a4 = L_mac(a4, w4, cj);
+			a5 = L_mac(a5, w5, cj);
+			a6 = L_mac(a6, w6, cj);
+			a7 = L_mac(a7, w7, cj);
+			w0 = w1;
+			w1 = w2;
+			w2 = w3;
+			w3 = w4;
+			w4 = w5;
+			w5 = w6;
+			w6 = w7;
+			if (j < order)	/* no read below in[-order] */
+				w7 = in[i - 8 - j];
+		}
+		out[i] = r_ound(L_shl(a0, sc));
+		out[i - 1] = r_ound(L_shl(a1, sc));
+		out[i - 2] = r_ound(L_shl(a2, sc));
+		out[i - 3] = r_ound(L_shl(a3, sc));
+		out[i - 4] = r_ound(L_shl(a4, sc));
+		out[i - 5] = r_ound(L_shl(a5, sc));
+		out[i - 6] = r_ound(L_shl(a6, sc));
+		out[i - 7] = r_ound(L_shl(a7, sc));
+	}
+	for (; i >= 0; i--) {
+		Word32 acc = 0;
+		for (int j = 0; j <= order; j++)
+			acc = L_mac(acc, in[i - j], c[j]);
+		out[i] = r_ound(L_shl(acc, sc));
+	}
+}
+
 MN void zerflt_Q(const int16_t *in, const int16_t *c, int16_t *out, int order,
 		 int n, Word16 qc)
 {
 	PROF_SCOPE(28);
 	Word16 sc = sub(15, qc);
+	if (order >= 16) {
+		zerflt_q_long(in, c, out, order, n, sc);
+		return;
+	}
 	if (order == 10) {
 		zerflt_q_fixed<10>(in, c, out, n, sc);
 		return;
