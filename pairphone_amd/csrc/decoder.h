@@ -914,18 +914,28 @@ MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_
 		if (i == 0) {
 			/* run the previous frame's filter over the first 20 samples for
 			 * the cross-fade tail */
-			v_copy(m1o, D->pf_mem1, LPC_ORD);
-			v_copy(m2o, D->pf_mem2, LPC_ORD);
+			Word16 af[LPC_ORD], ai[LPC_ORD];
+#pragma unroll
+			for (int k = 0; k < LPC_ORD; k++) {
+				m1o[k] = D->pf_mem1[k];
+				m2o[k] = D->pf_mem2[k];
+				af[k] = D->pf_aFIR[k];
+				ai[k] = D->pf_aIIR[k];
+			}
 			for (int j = 0; j < 20; j++) {
 				L = 0;
+#pragma unroll
 				for (int k = 0; k < LPC_ORD; k++)
-					L = L_add(L, L_mult(m1o[k], D->pf_aFIR[k]));
+					L = L_add(L, L_mult(m1o[k], af[k]));
+#pragma unroll
 				for (int k = LPC_ORD - 1; k > 0; k--)
 					m1o[k] = m1o[k - 1];
 				m1o[0] = synhp[j];
 				L = L_add(L, L_shl(L_deposit_l(synhp[j]), 13));
+#pragma unroll
 				for (int k = 0; k < LPC_ORD; k++)
-					L = L_sub(L, L_mult(m2o[k], D->pf_aIIR[k]));
+					L = L_sub(L, L_mult(m2o[k], ai[k]));
+#pragma unroll
 				for (int k = LPC_ORD - 1; k > 0; k--)
 					m2o[k] = m2o[k - 1];
 				t1 = extract_l(L_shr(L, 13));
@@ -943,21 +953,41 @@ MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_
 			t1 = mult(18678, t1);
 			t2 = mult(24576, t2);
 		}
-		for (int j = 0; j < 45; j++) {
-			L = 0;
-			for (int k = 0; k < LPC_ORD; k++)
-				L = L_add(L, L_mult(D->pf_mem1[k], D->pf_aFIR[k]));
-			for (int k = LPC_ORD - 1; k > 0; k--)
-				D->pf_mem1[k] = D->pf_mem1[k - 1];
-			D->pf_mem1[0] = synhp[j];
-			L = L_add(L, L_shl(L_deposit_l(synhp[j]), 13));
-			for (int k = 0; k < LPC_ORD; k++)
-				L = L_sub(L, L_mult(D->pf_mem2[k], D->pf_aIIR[k]));
-			for (int k = LPC_ORD - 1; k > 0; k--)
-				D->pf_mem2[k] = D->pf_mem2[k - 1];
-			L = L_shr(L, 13);
-			D->pf_mem2[0] = extract_l(L);
-			sp[i * 45 + j] = extract_l(L);
+		{	/* pole-zero filter; memories and coefficients held in
+			 * registers for the subframe (shifts become renames) */
+			Word16 m1[LPC_ORD], m2[LPC_ORD], af[LPC_ORD], ai[LPC_ORD];
+#pragma unroll
+			for (int k = 0; k < LPC_ORD; k++) {
+				m1[k] = D->pf_mem1[k];
+				m2[k] = D->pf_mem2[k];
+				af[k] = D->pf_aFIR[k];
+				ai[k] = D->pf_aIIR[k];
+			}
+			for (int j = 0; j < 45; j++) {
+				L = 0;
+#pragma unroll
+				for (int k = 0; k < LPC_ORD; k++)
+					L = L_add(L, L_mult(m1[k], af[k]));
+#pragma unroll
+				for (int k = LPC_ORD - 1; k > 0; k--)
+					m1[k] = m1[k - 1];
+				m1[0] = synhp[j];
+				L = L_add(L, L_shl(L_deposit_l(synhp[j]), 13));
+#pragma unroll
+				for (int k = 0; k < LPC_ORD; k++)
+					L = L_sub(L, L_mult(m2[k], ai[k]));
+#pragma unroll
+				for (int k = LPC_ORD - 1; k > 0; k--)
+					m2[k] = m2[k - 1];
+				L = L_shr(L, 13);
+				m2[0] = extract_l(L);
+				sp[i * 45 + j] = extract_l(L);
+			}
+#pragma unroll
+			for (int k = 0; k < LPC_ORD; k++) {
+				D->pf_mem1[k] = m1[k];
+				D->pf_mem2[k] = m2[k];
+			}
 		}
 	}
 	Word16 opE = pf_energy(sp, &op_sh);
@@ -982,9 +1012,8 @@ MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_
 	for (int i = 0; i < 20; i++)
 		sp[i] = add(mult(sp[i], (Word16) (i * 1638)), nokori[i]);
 	v_scale(sp, 29088, FRAME);
-	iir_2nd_d(sp, TB(lpf3500_den), TB(lpf3500_num), sp, D->lpf_din, D->lpf_dhi, D->lpf_dlo,
-		  FRAME);
-	iir_2nd_d(sp, TB(hpf60_den), TB(hpf60_num), sp, D->hpf_din, D->hpf_dhi, D->hpf_dlo, FRAME);
+	iir2_d(sp, TB(lpf3500_den), TB(lpf3500_num), D->lpf_din, D->lpf_dhi, D->lpf_dlo,
+	       TB(hpf60_den), TB(hpf60_num), D->hpf_din, D->hpf_dhi, D->hpf_dlo, FRAME);
 }
 
 /* ------------------------------------------------------------------ */

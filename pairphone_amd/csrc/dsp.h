@@ -820,6 +820,55 @@ MD void iir3_d(const int16_t *in, int16_t *out, const int16_t *den, const int16_
 	}
 }
 
+MD void biqd_load(Biqd &b, const int16_t *den, const int16_t *num, const int16_t *din,
+		  const int16_t *dhi, const int16_t *dlo)
+{
+	b.n0 = num[0];
+	b.n1 = num[1];
+	b.n2 = num[2];
+	b.d1 = den[1];
+	b.d2 = den[2];
+	b.i0 = din[0];
+	b.i1 = din[1];
+	b.h0 = dhi[0];
+	b.h1 = dhi[1];
+	b.l0 = dlo[0];
+	b.l1 = dlo[1];
+}
+
+MD void biqd_store(const Biqd &b, int16_t *din, int16_t *dhi, int16_t *dlo)
+{
+	din[0] = b.i0;
+	din[1] = b.i1;
+	dhi[0] = b.h0;
+	dhi[1] = b.h1;
+	dlo[0] = b.l0;
+	dlo[1] = b.l1;
+}
+
+/* two different iir_2nd_d filters in cascade, in place, sample by sample
+ * (postfilter's lpf3500 then hpf60: equal to the two sequential passes) */
+MD void iir2_d(int16_t *x, const int16_t *den1, const int16_t *num1, int16_t *din1,
+	       int16_t *dhi1, int16_t *dlo1, const int16_t *den2, const int16_t *num2,
+	       int16_t *din2, int16_t *dhi2, int16_t *dlo2, int n)
+{
+	Biqd a, b;
+	biqd_load(a, den1, num1, din1, dhi1, dlo1);
+	biqd_load(b, den2, num2, din2, dhi2, dlo2);
+	int i = 0;
+	for (; i + 4 <= n; i += 4) {
+		int16_t v0 = x[i], v1 = x[i + 1], v2 = x[i + 2], v3 = x[i + 3];
+		x[i] = biqd_step(b, biqd_step(a, v0));
+		x[i + 1] = biqd_step(b, biqd_step(a, v1));
+		x[i + 2] = biqd_step(b, biqd_step(a, v2));
+		x[i + 3] = biqd_step(b, biqd_step(a, v3));
+	}
+	for (; i < n; i++)
+		x[i] = biqd_step(b, biqd_step(a, x[i]));
+	biqd_store(a, din1, dhi1, dlo1);
+	biqd_store(b, din2, dhi2, dlo2);
+}
+
 /* ------------------------------------------------------------------ */
 /* LPC: melpe/lpc_lib.c                                               */
 /* ------------------------------------------------------------------ */
