@@ -687,16 +687,24 @@ MN Word16 low_rate_chn_read(DecState *D)
 /* harmonic excitation, melpe/harm.c                                   */
 /* ------------------------------------------------------------------ */
 
+#ifndef IDFT_BLK
+#define IDFT_BLK 12
+#endif
+
 /* realIDFT's cosine table entry i for period len (melpe/harm.c:70-80) */
-MD Word16 idft_cos_entry(Word16 len, int i)
+MD Word16 idft_cos_entry_w(Word16 w, int i)
 {
-	Word16 w = divide_s(16, len);	/* TWO_Q3 */
 	Word32 L = L_mult(w, (Word16) i);
 	if (L > 524288L)
 		L = L_sub(1048576L, L);
 	else if (L == 524288L)
 		L = L_sub(L, 1);
 	return cos_fxp(extract_l(L_shr(L, 4)));
+}
+
+MD Word16 idft_cos_entry(Word16 len, int i)
+{
+	return idft_cos_entry_w(divide_s(16, len), i);	/* w = TWO_Q3 / len */
 }
 
 MD void derive_idft_cos(DerivedTables *d)
@@ -721,7 +729,7 @@ MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 	 * per call, index stepped with add/sub wraps), same values */
 	int16_t cbuf[PITCHMAX];
 	for (int i = 0; i < len; i++)
-		cbuf[i] = idft_cos_entry(len, i);
+		cbuf[i] = idft_cos_entry_w(w, i);
 	const int16_t *c = cbuf;
 #else
 	const int16_t *c = g_der.idft_cos[len];
@@ -757,6 +765,41 @@ MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 			k = add(k, (Word16) i);
 		}
 #else
+		if (i + IDFT_BLK <= len) {
+			/* IDFT_BLK output samples at once: independent L_mac
+			 * chains (each in the reference's j order) sharing the
+			 * mag[] / phm[] loads, table gathers issued together */
+			Word32 Lq[IDFT_BLK];
+			int bq[IDFT_BLK];	/* (j * (i + q)) mod len */
+#pragma unroll
+			for (int q = 0; q < IDFT_BLK; q++) {
+				Lq[q] = L;
+				bq[q] = 0;
+			}
+			for (int j = 1; j < len2; j++) {
+				Word16 m = mag[j];
+				int p = phm[j];
+				int16_t cv[IDFT_BLK];
+#pragma unroll
+				for (int q = 0; q < IDFT_BLK; q++) {
+					bq[q] += i + q;
+					if (bq[q] >= len)
+						bq[q] -= len;
+					int k = bq[q] + p;
+					if (k >= len)
+						k -= len;
+					cv[q] = c[k];
+				}
+#pragma unroll
+				for (int q = 0; q < IDFT_BLK; q++)
+					Lq[q] = L_mac(Lq[q], m, cv[q]);
+			}
+#pragma unroll
+			for (int q = 0; q < IDFT_BLK; q++)
+				sig[i + q] = r_ound(Lq[q]);
+			i += IDFT_BLK - 1;
+			continue;
+		}
 		int base = 0;	/* (j * i) mod len */
 		for (int j = 1; j < len2; j++) {
 			base += i;
