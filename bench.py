@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--channels", type=int, default=262144, help="channels per GPU")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-channels", type=int, default=32)
+    ap.add_argument("--cpu-sample-channels", type=int, default=128)
     ap.add_argument("--cpu-jobs", type=int, default=0, help="0 = min(16, usable cores)")
     return ap.parse_args()
 
