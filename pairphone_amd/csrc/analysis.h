@@ -710,26 +710,54 @@ MD void norm40(Word40 *acc, Word16 *sh, Word32 *L)
 	*L = (Word32) *acc;
 }
 
+/* corPeak's peak list, kept in registers while the lags are scanned: up to
+ * NODE local maxima ordered by value descending, ties in insertion order.
+ * Peaks are inserted in the reference's scan order (lag MAXPITCH down to
+ * MINPITCH), so equal values keep the higher lag first, which is the pick
+ * melpe/pitch.c:351-359 makes (strict '>' scanning down from MAXPITCH).
+ * Zero (non-peak) values never enter: empty slots hold 0. */
+MD void peak_insert(int16_t *tv, int16_t *tj, int16_t v, int16_t j)
+{
+	#pragma unroll
+	for (int k = NODE - 1; k >= 0; k--) {
+		bool keep = tv[k] >= v;
+		bool prev = k > 0 && tv[k > 0 ? k - 1 : 0] >= v;
+		int16_t pv = k > 0 ? tv[k - 1] : v, pj = k > 0 ? tj[k - 1] : j;
+		tv[k] = keep ? tv[k] : (prev ? v : pv);
+		tj[k] = keep ? tj[k] : (prev ? j : pj);
+	}
+}
+
 /* corPeak :216 */
 MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 {
 	PROF_SCOPE(32);
 	int16_t pb[PIT_COR_LEN];
-	int16_t index[MAXPITCH + 1], gp[MAXPITCH + 1], peak[MAXPITCH + 1], corx[NODE];
 	const int PW = PIT_COR_LEN - MAXPITCH;	/* 73 */
 	remove_dc(in, pb, PIT_COR_LEN);
 	Word40 r0 = 0, rk = 0, A = 0;
 	Word16 r0s, rks;
 	Word32 Lr0, Lrk;
-	for (int i = 0; i < PW; i++)
-		r0 = L40_mac(r0, pb[i], pb[i]);
+	for (int i = 0; i < PW; i++) {	/* three opening sums, one pass */
+		int16_t u = pb[i], v = pb[i + MAXPITCH];
+		r0 = L40_mac(r0, u, u);
+		rk = L40_mac(rk, v, v);
+		A = L40_mac(A, u, v);
+	}
 	norm40(&r0, &r0s, &Lr0);
-	for (int i = MAXPITCH; i < PIT_COR_LEN; i++)
-		rk = L40_mac(rk, pb[i], pb[i]);
 	norm40(&rk, &rks, &Lrk);
-	for (int i = 0; i < PW; i++)
-		A = L40_mac(A, pb[i], pb[i + MAXPITCH]);
-	gp[MAXPITCH] = cor_gain(&Lr0, &r0s, rks, Lrk, A, true);
+	/* the reference keeps gp[20..147] and picks peaks afterwards
+	 * (:298-359); here the gains of the last two lags stay in registers
+	 * (g1 = gp[i+1], g2 = gp[i+2]) and each lag's peak value joins the
+	 * register peak list as soon as its lower neighbour is known.  The
+	 * sentinel -32768 stands for the missing neighbour at both ends
+	 * (gains are >= 0), which reproduces the end-point rules. */
+	int16_t tv[NODE], tj[NODE];
+	for (int k = 0; k < NODE; k++) {
+		tv[k] = 0;
+		tj[k] = 0;
+	}
+	int16_t g1 = cor_gain(&Lr0, &r0s, rks, Lrk, A, true), g2 = -32768;
 	int lo = 0, hi = MAXPITCH;
 	/* The cross terms A of the lag loop are 73-term sums of 2*x*y with
 	 * |x*y| <= 2^30, so |A| < 2^37 and the 40-bit clamp of L40_mac never
@@ -791,37 +819,52 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 			for (int j = lo; j < lo + PW; j++)
 				A = L40_mac(A, pb[j], pb[j + i]);
 		}
-		gp[i] = cor_gain(&Lr0, &r0s, rks, Lrk, A, true);
+		int16_t g = cor_gain(&Lr0, &r0s, rks, Lrk, A, true);
+		/* lag i+1 is a peak when above both neighbours */
+		peak_insert(tv, tj, (g1 > g2 && g1 > g) ? g1 : (int16_t) 0, (int16_t) (i + 1));
+		g2 = g1;
+		g1 = g;
 	}
+	peak_insert(tv, tj, (g1 > g2) ? g1 : (int16_t) 0, (int16_t) MINPITCH);
 	}
 	PROF_SCOPE(40);
-	peak[MINPITCH] = (gp[MINPITCH + 1] < gp[MINPITCH]) ? gp[MINPITCH] : (int16_t) 0;
-	peak[MAXPITCH] = (gp[MAXPITCH] > gp[MAXPITCH - 1]) ? gp[MAXPITCH] : (int16_t) 0;
-	for (int i = MINPITCH + 1; i < MAXPITCH; i++)
-		peak[i] = (gp[i] > gp[i - 1] && gp[i] > gp[i + 1]) ? gp[i] : (int16_t) 0;
-	v_zero(index, MAXPITCH + 1);
-	for (int i = 0; i < NODE; i++) {
-		int best = MAXPITCH;
-		for (int j = MAXPITCH - 1; j >= MINPITCH; j--)
-			if (peak[j] > peak[best])
-				best = j;
-		index[best] = (int16_t) (i + 1);
-		corx[i] = peak[best];
-		peak[best] = 0;
-		if (i == 0)
-			cs->pitch = (int16_t) best;
-	}
-	cs->corx = corx[0];
-	int n = 0;
-	for (int i = MINPITCH; i <= MAXPITCH; i++)
-		if (index[i] != 0) {
-			pt->pit[n] = (int16_t) i;
-			pt->weight[n] = corx[index[i] - 1];
-			n++;
+	/* The reference's NODE picks (:351-359): pick k is list entry k while
+	 * the list has positive entries, then lag MAXPITCH with value 0 (no
+	 * entry beats peak[MAXPITCH] once all are zero), and index[MAXPITCH]
+	 * ends up pointing at the last such pick.  pit/weight list the picked
+	 * lags in ascending order (:361-372), padded with (100, 0). */
+	cs->pitch = (tv[0] > 0) ? tj[0] : (int16_t) MAXPITCH;
+	cs->corx = tv[0];
+	bool full = tv[NODE - 1] > 0, has_max = false;
+	for (int k = 0; k < NODE; k++)
+		has_max |= tv[k] > 0 && tj[k] == MAXPITCH;
+	int16_t ej[NODE], ew[NODE];
+	for (int k = 0; k < NODE; k++) {
+		if (tv[k] > 0) {
+			ej[k] = tj[k];
+			ew[k] = (tj[k] == MAXPITCH && !full) ? (int16_t) 0 : tv[k];
+		} else if (!has_max && (k == 0 || tv[k > 0 ? k - 1 : 0] > 0)) {
+			ej[k] = MAXPITCH;	/* the first zero pick */
+			ew[k] = 0;
+		} else {
+			ej[k] = 1000;	/* unused: sorts last, becomes (100, 0) */
+			ew[k] = 0;
 		}
-	for (; n < NODE; n++) {
-		pt->pit[n] = 100;
-		pt->weight[n] = 0;
+	}
+	#pragma unroll
+	for (int r = 0; r < NODE; r++)	/* odd-even transposition sort on lag */
+		#pragma unroll
+		for (int k = r & 1; k + 1 < NODE; k += 2) {
+			bool sw = ej[k] > ej[k + 1];
+			int16_t a = ej[k], b = ej[k + 1], wa = ew[k], wb = ew[k + 1];
+			ej[k] = sw ? b : a;
+			ej[k + 1] = sw ? a : b;
+			ew[k] = sw ? wb : wa;
+			ew[k + 1] = sw ? wa : wb;
+		}
+	for (int k = 0; k < NODE; k++) {
+		pt->pit[k] = (ej[k] == 1000) ? (int16_t) 100 : ej[k];
+		pt->weight[k] = ew[k];
 	}
 	for (int i = 0; i < NODE - 1; i++)
 		for (int j = i + 1; j < NODE; j++) {
@@ -959,6 +1002,48 @@ MN Word16 bandEn(const int16_t *ac, int band)
 	return log10_fxp(extract_l(L_shr(e, 4)), 10);
 }
 
+/* The ten cross sums of frac_cor's full +-5 lag scan in one pass.  Lag
+ * n = 0..9 is hp-1-n; its window starts at lo_n (the count of even lags in
+ * [hp-1-n, hp-1], :540-560), so it reads in[lo_n + t] * in[lo_n + hp-1-n + t]
+ * for t < win.  Relative to the first a-start and the last b-start those
+ * offsets are compile-time constants once the parity of hp is fixed
+ * (ODD: hp odd), both within 0..5, so one pass keeps six a- and six
+ * b-samples in registers and loads two samples per t instead of twenty.
+ * The sums are 2*x*y over at most 200 terms, |sum| < 2^39: the 40-bit
+ * clamp of L40_mac never acts, so int64 sums are the reference's values. */
+template <int ODD>
+MD void fc_corr10(const int16_t *in, int hp, int win, Word40 *A)
+{
+	constexpr int lo0 = ODD ? 1 : 0, lo9 = 5;
+	const int16_t *pa = &in[lo0], *pb = &in[lo9 + hp - 10];
+	int64_t acc[10];
+	int av[6], bv[6];
+	for (int k = 0; k < 10; k++)
+		acc[k] = 0;
+	for (int k = 0; k < 5; k++) {
+		av[k] = pa[k];
+		bv[k] = pb[k];
+	}
+	#pragma unroll 2
+	for (int t = 0; t < win; t++) {
+		av[5] = pa[t + 5];
+		bv[5] = pb[t + 5];
+		#pragma unroll
+		for (int n = 0; n < 10; n++) {
+			int lon = ODD ? n / 2 + 1 : (n + 1) / 2;
+			int ao = lon - lo0, bo = (lon - n) - (lo9 - 9);
+			acc[n] += (int64_t) (av[ao] * bv[bo]);
+		}
+		#pragma unroll
+		for (int k = 0; k < 5; k++) {
+			av[k] = av[k + 1];
+			bv[k] = bv[k + 1];
+		}
+	}
+	for (int n = 0; n < 10; n++)
+		A[n] = 2 * acc[n];
+}
+
 /* frac_cor :504 -- best normalised correlation within +-5 of pitch */
 MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 {
@@ -970,17 +1055,27 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 	Word40 r0 = 0, rk = 0, A = 0;
 	Word16 r0s, rks;
 	Word32 Lr0, Lrk;
-	for (int i = 0; i < PIT_COR_LEN - hp; i++)
-		r0 = L40_mac(r0, in[i], in[i]);
+	Word16 win = sub(PIT_COR_LEN, hp);
+	/* the reference's three opening sums (:520-530) in one pass: each keeps
+	 * its own chain in index order */
+	for (int i = 0; i < win; i++) {
+		int16_t u = in[i], v = in[i + hp];
+		r0 = L40_mac(r0, u, u);
+		rk = L40_mac(rk, v, v);
+		A = L40_mac(A, u, v);
+	}
 	norm40(&r0, &r0s, &Lr0);
-	for (int i = hp; i < PIT_COR_LEN; i++)
-		rk = L40_mac(rk, in[i], in[i]);
 	norm40(&rk, &rks, &Lrk);
-	for (int i = 0; i < PIT_COR_LEN - hp; i++)
-		A = L40_mac(A, in[i], in[i + hp]);
 	Word16 maxgp = cor_gain(&Lr0, &r0s, rks, Lrk, A, true);
 	int lo = 0, hi = hp;
-	Word16 win = sub(PIT_COR_LEN, hp);
+	const bool blocked = (hp - lp) == 10;
+	Word40 blk[10];
+	if (blocked) {
+		if (hp & 1)
+			fc_corr10<1>(in, hp, win, blk);
+		else
+			fc_corr10<0>(in, hp, win, blk);
+	}
 	for (Word16 i = sub(hp, 1); i >= lp; i--) {
 		if (i % 2 == 0) {
 			r0 = L40_shr((Word40) Lr0, r0s);
@@ -995,9 +1090,14 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 			rk = L40_msu(rk, in[hi + win], in[hi + win]);
 			norm40(&rk, &rks, &Lrk);
 		}
-		A = 0;
-		for (int j = lo; j < lo + win; j++)
-			A = L40_mac(A, in[j], in[j + i]);
+		if (blocked) {
+			A = blk[hp - 1 - i];
+			OPC_ADD(OP_L40_mac, win);	/* census: the reference's per-lag sum */
+		} else {
+			A = 0;
+			for (int j = lo; j < lo + win; j++)
+				A = L40_mac(A, in[j], in[j + i]);
+		}
 		Word16 g = cor_gain(&Lr0, &r0s, rks, Lrk, A, false);
 		if (g > maxgp)
 			maxgp = g;
@@ -1010,54 +1110,64 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *ac)
 {
 	PROF_SCOPE(6);
-	int16_t sa[BPF_ORD / 3 + PIT_COR_LEN], sbb[BPF_ORD / 3 + PIT_COR_LEN];
+	/* so[2..222): the band-passed signal frac_cor reads; so[2..132) is
+	 * the previous call's tail (back_sigbuf) except on the first call */
+	int16_t so[BPF_ORD / 3 + PIT_COR_LEN];
 	int16_t insp[PIT_SUBFRAME];
-	int16_t *si, *so;
-	int slen;
 	const bool first = !E->cls_started;
 	const int KEEP = PIT_COR_LEN - PIT_SUBFRAME;	/* 130 */
+	const int16_t *x;
+	int16_t *y;
+	int slen;
 	if (first) {
 		E->voicedEn = 10240;
 		E->silenceEn = 6144;
 		E->voicedCnt = 0;
 		v_zero(E->bpfdel, BPF_ORD + BPF_ORD / 3);
-		si = sa;
-		so = sbb;
 		slen = PIT_COR_LEN;
-		v_copy(&si[2], &in[(PIT_SUBFRAME - PIT_COR_LEN) / 2], slen);
-	} else {
-		si = sa + KEEP;
-		so = sbb + KEEP;
-		slen = PIT_SUBFRAME;
-		v_copy(&si[2], &in[(PIT_COR_LEN - PIT_SUBFRAME) / 2], slen);
-		v_copy(&so[2 - KEEP], E->back_sigbuf, KEEP);
-	}
-	const int16_t *pn = TB(bpf_num), *pd = TB(bpf_den) + 1;
-	for (int s = 0; s < BPF_ORD / 2; s++) {
-		v_copy(si, &E->bpfdel[2 * s], 2);
-		v_copy(so, &E->bpfdel[2 * s + 2], 2);
-		for (int j = 2; j < slen + 2; j++) {
-			Word32 t = L_mult(si[j], pn[0]);
-			t = L_mac(t, si[j - 1], pn[1]);
-			t = L_mac(t, si[j - 2], pn[2]);
-			t = L_mac(t, so[j - 1], pd[0]);
-			t = L_mac(t, so[j - 2], pd[1]);
-			so[j] = r_ound(L_shl(t, 2));
-		}
-		v_copy(&E->bpfdel[2 * s], &si[slen], 2);
-		int16_t *tp = si;
-		si = so;
-		so = tp;
-		pn += 3;
-		pd += 3;
-	}
-	if (first) {
+		x = &in[(PIT_SUBFRAME - PIT_COR_LEN) / 2];
+		y = &so[2];
 		E->cls_started = 1;
-		so = si;
 	} else {
-		so = si - KEEP;
+		slen = PIT_SUBFRAME;
+		x = &in[(PIT_COR_LEN - PIT_SUBFRAME) / 2];
+		y = &so[2 + KEEP];
+		v_copy(&so[2], E->back_sigbuf, KEEP);
 	}
-	v_copy(&E->bpfdel[BPF_ORD], &so[PIT_COR_LEN], 2);
+	/* The reference runs the three sections one after the other through
+	 * ping-pong buffers (:126-168), section s reading its two past inputs
+	 * from bpfdel[2s..2s+1] and past outputs from bpfdel[2s+2..2s+3] (the
+	 * next section's past inputs).  Section s at sample j depends only on
+	 * section s-1 at samples <= j, so the cascade runs sample by sample
+	 * with the four two-sample histories in registers; what is left in
+	 * bpfdel afterwards is the same last-two-samples of each stage. */
+	{
+		const int16_t *pn = TB(bpf_num), *pd = TB(bpf_den);
+		Biq bq[3];
+		for (int k = 0; k < 3; k++) {
+			bq[k].n0 = pn[3 * k];
+			bq[k].n1 = pn[3 * k + 1];
+			bq[k].n2 = pn[3 * k + 2];
+			bq[k].d1 = pd[3 * k + 1];
+			bq[k].d2 = pd[3 * k + 2];
+			bq[k].i0 = E->bpfdel[2 * k + 1];
+			bq[k].i1 = E->bpfdel[2 * k];
+			bq[k].o0 = E->bpfdel[2 * k + 3];
+			bq[k].o1 = E->bpfdel[2 * k + 2];
+		}
+		int j = 0;
+		for (; j + 2 <= slen; j += 2) {
+			int16_t v0 = x[j], v1 = x[j + 1];
+			y[j] = biq_step(bq[2], biq_step(bq[1], biq_step(bq[0], v0)));
+			y[j + 1] = biq_step(bq[2], biq_step(bq[1], biq_step(bq[0], v1)));
+		}
+		for (int k = 0; k < 3; k++) {
+			E->bpfdel[2 * k] = bq[k].i1;
+			E->bpfdel[2 * k + 1] = bq[k].i0;
+		}
+		E->bpfdel[BPF_ORD] = bq[2].o1;
+		E->bpfdel[BPF_ORD + 1] = bq[2].o0;
+	}
 	v_copy(E->back_sigbuf, &so[2 + PIT_SUBFRAME], KEEP);
 
 	Word16 mx = 0, t1, t2, sh1 = 0;

@@ -1063,34 +1063,47 @@ MN void lsp_to_freq(const int16_t *lsp, int16_t *freq, int order)
 	smag[2] = 0;
 	Word16 p2 = shr((Word16) order, 1);
 	Word16 count = 0;
-	for (int i = 0; i <= 256; i++) {
-		Word16 pc = (Word16) i;
-		Word32 acc = L_mult(lsp[p2], 8192);
-		for (int j = p2 - 1; j >= 0; j--) {
-			acc = L_add(acc, L_shr(L_mult(lsp[j], lc[pc]), 1));
-			pc = add(pc, (Word16) i);
-			if (pc > 511)
-				pc -= 512;
+	/* The reference steps the grid index by pc = add(pc, i), wrapping at
+	 * 512 (:668-672): term k of point i reads lsp_cos[k*i mod 512], never
+	 * saturating (k*i <= 1280).  Those indices are wave-uniform and
+	 * independent of the data, so the polynomial values of 8 grid points
+	 * are formed first (their 40 table loads issued together), then the
+	 * sign-change scan walks them in order. */
+	for (int i0 = 0; i0 <= 256; i0 += 8) {
+		Word32 accs[8];
+		#pragma unroll
+		for (int u = 0; u < 8; u++) {
+			int i = i0 + u;
+			Word32 acc = L_mult(lsp[p2], 8192);
+			for (int j = p2 - 1; j >= 0; j--)
+				acc = L_add(acc, L_shr(L_mult(lsp[j], lc[((p2 - j) * i) & 511]), 1));
+			accs[u] = acc;
 		}
-		smag[2] = extract_h(acc);
-		mag[2] = L_abs(acc);
-		if (mag[2] < mag[1]) {
-			prev_less = true;
-		} else {
-			if (prev_less && (smag[0] ^ smag[2]) < 0) {
-				Word32 n1 = L_shr(L_sub(mag[0], mag[2]), 1);
-				Word32 d1 = L_add(L_sub(mag[0], L_shl(mag[1], 1)), mag[2]);
-				Word16 t = shr(L_divider2(n1, d1, 0, 0), 9);
-				t = add(shl(sub((Word16) i, 1), 6), t);
-				freq[count] = divide_s(t, shl(512, 5));
-				count = add(count, 1);
+		int nu = (256 - i0 + 1) < 8 ? (256 - i0 + 1) : 8;
+		for (int u = 0; u < nu; u++) {
+			int i = i0 + u;
+			OPC_ADD(OP_add, p2);	/* census: the reference's index steps */
+			Word32 acc = accs[u];
+			smag[2] = extract_h(acc);
+			mag[2] = L_abs(acc);
+			if (mag[2] < mag[1]) {
+				prev_less = true;
+			} else {
+				if (prev_less && (smag[0] ^ smag[2]) < 0) {
+					Word32 n1 = L_shr(L_sub(mag[0], mag[2]), 1);
+					Word32 d1 = L_add(L_sub(mag[0], L_shl(mag[1], 1)), mag[2]);
+					Word16 t = shr(L_divider2(n1, d1, 0, 0), 9);
+					t = add(shl(sub((Word16) i, 1), 6), t);
+					freq[count] = divide_s(t, shl(512, 5));
+					count = add(count, 1);
+				}
+				prev_less = false;
 			}
-			prev_less = false;
+			mag[0] = mag[1];
+			mag[1] = mag[2];
+			smag[0] = smag[1];
+			smag[1] = smag[2];
 		}
-		mag[0] = mag[1];
-		mag[1] = mag[2];
-		smag[0] = smag[1];
-		smag[1] = smag[2];
 	}
 	if (count != p2) {
 		freq[0] = dw0;
