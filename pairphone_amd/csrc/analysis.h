@@ -144,34 +144,39 @@ MD void q_bpvc_dec(int16_t *bpvc, Word16 idx, int16_t uv, int nb)
 MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 {
 	Word16 sc = 0;
-	Word32 sum = 0, margin = LW_MAX_;
-	bool ovf = false;
-	int i = 0;
-	for (; i + 4 <= len && !ovf; i += 4) {	/* samples in blocks of 4 */
-		int16_t v[4] = {in[i], in[i + 1], in[i + 2], in[i + 3]};
-		for (int k = 0; k < 4; k++) {
-			Word32 t = L_mult(v[k], v[k]);
-			if (!ovf && t <= margin) {
+	Word32 corr;
+	bool ovf;
+#if defined(MELPE_OPCOUNT)
+	/* census build: the reference's loop, op for op */
+	{
+		Word32 sum = 0, margin = LW_MAX_;
+		ovf = false;
+		for (int i = 0; i < len && !ovf; i++) {
+			Word32 t = L_mult(in[i], in[i]);
+			if (t <= margin) {
 				sum = L_add(sum, t);
 				margin = L_sub(margin, t);
 			} else {
 				ovf = true;
 			}
 		}
+		corr = sum;
 	}
-	for (; i < len && !ovf; i++) {
-		Word32 t = L_mult(in[i], in[i]);
-		if (t <= margin) {
-			sum = L_add(sum, t);
-			margin = L_sub(margin, t);
-		} else {
-			ovf = true;
-		}
+#else
+	/* Every term L_mult(x, x) is >= 0, so the reference's running margin
+	 * test (:193-203) fails exactly when the running sum first exceeds
+	 * LW_MAX, i.e. iff the whole 64-bit sum does; without it L_add never
+	 * saturates and the sum is exact.  One pass, no data-dependent exit. */
+	{
+		int64_t sum = 0;
+		#pragma unroll 8
+		for (int i = 0; i < len; i++)
+			sum += L_mult(in[i], in[i]);
+		ovf = sum > (int64_t) LW_MAX_;
+		corr = (Word32) sum;
 	}
-	if (ovf)
-		margin = LW_MIN_;
-	Word32 corr = sum;
-	if (margin == LW_MIN_) {
+#endif
+	if (ovf) {
 		int16_t tb[PITCH_FR + 8];
 		sc = 5;
 		v_equ_shr(tb, in, sc, len);

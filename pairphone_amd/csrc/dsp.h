@@ -288,13 +288,18 @@ MD Word16 add_shr(Word16 a, Word16 b)	/* :781 */
 /* envelope :62 -- rectify + 2nd-order smoother; out[-1], out[-2] are history */
 MN void envelope(const int16_t *in, int16_t prev_in, int16_t *out, int n)
 {
-	Word16 pa = abs_s(prev_in);
+	/* the two past outputs ride in registers (out may be in: in[i] is
+	 * always read before out[i] is written, as in the reference) */
+	Word16 pa = abs_s(prev_in), y1 = out[-1], y2 = out[-2];
 	for (int i = 0; i < n; i++) {
 		Word16 ca = abs_s(in[i]);
 		Word32 acc = L_shr(L_deposit_h(sub(ca, pa)), 5);
-		acc = L_mac(acc, 31565, out[i - 1]);
-		acc = L_mac(acc, -15415, out[i - 2]);
-		out[i] = r_ound(L_shl(acc, 1));
+		acc = L_mac(acc, 31565, y1);
+		acc = L_mac(acc, -15415, y2);
+		Word16 y = r_ound(L_shl(acc, 1));
+		out[i] = y;
+		y2 = y1;
+		y1 = y;
 		pa = ca;
 	}
 }

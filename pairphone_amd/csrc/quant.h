@@ -356,7 +356,21 @@ MD void lspVQ_t(const int16_t *target, const int16_t *weight, int16_t *qout, con
 	const int16_t *cbp = cb;
 	Word16 off = 0;
 	for (int s1 = 0; s1 < tos; s1++) {
-		v_set(dMin, SW_MAX_, LSP_VQ_CAND);
+		/* The M-best list of this stage lives in registers: distortions
+		 * dm[] ascending and, per slot, a tag naming what InsertCand
+		 * (:735-788) would have left in nextIndex[slot][0..s1]: (c1, e) for
+		 * an entry inserted at this stage (index[c1][0..s1) followed by
+		 * e), or -1-r for row r as it stood before the stage, shifted down
+		 * by later inserts.  The network below is InsertCand's insert
+		 * (before equal distortions, last slot evicted) on registers; the
+		 * rows are written out once the stage's scan is done. */
+		int16_t dm[LSP_VQ_CAND];
+		int32_t tag[LSP_VQ_CAND];
+#pragma unroll
+		for (int k = 0; k < LSP_VQ_CAND; k++) {
+			dm[k] = SW_MAX_;
+			tag[k] = -1 - k;
+		}
 		Word16 maxd = SW_MAX_;
 		for (int c1 = 0; c1 < ncPrev; c1++) {
 			off = 0;
@@ -366,10 +380,39 @@ MD void lspVQ_t(const int16_t *target, const int16_t *weight, int16_t *qout, con
 				ct[i] = sub(target[i], cand[c1][i]);
 			for (int e = 0; e < cb_size[s1]; e++) {
 				Word16 d = WeightedMSE_t<DIM>(wr, cbp + off, ct, maxd);
-				if (d < maxd)
-					maxd = InsertCand(c1, s1, dMin, d, (int16_t) e, nextIndex, index);
+				if (d < maxd) {
+					int32_t nt = (c1 << 16) | e;
+#pragma unroll
+					for (int k = LSP_VQ_CAND - 1; k >= 0; k--) {
+						bool keep = dm[k] < d;
+						bool prev = k == 0 || dm[k > 0 ? k - 1 : 0] < d;
+						int16_t pd = k > 0 ? dm[k - 1] : d;
+						int32_t pt = k > 0 ? tag[k - 1] : nt;
+						dm[k] = keep ? dm[k] : (prev ? d : pd);
+						tag[k] = keep ? tag[k] : (prev ? nt : pt);
+					}
+					maxd = dm[LSP_VQ_CAND - 1];
+				}
 				off = add(off, (Word16) dim);
 			}
+		}
+		{
+			int16_t rows[LSP_VQ_CAND][LSP_VQ_STAGES];
+			for (int k = 0; k < LSP_VQ_CAND; k++) {
+				if (tag[k] >= 0) {
+					int c1 = tag[k] >> 16;
+					for (int i = 0; i < s1; i++)
+						rows[k][i] = index[c1][i];
+					rows[k][s1] = (int16_t) (tag[k] & 0xffff);
+				} else {
+					for (int i = 0; i <= s1; i++)
+						rows[k][i] = nextIndex[-1 - tag[k]][i];
+				}
+			}
+			for (int k = 0; k < LSP_VQ_CAND; k++)
+				for (int i = 0; i <= s1; i++)
+					nextIndex[k][i] = rows[k][i];
+			v_copy(dMin, dm, LSP_VQ_CAND);
 		}
 		if (!flag && s1 == tos - 1) {
 			ncPrev = 1;
