@@ -28,7 +28,7 @@ __global__ __launch_bounds__(WAVE) void k_npp(EncState *enc, int16_t *sp, int fr
 	wv_state_in(&W, &enc[c].npp, lane);
 	int16_t *x = sp + (size_t) c * stride;
 	for (int f = 0; f < frames; f++)
-		wv_npp_frame(&W, x + f * NPP_HOP, stride - f * NPP_HOP, rate1200 != 0, &kc, lane);
+		wv_npp_frame(&W, &enc[c].npp, x + f * NPP_HOP, stride - f * NPP_HOP, rate1200 != 0, &kc, lane);
 	wv_state_out(&enc[c].npp, &W, lane);
 }
 
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(WAVE) void k_enc_npp(EncState *enc, int16_t *sp, co
 	wv_state_in(&W, &enc[c].npp, lane);
 	int16_t *x = sp + (size_t) c * BLOCK;
 	for (int f = 0; f < NF; f++)
-		wv_npp_frame(&W, x + f * FRAME, BLOCK - f * FRAME, true, &kc, lane);
+		wv_npp_frame(&W, &enc[c].npp, x + f * FRAME, BLOCK - f * FRAME, true, &kc, lane);
 	wv_state_out(&enc[c].npp, &W, lane);
 }
 

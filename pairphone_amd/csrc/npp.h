@@ -9,6 +9,8 @@
 #ifndef MELPE_NPP_H
 #define MELPE_NPP_H
 
+#include <stddef.h>
+
 #include "dsp.h"
 
 namespace mlp {
@@ -37,19 +39,27 @@ struct NppState {
 	int16_t sm_shift[NPP_NB], noise_shift[NPP_NB];
 	int16_t av_shift[NPP_NB], av2_shift[NPP_NB];
 	int16_t act_min[NPP_NB], act_min_shift[NPP_NB];
-	int16_t act_min_sub[NPP_NB], act_min_sub_shift[NPP_NB];
 	int16_t ksi[NPP_NB], ksi_shift[NPP_NB];
 	int16_t smoothedspect[NPP_NB], var_sp_av[NPP_NB], var_sp_2[NPP_NB];
 	int16_t noisespect[NPP_NB];
-	int16_t qla[NPP_NB], localflag[NPP_NB];
-	int16_t circb_min[NPP_NB], circb_min_shift[NPP_NB];
+	int16_t qla[NPP_NB];
 	int16_t agal[NPP_NB], agal_shift[NPP_NB];
 	int16_t qk[NPP_NB], Gain[NPP_NB];
-	int16_t circb[NPP_NMINWIN][NPP_NB], circb_shift[NPP_NMINWIN][NPP_NB];
 	int16_t speech_in[NPP_WIN];
 	int16_t overlap[NPP_OVL];
+	/* ---- min-statistics memory: touched only by min_search and
+	 * minstat_init, once per frame.  Kept last so the wave kernel can hold
+	 * the part above in LDS (NPP_HOT_BYTES) and leave this part in the HBM
+	 * record; every access goes through the `m` view of those functions. */
+	int16_t act_min_sub[NPP_NB], act_min_sub_shift[NPP_NB];
+	int16_t localflag[NPP_NB];
+	int16_t circb_min[NPP_NB], circb_min_shift[NPP_NB];
+	int16_t circb[NPP_NMINWIN][NPP_NB], circb_shift[NPP_NMINWIN][NPP_NB];
 	int16_t pad_;	/* size multiple of 4: kernels copy state by dwords */
 };
+#define NPP_HOT_BYTES offsetof(NppState, act_min_sub)
+static_assert(NPP_HOT_BYTES % 4 == 0, "NppState hot part copied by dwords");
+static_assert(sizeof(NppState) % 4 == 0, "NppState copied by dwords");
 
 /* per-frame scratch that the reference keeps in file statics but rewrites
  * before every read (YY, vk, noisespect2, var_rel, alpha_var, ybuf, temp_yy) */
@@ -584,61 +594,61 @@ MD Word16 npp_noise_slope(const NppState *s)
 /* min_search :889 -- minimum tracking over 8 windows of 9 frames.  Every
  * loop of the reference touches bin i only, so the per-bin part runs each
  * bin through the whole branch; the counters advance afterwards. */
-MD void npp_min_search_bin(NppState *s, const int16_t *bsp, const int16_t *bsh,
+MD void npp_min_search_bin(NppState *s, NppState *m, const int16_t *bsp, const int16_t *bsh,
 			   const int16_t *bsub, const int16_t *bsubsh, Word16 slope, int i)
 {
 	if (s->minspec_counter == 0) {
 		if (cmp_shift(bsp[i], bsh[i], s->act_min[i], s->act_min_shift[i]) < 0) {
 			s->act_min[i] = bsp[i];
 			s->act_min_shift[i] = bsh[i];
-			s->act_min_sub[i] = bsub[i];
-			s->act_min_sub_shift[i] = bsubsh[i];
-			s->localflag[i] = 0;
+			m->act_min_sub[i] = bsub[i];
+			m->act_min_sub_shift[i] = bsubsh[i];
+			m->localflag[i] = 0;
 		}
-		s->circb[s->circb_index][i] = s->act_min[i];
-		s->circb_shift[s->circb_index][i] = s->act_min_shift[i];
-		Word16 t1 = s->circb[0][i], t2 = s->circb_shift[0][i];
+		m->circb[s->circb_index][i] = s->act_min[i];
+		m->circb_shift[s->circb_index][i] = s->act_min_shift[i];
+		Word16 t1 = m->circb[0][i], t2 = m->circb_shift[0][i];
 		for (int k = 1; k < NPP_NMINWIN; k++)
-			if (cmp_shift(s->circb[k][i], s->circb_shift[k][i], t1, t2) < 0) {
-				t1 = s->circb[k][i];
-				t2 = s->circb_shift[k][i];
+			if (cmp_shift(m->circb[k][i], m->circb_shift[k][i], t1, t2) < 0) {
+				t1 = m->circb[k][i];
+				t2 = m->circb_shift[k][i];
 			}
-		s->circb_min[i] = t1;
-		s->circb_min_shift[i] = t2;
-		Word16 t = mult(slope, s->circb_min[i]);
-		Word16 ts = add(s->circb_min_shift[i], 4);
-		if (s->localflag[i] &&
-		    cmp_shift(s->act_min_sub[i], s->act_min_sub_shift[i],
-			      s->circb_min[i], s->circb_min_shift[i]) > 0 &&
-		    cmp_shift(s->act_min_sub[i], s->act_min_sub_shift[i], t, ts) < 0) {
-			s->circb_min[i] = s->act_min_sub[i];
-			s->circb_min_shift[i] = s->act_min_sub_shift[i];
+		m->circb_min[i] = t1;
+		m->circb_min_shift[i] = t2;
+		Word16 t = mult(slope, m->circb_min[i]);
+		Word16 ts = add(m->circb_min_shift[i], 4);
+		if (m->localflag[i] &&
+		    cmp_shift(m->act_min_sub[i], m->act_min_sub_shift[i],
+			      m->circb_min[i], m->circb_min_shift[i]) > 0 &&
+		    cmp_shift(m->act_min_sub[i], m->act_min_sub_shift[i], t, ts) < 0) {
+			m->circb_min[i] = m->act_min_sub[i];
+			m->circb_min_shift[i] = m->act_min_sub_shift[i];
 			for (int k = 0; k < NPP_NMINWIN; k++) {
-				s->circb[k][i] = s->circb_min[i];
-				s->circb_shift[k][i] = s->circb_min_shift[i];
+				m->circb[k][i] = m->circb_min[i];
+				m->circb_shift[k][i] = m->circb_min_shift[i];
 			}
 		}
-		s->localflag[i] = 0;
+		m->localflag[i] = 0;
 	} else if (s->minspec_counter == 1) {
 		s->act_min[i] = bsp[i];
 		s->act_min_shift[i] = bsh[i];
-		s->act_min_sub[i] = bsub[i];
-		s->act_min_sub_shift[i] = bsubsh[i];
+		m->act_min_sub[i] = bsub[i];
+		m->act_min_sub_shift[i] = bsubsh[i];
 	} else {
 		if (cmp_shift(bsp[i], bsh[i], s->act_min[i], s->act_min_shift[i]) < 0) {
 			s->act_min[i] = bsp[i];
 			s->act_min_shift[i] = bsh[i];
-			s->act_min_sub[i] = bsub[i];
-			s->act_min_sub_shift[i] = bsubsh[i];
-			s->localflag[i] = 1;
+			m->act_min_sub[i] = bsub[i];
+			m->act_min_sub_shift[i] = bsubsh[i];
+			m->localflag[i] = 1;
 		}
-		if (cmp_shift(s->act_min_sub[i], s->act_min_sub_shift[i],
-			      s->circb_min[i], s->circb_min_shift[i]) < 0) {
-			s->circb_min[i] = s->act_min_sub[i];
-			s->circb_min_shift[i] = s->act_min_sub_shift[i];
+		if (cmp_shift(m->act_min_sub[i], m->act_min_sub_shift[i],
+			      m->circb_min[i], m->circb_min_shift[i]) < 0) {
+			m->circb_min[i] = m->act_min_sub[i];
+			m->circb_min_shift[i] = m->act_min_sub_shift[i];
 		}
-		s->noisespect[i] = s->circb_min[i];
-		s->noise_shift[i] = s->circb_min_shift[i];
+		s->noisespect[i] = m->circb_min[i];
+		s->noise_shift[i] = m->circb_min_shift[i];
 		Word32 L = L_mult(NOISE_BIAS, s->noisespect[i]);
 		if (L < 0x40000000L) {
 			L = L_shl(L, 1);
@@ -667,7 +677,7 @@ MN void npp_min_search(NppState *s, const int16_t *bsp, const int16_t *bsh,
 {
 	Word16 slope = npp_noise_slope(s);
 	for (int i = 0; i < NPP_NB; i++)
-		npp_min_search_bin(s, bsp, bsh, bsub, bsubsh, slope, i);
+		npp_min_search_bin(s, s, bsp, bsh, bsub, bsubsh, slope, i);
 	npp_min_search_post(s);
 }
 

@@ -86,7 +86,9 @@ __device__ __forceinline__ int bin_at(int r0, int r1, int r2, int i)
 /* LDS image of one channel's NPP */
 struct NppWave {
 	NppScratch w;	/* YY.., ybuf, temp_yy (int32 first: alignment) */
-	NppState s;
+	/* the channel's NppState up to its min-statistics memory (NPP_HOT_BYTES);
+	 * that memory stays in the HBM record (the `m` view below) */
+	uint32_t s_hot[NPP_HOT_BYTES / 4];
 	int16_t Ymag[NPP_NB], Ymag_shift[NPP_NB], GainD[NPP_NB];
 	int16_t gk[NPP_NB], gks[NPP_NB];
 	int16_t bsp[NPP_NB], bsub[NPP_NB], bsh[NPP_NB], bsubsh[NPP_NB];
@@ -97,6 +99,13 @@ struct NppWave {
 /* per-lane constants of the FFT and the analysis window, loaded once per
  * kernel: the twiddles of the lane's two butterflies in each of the six
  * twiddled stages (packed wr | wi << 16), and win[lane + 64 t] */
+/* the LDS image as an NppState: only fields before NPP_HOT_BYTES are
+ * touched through it */
+MD NppState *wv_S(NppWave *W)
+{
+	return (NppState *) W->s_hot;
+}
+
 struct WvConst {
 	int tw[6][2];
 	int16_t win[4];
@@ -274,21 +283,21 @@ MD void wv_mirror(int16_t *yb, int lane)
 }
 
 /* minstat_init :1164 */
-MD void wv_minstat_init(NppState *s, int lane)
+MD void wv_minstat_init(NppState *s, NppState *m, int lane)
 {
 	LANE_LOOP(i, NPP_NB) {
 		Word16 sp = mult(s->lambdaD[i], NOISE_BIAS);
 		Word16 ls = s->lambdaD_shift[i];
 		s->smoothedspect[i] = sp;
 		for (int k = 0; k < NPP_NMINWIN; k++) {
-			s->circb[k][i] = sp;
-			s->circb_shift[k][i] = ls;
+			m->circb[k][i] = sp;
+			m->circb_shift[k][i] = ls;
 		}
 		s->sm_shift[i] = ls;
 		s->act_min[i] = sp;
 		s->act_min_shift[i] = ls;
-		s->act_min_sub[i] = sp;
-		s->act_min_sub_shift[i] = ls;
+		m->act_min_sub[i] = sp;
+		m->act_min_sub_shift[i] = ls;
 		s->noisespect[i] = sp;
 		s->noise_shift[i] = ls;
 		s->var_sp_av[i] = mult(sp, 20066);
@@ -302,9 +311,9 @@ MD void wv_minstat_init(NppState *s, int lane)
 }
 
 /* enh_init :1023 -- initial noise estimate; `noise` (256, LDS) is consumed */
-MD void wv_enh_init(NppWave *W, int16_t *noise, const WvConst *kc, int lane)
+MD void wv_enh_init(NppWave *W, int16_t *noise, const WvConst *kc, int lane, NppState *m)
 {
-	NppState *s = &W->s;
+	NppState *s = wv_S(W);
 	int16_t *yb = W->w.ybuf;
 	int32_t *ty = W->w.temp_yy;
 	int mx = 0;
@@ -394,17 +403,17 @@ MD void wv_enh_init(NppWave *W, int16_t *noise, const WvConst *kc, int lane)
 	s->n_pwr_shift = sub(add(nsh, 1), sh);
 	s->SN_LT = divide_s(14648, s->n_pwr);
 	s->SN_LT_shift = sub(22, s->n_pwr_shift);
-	wv_minstat_init(s, lane);
+	wv_minstat_init(s, m, lane);
 	wsync();
 }
 
 /* process_frame :1212 -- one 256-sample analysis/synthesis frame; in and
  * out are 256-sample LDS buffers */
-MD void wv_process_frame(NppWave *W, const int16_t *in, int16_t *out, const WvConst *kc,
+MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *out, const WvConst *kc,
 			 int lane)
 {
 	PROF_SCOPE(34);
-	NppState *s = &W->s;
+	NppState *s = wv_S(W);
 	NppScratch *w = &W->w;
 	int16_t *yb = w->ybuf;
 	int32_t *ty = w->temp_yy;
@@ -513,7 +522,7 @@ MD void wv_process_frame(NppWave *W, const int16_t *in, int16_t *out, const WvCo
 	Word16 slope = npp_noise_slope(s);
 	LANE_LOOP(i, NPP_NB) {
 		npp_bias2_bin(s, w, W->bsp, W->bsh, W->bsub, W->bsubsh, vsq, f1, f2, i);
-		npp_min_search_bin(s, W->bsp, W->bsh, W->bsub, W->bsubsh, slope, i);
+		npp_min_search_bin(s, m, W->bsp, W->bsh, W->bsub, W->bsubsh, slope, i);
 		gk[i] = divide_s(shr(w->YY[i], 1), s->lambdaD[i]);
 		gks[i] = sub(add(w->YY_shift[i], 1), s->lambdaD_shift[i]);
 	}
@@ -714,11 +723,11 @@ MD void wv_process_frame(NppWave *W, const int16_t *in, int16_t *out, const WvCo
 /* npp :170 -- 180 new samples from `x` (global memory), 180 enhanced
  * samples back to the same place.  `avail` = valid samples at x for the
  * first call's 256-sample read (npp.c:176-189); short reads see zeros. */
-MD void wv_npp_frame(NppWave *W, int16_t *x, int avail, bool rate1200, const WvConst *kc,
+MD void wv_npp_frame(NppWave *W, NppState *m, int16_t *x, int avail, bool rate1200, const WvConst *kc,
 		     int lane)
 {
 	PROF_SCOPE(0);
-	NppState *s = &W->s;
+	NppState *s = wv_S(W);
 	if (!s->started) {
 		int16_t *noise = W->buf;
 		LANE_LOOP(i, NPP_WIN) {
@@ -730,7 +739,7 @@ MD void wv_npp_frame(NppWave *W, int16_t *x, int avail, bool rate1200, const WvC
 			noise[i] = v;
 		}
 		wsync();
-		wv_enh_init(W, noise, kc, lane);
+		wv_enh_init(W, noise, kc, lane, m);
 		LANE_LOOP(i, NPP_WIN)
 			s->speech_in[i] = 0;
 		s->started = 1;
@@ -742,7 +751,7 @@ MD void wv_npp_frame(NppWave *W, int16_t *x, int avail, bool rate1200, const WvC
 	LANE_LOOP(i, NPP_HOP)
 		s->speech_in[NPP_OVL + i] = x[i];
 	wsync();
-	wv_process_frame(W, s->speech_in, W->out, kc, lane);
+	wv_process_frame(W, m, s->speech_in, W->out, kc, lane);
 	LANE_LOOP(i, NPP_OVL) {
 		Word16 o = add(W->out[i], s->overlap[i]);
 		s->overlap[i] = W->out[NPP_HOP + i];
@@ -759,8 +768,8 @@ MD void wv_state_in(NppWave *W, const NppState *g, int lane)
 {
 	PROF_SCOPE(35);
 	const uint32_t *src = (const uint32_t *) g;
-	uint32_t *dst = (uint32_t *) &W->s;
-	LANE_LOOP(i, (int) (sizeof(NppState) / 4))
+	uint32_t *dst = W->s_hot;
+	LANE_LOOP(i, (int) (NPP_HOT_BYTES / 4))
 		dst[i] = src[i];
 	wsync();
 }
@@ -769,9 +778,9 @@ MD void wv_state_out(NppState *g, const NppWave *W, int lane)
 {
 	PROF_SCOPE(35);
 	wsync();
-	const uint32_t *src = (const uint32_t *) &W->s;
+	const uint32_t *src = W->s_hot;
 	uint32_t *dst = (uint32_t *) g;
-	LANE_LOOP(i, (int) (sizeof(NppState) / 4))
+	LANE_LOOP(i, (int) (NPP_HOT_BYTES / 4))
 		dst[i] = src[i];
 }
 
