@@ -50,6 +50,10 @@ SF_SAMPLES = 540
 SF_BYTES = 11
 SF_SECONDS = SF_SAMPLES / 8000.0
 PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12     # INT32 lane-ops/s, T
+# Keccak-f[1600] per voice packet, 64-bit ops counted as two 32-bit lane-ops:
+# per round theta 55 (25 xor parity, 5 rot + 5 xor D, 25 xor apply), rho+pi
+# 24 rot, chi 75 (not, and, xor per lane), iota 1 = 155 64-bit ops; x 24 rounds
+VC_OPS_PER_PACKET = 2 * 155 * 24
 REF_TOOL = os.path.join(ROOT, "oracle", "_ref", "ref_tool")
 
 
@@ -213,6 +217,28 @@ def main():
                "ms_per_step": 1e3 * dec_s / K, "kernel_ms": dec_kms}
         log("decode: %.1f ms/step (kernel %.1f ms)" % (1e3 * dec_s / K, dec_kms))
 
+    # voice-frame crypt (VoiceEnc, crp.c:986-1000) of each superframe's
+    # packets, the TX step after melpe_a: one packet per channel per launch
+    lib = eng.lib
+    g = torch.Generator().manual_seed(RUN_SEED + rank)
+    keys = torch.randint(0, 256, (C, 16), dtype=torch.uint8, generator=g).to(dev)
+    ctrs = torch.randint(0, 2**31, (C,), dtype=torch.int32, generator=g).to(dev)
+    cbits = bits.clone()
+
+    def crypt(s):
+        if lib.melpe_voice_crypt_dev(cbits[s].data_ptr(), ctrs.data_ptr(), keys.data_ptr(),
+                                     None, C, 1, 0, sptr):
+            raise RuntimeError(lib.melpe_last_error().decode())
+    crypt_s, (crypt_kms,) = timed([crypt])
+    crypt_ach = VC_OPS_PER_PACKET * C / (crypt_kms / 1e3) / 1e12
+    vcrypt = {"kernel": "k_voice_crypt", "value": world * C * K / crypt_s, "unit": "packets/s",
+              "kernel_ms": crypt_kms, "packets_per_launch": C,
+              "roofline": {"bound": "valu", "ops_per_packet": VC_OPS_PER_PACKET,
+                           "achieved": crypt_ach, "peak": PEAK_VALU_TOPS,
+                           "unit": "T INT32 VALU lane-ops/s", "frac": crypt_ach / PEAK_VALU_TOPS,
+                           "algorithmic_hbm_bytes_per_launch": C * (2 * SF_BYTES + 16 + 4)}}
+    log("voice crypt: kernel %.3f ms per %d packets" % (crypt_kms, C))
+
     if rank != 0:
         return
     value = world * C * K * SF_SECONDS / enc_s
@@ -258,7 +284,7 @@ def main():
                    "parallelism": "channel shards, %d GPU(s), no collective" % world},
         "realtime_factor": value / (world * C),
         "roofline": roof, "cpu_baseline": base, "decode": dec, "parity_spot_check": parity,
-        "bitstream_gather": gathered,
+        "bitstream_gather": gathered, "voice_crypt": vcrypt,
     }
     print(json.dumps(line), flush=True)
 

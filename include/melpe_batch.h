@@ -88,6 +88,25 @@ int melpe_synth_host(uint32_t run_seed, uint32_t channel, int16_t *out, int samp
  * measured with HIP events (0 if unavailable) */
 double melpe_last_kernel_ms(const melpe_engine *e);
 
+/* Voice-frame encryption, the step after melpe_a on TX and before melpe_s on
+ * RX: PairPhone's VoiceEnc (dir 0) / VoiceDec (dir 1), crp.c:986-1027,
+ * called from MakeCtr (crp.c:819) and ProcessCtr (crp.c:980).  Each 11-byte
+ * packet is XORed in place with gamma = Keccak sponge (r 576, c 1024) of
+ * counter (4 bytes little-endian) || key (16 bytes), 81 bits.
+ * pkts: C x K x 11 bytes (packet k of channel c at (c*K + k)*11).
+ * counters: C uint32, packet k uses counters[c] + k (cnt_out / cnt_in, which
+ *   advance by one per packet, crp.c:805).
+ * keys: C x 16 bytes, the channel's skey[0..15] to encrypt or skey[16..31]
+ *   to decrypt (crp.c:995, :1021); device pointer 16-byte aligned.
+ * invert: optional C-byte mask (NULL = none), decrypt only: nonzero = the
+ *   channel polarity flag finv < 0 (crp.c:1011-1015), the packet's 81 bits
+ *   are inverted before decryption. */
+int melpe_voice_crypt_dev(void *d_pkts, const void *d_counters, const void *d_keys,
+			  const void *d_invert, int channels, int packets, int dir,
+			  void *hip_stream);
+int melpe_voice_crypt_host(unsigned char *pkts, const uint32_t *counters,
+			   const unsigned char *keys, const uint8_t *invert, int channels,
+			   int packets, int dir);
 const char *melpe_last_error(void);
 
 /* Diagnostics: per-stage wave-cycle totals of a profiling build

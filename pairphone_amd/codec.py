@@ -52,6 +52,8 @@ def load_library(path=None):
         "melpe_last_error": (ctypes.c_char_p, []),
         "melpe_single_reset": (i32, []),
         "melpe_prof_read": (i32, [vp, i32]),
+        "melpe_voice_crypt_dev": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
+        "melpe_voice_crypt_host": (i32, [vp, vp, vp, vp, i32, i32, i32]),
         "melpe_i": (None, []),
         "melpe_a": (None, [vp, vp]),
         "melpe_s": (None, [vp, vp]),
@@ -80,6 +82,35 @@ def synth_signal(run_seed, channel, samples):
     out = np.zeros(samples, dtype=np.int16)
     _check(load_library().melpe_synth_host(run_seed, channel, _ptr(out), samples))
     return out
+
+
+def _crypt(pkts, counters, keys, invert, direction):
+    pkts = np.ascontiguousarray(pkts, dtype=np.uint8)
+    if pkts.ndim == 2:
+        pkts = pkts[:, None, :]
+    if pkts.ndim != 3 or pkts.shape[2] != SF_BYTES:
+        raise ValueError("packets must be C x 11 or C x K x 11 bytes")
+    out = pkts.copy()
+    C, K = out.shape[:2]
+    counters = np.ascontiguousarray(counters, dtype=np.uint32).reshape(C)
+    keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(C, 16)
+    inv = None if invert is None else np.ascontiguousarray(invert, dtype=np.uint8).reshape(C)
+    _check(load_library().melpe_voice_crypt_host(_ptr(out), _ptr(counters), _ptr(keys),
+                                                  _ptr(inv), C, K, direction))
+    return out
+
+
+def VoiceEnc(pkts, counters, keys):
+    """crp.c:986-1000 on C channels x K packets: each 11-byte packet XORed
+    with the 81-bit sponge keystream of (counters[c] + k, keys[c]), keys =
+    the channel's skey[0..15].  Returns the encrypted copy."""
+    return _crypt(pkts, counters, keys, None, 0)
+
+
+def VoiceDec(pkts, counters, keys, invert=None):
+    """crp.c:1004-1027: `invert[c]` nonzero = polarity flag finv < 0 (the
+    81 bits are inverted first); keys = skey[16..31]."""
+    return _crypt(pkts, counters, keys, invert, 1)
 
 
 class MelpeEngine:

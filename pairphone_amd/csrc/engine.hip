@@ -24,6 +24,7 @@
 #include "kern.h"
 #define SYN_FN __host__ __device__ static inline
 #include "synth.h"
+#include "voice_crypt.h"
 #include "../../include/melpe.h"
 #include "../../include/melpe_batch.h"
 
@@ -127,6 +128,32 @@ __global__ __launch_bounds__(WAVE) void k_synth(synth_state *s, int16_t *out, in
 	synth_state st = s[c];
 	synth_block(&st, out + (size_t) c * samples, samples);
 	s[c] = st;
+}
+
+
+/* VoiceEnc / VoiceDec (crp.c:986-1027, voice_crypt.h), one lane per packet:
+ * packet k of channel c is pkts[(c*K + k)*11 ..], its counter counters[c] + k
+ * (cnt_out / cnt_in advance by one per packet, crp.c:805), its key the
+ * channel's 16 bytes keys[c*16 ..] */
+__global__ __launch_bounds__(256) void k_voice_crypt(unsigned char *pkts, const uint32_t *counters,
+						     const uint4 *keys, const uint8_t *invert,
+						     int channels, int packets, int dir)
+{
+	long i = blockIdx.x * (long) blockDim.x + threadIdx.x;
+	if (i >= (long) channels * packets)
+		return;
+	int c = (int) (i / packets), k = (int) (i - (long) c * packets);
+	uint4 kv = keys[c];
+	uint32_t key[4] = {kv.x, kv.y, kv.z, kv.w};
+	unsigned char *p = pkts + i * VC_PKT_BYTES;
+	unsigned char b[VC_PKT_BYTES];
+#pragma unroll
+	for (int j = 0; j < VC_PKT_BYTES; j++)
+		b[j] = p[j];
+	vc_apply(b, counters[c] + (uint32_t) k, key, dir, invert ? invert[c] : 0);
+#pragma unroll
+	for (int j = 0; j < VC_PKT_BYTES; j++)
+		p[j] = b[j];
 }
 
 /* ------------------------------------------------------------------ */
@@ -590,6 +617,55 @@ void melpe_s(short *sp, unsigned char *buf)
 		fprintf(stderr, "libmelpe_amd: melpe_s failed: %s\n", g_err.c_str());
 		abort();
 	}
+}
+
+
+int melpe_voice_crypt_dev(void *d_pkts, const void *d_counters, const void *d_keys,
+			  const void *d_invert, int channels, int packets, int dir,
+			  void *hip_stream)
+{
+	if (!d_pkts || !d_counters || !d_keys || channels <= 0 || packets <= 0 ||
+	    (dir != 0 && dir != 1))
+		return fail_msg("melpe_voice_crypt_dev: bad arguments");
+	if (((uintptr_t) d_keys & 15) || ((uintptr_t) d_counters & 3))
+		return fail_msg("melpe_voice_crypt_dev: keys must be 16-byte and counters "
+				"4-byte aligned");
+	long n = (long) channels * packets;
+	long blocks = (n + 255) / 256;
+	if (blocks > 0x7fffffffL)
+		return fail_msg("melpe_voice_crypt_dev: too many packets");
+	k_voice_crypt<<<(unsigned) blocks, 256, 0, (hipStream_t) hip_stream>>>(
+		(unsigned char *) d_pkts, (const uint32_t *) d_counters, (const uint4 *) d_keys,
+		(const uint8_t *) d_invert, channels, packets, dir);
+	HIPCHK(hipGetLastError());
+	return 0;
+}
+
+int melpe_voice_crypt_host(unsigned char *pkts, const uint32_t *counters,
+			   const unsigned char *keys, const uint8_t *invert, int channels,
+			   int packets, int dir)
+{
+	if (!pkts || !counters || !keys || channels <= 0 || packets <= 0)
+		return fail_msg("melpe_voice_crypt_host: bad arguments");
+	size_t pb = (size_t) channels * packets * VC_PKT_BYTES;
+	size_t kb = (size_t) channels * VC_KEY_BYTES, cb = (size_t) channels * 4;
+	unsigned char *d = nullptr;
+	HIPCHK(hipMalloc(&d, kb + cb + channels + pb));
+	unsigned char *dk = d, *dc = d + kb, *di = dc + cb, *dp = di + channels;
+	int rc = 0;
+	hipError_t he;
+	if ((he = hipMemcpy(dk, keys, kb, hipMemcpyHostToDevice)) != hipSuccess ||
+	    (he = hipMemcpy(dc, counters, cb, hipMemcpyHostToDevice)) != hipSuccess ||
+	    (invert && (he = hipMemcpy(di, invert, channels, hipMemcpyHostToDevice)) != hipSuccess) ||
+	    (he = hipMemcpy(dp, pkts, pb, hipMemcpyHostToDevice)) != hipSuccess)
+		rc = fail("melpe_voice_crypt_host: upload", he);
+	if (!rc)
+		rc = melpe_voice_crypt_dev(dp, dc, dk, invert ? di : nullptr, channels, packets,
+					   dir, nullptr);
+	if (!rc && (he = hipMemcpy(pkts, dp, pb, hipMemcpyDeviceToHost)) != hipSuccess)
+		rc = fail("melpe_voice_crypt_host: download", he);
+	hipFree(d);
+	return rc;
 }
 
 }  // extern "C"

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "codec.h"
+#include "voice_crypt.h"
 
 using namespace mlp;
 
@@ -209,6 +210,22 @@ int emu_stagecount(uint64_t *out, int n)
 const char *emu_op_names(void)
 {
 	return MELPE_OP_NAMES;
+}
+
+
+/* host build of the voice-frame crypt (voice_crypt.h), same layout as
+ * melpe_voice_crypt_host */
+int emu_voice_crypt(unsigned char *pkts, const uint32_t *counters, const unsigned char *keys,
+		    const uint8_t *invert, int channels, int packets, int dir)
+{
+	for (int c = 0; c < channels; c++) {
+		uint32_t key[4];
+		memcpy(key, keys + 16 * (size_t) c, 16);
+		for (int k = 0; k < packets; k++)
+			vc_apply(pkts + ((size_t) c * packets + k) * VC_PKT_BYTES,
+				 counters[c] + (uint32_t) k, key, dir, invert ? invert[c] : 0);
+	}
+	return 0;
 }
 
 }  // extern "C"
