@@ -238,6 +238,22 @@ def main():
                            "unit": "T INT32 VALU lane-ops/s", "frac": crypt_ach / PEAK_VALU_TOPS,
                            "algorithmic_hbm_bytes_per_launch": C * (2 * SF_BYTES + 16 + 4)}}
     log("voice crypt: kernel %.3f ms per %d packets" % (crypt_kms, C))
+    # TX voice-activity gate (vad2 x6 per superframe, tx.c:234-239) on the
+    # same PCM, one superframe per channel per launch, state resident
+    vst = torch.zeros(C * lib.melpe_vad_state_bytes(), dtype=torch.uint8, device=dev)
+    votes = torch.zeros((W + K, C), dtype=torch.uint8, device=dev)
+    if lib.melpe_vad_reset_dev(vst.data_ptr(), C, None, sptr):
+        raise RuntimeError(lib.melpe_last_error().decode())
+
+    def vad(s):
+        if lib.melpe_vad_dev(vst.data_ptr(), pcm[s].data_ptr(), votes[s].data_ptr(), C, None,
+                             sptr):
+            raise RuntimeError(lib.melpe_last_error().decode())
+    vad_s, (vad_kms,) = timed([vad])
+    vgate = {"kernel": "k_vad", "value": world * C * K * SF_SECONDS / vad_s,
+             "unit": "channel-s/s gated", "kernel_ms": vad_kms,
+             "silent_fraction": float((votes[W:] == 0).float().mean().item())}
+    log("vad: kernel %.3f ms per %d channel-superframes" % (vad_kms, C))
 
     if rank != 0:
         return
@@ -284,7 +300,7 @@ def main():
                    "parallelism": "channel shards, %d GPU(s), no collective" % world},
         "realtime_factor": value / (world * C),
         "roofline": roof, "cpu_baseline": base, "decode": dec, "parity_spot_check": parity,
-        "bitstream_gather": gathered, "voice_crypt": vcrypt,
+        "bitstream_gather": gathered, "voice_crypt": vcrypt, "vad": vgate,
     }
     print(json.dumps(line), flush=True)
 

@@ -107,6 +107,23 @@ int melpe_voice_crypt_dev(void *d_pkts, const void *d_counters, const void *d_ke
 int melpe_voice_crypt_host(unsigned char *pkts, const uint32_t *counters,
 			   const unsigned char *keys, const uint8_t *invert, int channels,
 			   int packets, int dir);
+/* Voice activity detection, the TX gate in front of melpe_a: PairPhone runs
+ * the AMR VAD option 2 (vad/vad2.c:203) on six 80-sample windows of every
+ * superframe, at offsets 10, 100, ..., 460 (tx.c:234-239,
+ * melpe_enc.c:48-53), and sends the superframe as silence when all six say
+ * no.  state: C records of melpe_vad_state_bytes() bytes (device memory,
+ * 4-byte aligned), one vadState2 (vad/vad2.h:76-103) per channel;
+ * melpe_vad_reset_dev = vad2_reset (vad/vad2.c:876) on the channels of
+ * `mask` (NULL = all).  melpe_vad_dev: sp is C x 540 int16, votes[c] (out,
+ * uint8) = the sum of the six decisions (0 = silence); inactive channels
+ * (active[c] == 0) keep their state and vote.  melpe_vad_host takes host
+ * buffers, state included. */
+int melpe_vad_state_bytes(void);
+int melpe_vad_reset_dev(void *d_state, int channels, const void *d_mask, void *hip_stream);
+int melpe_vad_dev(void *d_state, const void *d_sp, void *d_votes, int channels,
+		  const void *d_active, void *hip_stream);
+int melpe_vad_host(unsigned char *state, const int16_t *sp, uint8_t *votes, int channels,
+		   const uint8_t *active);
 const char *melpe_last_error(void);
 
 /* Diagnostics: per-stage wave-cycle totals of a profiling build

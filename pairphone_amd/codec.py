@@ -54,6 +54,10 @@ def load_library(path=None):
         "melpe_prof_read": (i32, [vp, i32]),
         "melpe_voice_crypt_dev": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
         "melpe_voice_crypt_host": (i32, [vp, vp, vp, vp, i32, i32, i32]),
+        "melpe_vad_state_bytes": (i32, []),
+        "melpe_vad_reset_dev": (i32, [vp, i32, vp, vp]),
+        "melpe_vad_dev": (i32, [vp, vp, vp, i32, vp, vp]),
+        "melpe_vad_host": (i32, [vp, vp, vp, i32, vp]),
         "melpe_i": (None, []),
         "melpe_a": (None, [vp, vp]),
         "melpe_s": (None, [vp, vp]),
@@ -111,6 +115,29 @@ def VoiceDec(pkts, counters, keys, invert=None):
     """crp.c:1004-1027: `invert[c]` nonzero = polarity flag finv < 0 (the
     81 bits are inverted first); keys = skey[16..31]."""
     return _crypt(pkts, counters, keys, invert, 1)
+
+
+class Vad:
+    """PairPhone's TX voice-activity gate on C channels (vad/vad2.c run on six
+    windows per superframe, tx.c:234-239); state per channel = a fresh
+    vad2_reset vadState2.  `superframe(sp)` returns the C votes (0..6);
+    0 means the superframe is sent as silence."""
+
+    def __init__(self, channels):
+        self.lib = load_library()
+        self.C = channels
+        self.state = np.zeros(channels * self.lib.melpe_vad_state_bytes(), np.uint8)
+
+    def reset(self):
+        self.state[:] = 0
+
+    def superframe(self, sp, active=None):
+        sp = np.ascontiguousarray(sp, dtype=np.int16).reshape(self.C, SF_SAMPLES)
+        votes = np.zeros(self.C, np.uint8)
+        act = None if active is None else np.ascontiguousarray(active, np.uint8)
+        _check(self.lib.melpe_vad_host(_ptr(self.state), _ptr(sp), _ptr(votes), self.C,
+                                       _ptr(act)))
+        return votes
 
 
 class MelpeEngine:

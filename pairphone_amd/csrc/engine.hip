@@ -25,6 +25,7 @@
 #define SYN_FN __host__ __device__ static inline
 #include "synth.h"
 #include "voice_crypt.h"
+#include "vad.h"
 #include "../../include/melpe.h"
 #include "../../include/melpe_batch.h"
 
@@ -154,6 +155,30 @@ __global__ __launch_bounds__(256) void k_voice_crypt(unsigned char *pkts, const 
 #pragma unroll
 	for (int j = 0; j < VC_PKT_BYTES; j++)
 		p[j] = b[j];
+}
+
+
+/* VAD of one superframe per channel (vad.h): the six vad2 windows of
+ * tx.c:234-239 on the channel's 540 samples; votes[c] = their sum */
+__global__ __launch_bounds__(WAVE) void k_vad(VadState *st, const int16_t *sp, uint8_t *votes,
+					      const uint8_t *active, int channels)
+{
+	int c = blockIdx.x * blockDim.x + threadIdx.x;
+	if (c >= channels || (active && !active[c]))
+		return;
+	VadState s = st[c];
+	votes[c] = (uint8_t) va_superframe(sp + (size_t) c * MELPE_SF_SAMPLES, &s);
+	st[c] = s;
+}
+
+__global__ __launch_bounds__(WAVE) void k_vad_reset(VadState *st, const uint8_t *mask, int channels)
+{
+	int c = blockIdx.x * blockDim.x + threadIdx.x;
+	if (c >= channels || (mask && !mask[c]))
+		return;
+	VadState z;
+	memset(&z, 0, sizeof z);
+	st[c] = z;
 }
 
 /* ------------------------------------------------------------------ */
@@ -664,6 +689,64 @@ int melpe_voice_crypt_host(unsigned char *pkts, const uint32_t *counters,
 					   dir, nullptr);
 	if (!rc && (he = hipMemcpy(pkts, dp, pb, hipMemcpyDeviceToHost)) != hipSuccess)
 		rc = fail("melpe_voice_crypt_host: download", he);
+	hipFree(d);
+	return rc;
+}
+
+
+int melpe_vad_state_bytes(void)
+{
+	return (int) sizeof(VadState);
+}
+
+int melpe_vad_reset_dev(void *d_state, int channels, const void *d_mask, void *hip_stream)
+{
+	if (!d_state || channels <= 0)
+		return fail_msg("melpe_vad_reset_dev: bad arguments");
+	if ((uintptr_t) d_state & 3)
+		return fail_msg("melpe_vad_reset_dev: state must be 4-byte aligned");
+	k_vad_reset<<<grid_for(channels), WAVE, 0, (hipStream_t) hip_stream>>>(
+		(VadState *) d_state, (const uint8_t *) d_mask, channels);
+	HIPCHK(hipGetLastError());
+	return 0;
+}
+
+int melpe_vad_dev(void *d_state, const void *d_sp, void *d_votes, int channels,
+		  const void *d_active, void *hip_stream)
+{
+	if (!d_state || !d_sp || !d_votes || channels <= 0)
+		return fail_msg("melpe_vad_dev: bad arguments");
+	if ((uintptr_t) d_state & 3)
+		return fail_msg("melpe_vad_dev: state must be 4-byte aligned");
+	k_vad<<<grid_for(channels), WAVE, 0, (hipStream_t) hip_stream>>>(
+		(VadState *) d_state, (const int16_t *) d_sp, (uint8_t *) d_votes,
+		(const uint8_t *) d_active, channels);
+	HIPCHK(hipGetLastError());
+	return 0;
+}
+
+int melpe_vad_host(unsigned char *state, const int16_t *sp, uint8_t *votes, int channels,
+		   const uint8_t *active)
+{
+	if (!state || !sp || !votes || channels <= 0)
+		return fail_msg("melpe_vad_host: bad arguments");
+	size_t sb = sizeof(VadState) * (size_t) channels;
+	size_t pb = sizeof(int16_t) * MELPE_SF_SAMPLES * (size_t) channels;
+	unsigned char *d = nullptr;
+	HIPCHK(hipMalloc(&d, sb + pb + 2 * (size_t) channels));
+	unsigned char *ds = d, *dp = d + sb, *dv = dp + pb, *da = dv + channels;
+	int rc = 0;
+	hipError_t he;
+	if ((he = hipMemcpy(ds, state, sb, hipMemcpyHostToDevice)) != hipSuccess ||
+	    (he = hipMemcpy(dp, sp, pb, hipMemcpyHostToDevice)) != hipSuccess ||
+	    (he = hipMemcpy(dv, votes, channels, hipMemcpyHostToDevice)) != hipSuccess ||
+	    (active && (he = hipMemcpy(da, active, channels, hipMemcpyHostToDevice)) != hipSuccess))
+		rc = fail("melpe_vad_host: upload", he);
+	if (!rc)
+		rc = melpe_vad_dev(ds, dp, dv, channels, active ? da : nullptr, nullptr);
+	if (!rc && ((he = hipMemcpy(state, ds, sb, hipMemcpyDeviceToHost)) != hipSuccess ||
+		    (he = hipMemcpy(votes, dv, channels, hipMemcpyDeviceToHost)) != hipSuccess))
+		rc = fail("melpe_vad_host: download", he);
 	hipFree(d);
 	return rc;
 }

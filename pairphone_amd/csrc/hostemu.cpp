@@ -15,6 +15,7 @@
 
 #include "codec.h"
 #include "voice_crypt.h"
+#include "vad.h"
 
 using namespace mlp;
 
@@ -225,6 +226,23 @@ int emu_voice_crypt(unsigned char *pkts, const uint32_t *counters, const unsigne
 			vc_apply(pkts + ((size_t) c * packets + k) * VC_PKT_BYTES,
 				 counters[c] + (uint32_t) k, key, dir, invert ? invert[c] : 0);
 	}
+	return 0;
+}
+
+int emu_vad_state_bytes(void)
+{
+	return (int) sizeof(VadState);
+}
+
+/* host build of k_vad: `nsf` superframes of C channels, sp C x (nsf*540),
+ * votes C x nsf, state C records (zeroed by the caller = vad2_reset) */
+int emu_vad(unsigned char *state, const int16_t *sp, uint8_t *votes, int channels, int nsf)
+{
+	VadState *st = (VadState *) state;
+	for (int c = 0; c < channels; c++)
+		for (int k = 0; k < nsf; k++)
+			votes[(size_t) c * nsf + k] = (uint8_t) va_superframe(
+				sp + ((size_t) c * nsf + k) * 540, &st[c]);
 	return 0;
 }
 

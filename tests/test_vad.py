@@ -1,0 +1,111 @@
+"""TX voice-activity gate parity against the reference.
+
+The AMR VAD option 2 (vad/vad2.c) that PairPhone runs on six 80-sample
+windows per superframe (tx.c:234-239, melpe_enc.c:48-53).  Oracle = the
+reference's own vad/*.c compiled into oracle/_ref/libref_vad.so (harness
+oracle/ref_vad.c, fresh vad2_reset state per channel); golden fixture
+tests/golden/vad.json (make_vad_golden.py): 56 speech-like channels + 8 edge
+channels x 149 superframes, votes = sum of the six decisions.
+
+CPU: oracle and the host build of vad.h against the golden.
+GPU: k_vad through the C ABI against the golden (host ABI, superframe by
+superframe), at 65,536 channels against the live oracle through the device
+ABI, ragged activity masks and per-channel reset.
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, GOLDEN
+
+sys.path.insert(0, GOLDEN)
+from make_vad_golden import inputs, ref_vad  # noqa: E402
+
+EMU = os.path.join(ROOT, "build", "libmelpe_hostemu.so")
+P = ctypes.c_void_p
+
+
+def golden():
+    g = json.load(open(os.path.join(GOLDEN, "vad.json")))
+    v = np.frombuffer(bytes.fromhex(g["votes_hex"]), np.uint8)
+    return g, v.reshape(g["channels"], g["superframes"])
+
+
+def emu_vad(x, nsf):
+    lib = ctypes.CDLL(EMU)
+    C = x.shape[0]
+    st = np.zeros(C * lib.emu_vad_state_bytes(), np.uint8)
+    votes = np.zeros((C, nsf), np.uint8)
+    x = np.ascontiguousarray(x, np.int16)
+    lib.emu_vad(P(st.ctypes.data), P(x.ctypes.data), P(votes.ctypes.data), C, nsf)
+    return votes
+
+
+def test_oracle_matches_golden():
+    g, want = golden()
+    assert np.array_equal(ref_vad(inputs(g["channels"], g["superframes"], g["seed"]),
+                                  g["superframes"]), want)
+
+
+def test_hostemu_matches_golden():
+    g, want = golden()
+    got = emu_vad(inputs(g["channels"], g["superframes"], g["seed"]), g["superframes"])
+    assert np.array_equal(got, want)
+    assert (want == 0).any() and (want == 6).any()     # both gate outcomes covered
+
+
+@pytest.mark.gpu
+def test_gpu_matches_golden():
+    from pairphone_amd import Vad
+    g, want = golden()
+    C, nsf = g["channels"], g["superframes"]
+    x = inputs(C, nsf, g["seed"]).reshape(C, nsf, 540)
+    vad = Vad(C)
+    got = np.stack([vad.superframe(x[:, k]) for k in range(nsf)], axis=1)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_gpu_65536_channels_ragged_match_reference():
+    import torch
+    from pairphone_amd import load_library, synth_signal
+    lib = load_library()
+    C, nsf = 65536, 6
+    rng = np.random.default_rng(5)
+    # distinct channels: generator channels 0..255 cycled, scaled per channel
+    base = np.stack([synth_signal(3, c, nsf * 540) for c in range(256)])
+    gain = rng.integers(1, 5, C)
+    x = (base[np.arange(C) % 256].astype(np.int32) * gain[:, None] // 2)
+    x = np.clip(x, -32768, 32767).astype(np.int16)
+    want = ref_vad(x, nsf)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    st = torch.zeros(C * lib.melpe_vad_state_bytes(), dtype=torch.uint8, device=dev)
+    assert lib.melpe_vad_reset_dev(st.data_ptr(), C, None, s) == 0
+    d_x = torch.from_numpy(x.reshape(C, nsf, 540)).to(dev)
+    votes = torch.full((nsf, C), 255, dtype=torch.uint8, device=dev)
+    for k in range(nsf):
+        sp = d_x[:, k].contiguous()
+        assert lib.melpe_vad_dev(st.data_ptr(), sp.data_ptr(), votes[k].data_ptr(), C,
+                                 None, s) == 0
+    assert np.array_equal(votes.cpu().numpy().T, want)
+    # ragged: odd channels skip superframe 0 (state and vote untouched), so
+    # they see superframes 1..5 as their first five
+    mask = (np.arange(C) % 2 == 0).astype(np.uint8)
+    d_m = torch.from_numpy(mask).to(dev)
+    assert lib.melpe_vad_reset_dev(st.data_ptr(), C, None, s) == 0
+    votes.fill_(255)
+    for k in range(nsf):
+        sp = d_x[:, k].contiguous()
+        m = d_m.data_ptr() if k == 0 else None
+        assert lib.melpe_vad_dev(st.data_ptr(), sp.data_ptr(), votes[k].data_ptr(), C, m,
+                                 s) == 0
+    got = votes.cpu().numpy().T
+    assert np.array_equal(got[0::2], want[0::2])
+    assert (got[1::2, 0] == 255).all()
+    want_odd = ref_vad(x.reshape(C, nsf, 540)[1::2, 1:].reshape(C // 2, -1), nsf - 1)
+    assert np.array_equal(got[1::2, 1:], want_odd)
