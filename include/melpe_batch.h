@@ -124,6 +124,13 @@ int melpe_vad_dev(void *d_state, const void *d_sp, void *d_votes, int channels,
 		  const void *d_active, void *hip_stream);
 int melpe_vad_host(unsigned char *state, const int16_t *sp, uint8_t *votes, int channels,
 		   const uint8_t *active);
+/* The TX front end of one superframe (BASELINE config 5, tx.c:232-245):
+ * the VAD gate above, then melpe_a on the channels it opens.  gate[c]
+ * (out) = active[c] && votes[c] > 0; gated-off channels keep their codec
+ * state, PCM and bits, exactly as when tx.c skips melpe_a.  d_active NULL =
+ * all channels (ragged streams pass their mask). */
+int melpe_tx_dev(melpe_engine *e, void *d_vad_state, void *d_bits, void *d_sp, void *d_votes,
+		 void *d_gate, const void *d_active, void *hip_stream);
 const char *melpe_last_error(void);
 
 /* Diagnostics: per-stage wave-cycle totals of a profiling build

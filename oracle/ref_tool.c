@@ -271,6 +271,28 @@ int main(int argc, char **argv)
 			fclose(dump);
 		return 0;
 	}
+	/* VAD-gated TX (tx.c:234-245): superframe k is encoded only when
+	 * gate[k] != 0; a gated-off superframe leaves the codec untouched and
+	 * its 11 output bytes zero */
+	if (!strcmp(argv[1], "encgate") && argc == 5) {
+		long len, glen, k;
+		int16_t *pcm = (int16_t *) read_file(argv[2], &len);
+		unsigned char *gate = (unsigned char *) read_file(argv[3], &glen);
+		unsigned char *bits = (unsigned char *) calloc(glen + 1, 11);
+		short sp[BLOCK];
+		FILE *f;
+		melpe_i();
+		for (k = 0; k < glen && (k + 1) * BLOCK * 2 <= len; k++) {
+			if (!gate[k])
+				continue;
+			memcpy(sp, pcm + k * BLOCK, sizeof(sp));
+			melpe_a(bits + k * 11, sp);
+		}
+		f = fopen(argv[4], "wb");
+		fwrite(bits, 11, k, f);
+		fclose(f);
+		return 0;
+	}
 	if (!strcmp(argv[1], "dec") && (argc == 4 || argc == 5)) {
 		long len, nsf;
 		unsigned char *bits = (unsigned char *) read_file(argv[2], &len);

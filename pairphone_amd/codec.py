@@ -58,6 +58,7 @@ def load_library(path=None):
         "melpe_vad_reset_dev": (i32, [vp, i32, vp, vp]),
         "melpe_vad_dev": (i32, [vp, vp, vp, i32, vp, vp]),
         "melpe_vad_host": (i32, [vp, vp, vp, i32, vp]),
+        "melpe_tx_dev": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
         "melpe_i": (None, []),
         "melpe_a": (None, [vp, vp]),
         "melpe_s": (None, [vp, vp]),
@@ -212,6 +213,11 @@ class MelpeEngine:
 
     def encode_ana_dev(self, d_bits, d_sp, d_active=None, stream=None):
         _check(self.lib.melpe_encode_ana_dev(self.h, d_bits, d_sp, d_active, stream))
+
+    def tx_dev(self, d_vad_state, d_bits, d_sp, d_votes, d_gate, d_active=None, stream=None):
+        """VAD gate + melpe_a on the channels it opens (tx.c:232-245)"""
+        _check(self.lib.melpe_tx_dev(self.h, d_vad_state, d_bits, d_sp, d_votes, d_gate,
+                                     d_active, stream))
 
     def decode_dev(self, d_sp, d_bits, d_active=None, stream=None):
         _check(self.lib.melpe_decode_dev(self.h, d_sp, d_bits, d_active, stream))

@@ -161,14 +161,22 @@ __global__ __launch_bounds__(256) void k_voice_crypt(unsigned char *pkts, const 
 /* VAD of one superframe per channel (vad.h): the six vad2 windows of
  * tx.c:234-239 on the channel's 540 samples; votes[c] = their sum */
 __global__ __launch_bounds__(WAVE) void k_vad(VadState *st, const int16_t *sp, uint8_t *votes,
-					      const uint8_t *active, int channels)
+					      uint8_t *gate, const uint8_t *active, int channels)
 {
 	int c = blockIdx.x * blockDim.x + threadIdx.x;
-	if (c >= channels || (active && !active[c]))
+	if (c >= channels)
 		return;
+	if (active && !active[c]) {
+		if (gate)
+			gate[c] = 0;
+		return;
+	}
 	VadState s = st[c];
-	votes[c] = (uint8_t) va_superframe(sp + (size_t) c * MELPE_SF_SAMPLES, &s);
+	int n = va_superframe(sp + (size_t) c * MELPE_SF_SAMPLES, &s);
 	st[c] = s;
+	votes[c] = (uint8_t) n;
+	if (gate)	/* tx.c:242-244: encoded when any window voted */
+		gate[c] = n > 0;
 }
 
 __global__ __launch_bounds__(WAVE) void k_vad_reset(VadState *st, const uint8_t *mask, int channels)
@@ -719,7 +727,7 @@ int melpe_vad_dev(void *d_state, const void *d_sp, void *d_votes, int channels,
 	if ((uintptr_t) d_state & 3)
 		return fail_msg("melpe_vad_dev: state must be 4-byte aligned");
 	k_vad<<<grid_for(channels), WAVE, 0, (hipStream_t) hip_stream>>>(
-		(VadState *) d_state, (const int16_t *) d_sp, (uint8_t *) d_votes,
+		(VadState *) d_state, (const int16_t *) d_sp, (uint8_t *) d_votes, nullptr,
 		(const uint8_t *) d_active, channels);
 	HIPCHK(hipGetLastError());
 	return 0;
@@ -749,6 +757,22 @@ int melpe_vad_host(unsigned char *state, const int16_t *sp, uint8_t *votes, int 
 		rc = fail("melpe_vad_host: download", he);
 	hipFree(d);
 	return rc;
+}
+
+
+int melpe_tx_dev(melpe_engine *e, void *d_vad_state, void *d_bits, void *d_sp, void *d_votes,
+		 void *d_gate, const void *d_active, void *hip_stream)
+{
+	if (!e || !d_vad_state || !d_bits || !d_sp || !d_votes || !d_gate)
+		return fail_msg("melpe_tx_dev: bad arguments");
+	if ((uintptr_t) d_vad_state & 3)
+		return fail_msg("melpe_tx_dev: state must be 4-byte aligned");
+	HIPCHK(hipSetDevice(e->device));
+	k_vad<<<grid_for(e->channels), WAVE, 0, (hipStream_t) hip_stream>>>(
+		(VadState *) d_vad_state, (const int16_t *) d_sp, (uint8_t *) d_votes,
+		(uint8_t *) d_gate, (const uint8_t *) d_active, e->channels);
+	HIPCHK(hipGetLastError());
+	return melpe_encode_dev(e, d_bits, d_sp, d_gate, hip_stream);
 }
 
 }  // extern "C"

@@ -35,3 +35,15 @@ def run_ref(*args, jobs=8):
 def engine_lib():
     from pairphone_amd import load_library
     return load_library()
+
+
+@pytest.fixture(autouse=True)
+def _torch_hip_first(request):
+    """GPU tests: bring up torch's HIP context before the engine library
+    makes its first HIP call, so tests that mix the C ABI with torch device
+    buffers see the same device set in any order."""
+    if request.node.get_closest_marker("gpu") is not None:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    yield

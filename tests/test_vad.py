@@ -109,3 +109,65 @@ def test_gpu_65536_channels_ragged_match_reference():
     assert (got[1::2, 0] == 255).all()
     want_odd = ref_vad(x.reshape(C, nsf, 540)[1::2, 1:].reshape(C // 2, -1), nsf - 1)
     assert np.array_equal(got[1::2, 1:], want_odd)
+
+
+@pytest.mark.gpu
+def test_gpu_tx_front_end_vad_gated_ragged_matches_reference(tmp_path, ref_tool):
+    """BASELINE config 5 in miniature: ragged stream lengths, the VAD gate
+    and melpe_a on the superframes it opens (melpe_tx_dev), against the
+    reference VAD + the reference codec run only on the gated superframes
+    (ref_tool encgate)."""
+    import subprocess
+    from concurrent.futures import ThreadPoolExecutor
+    import torch
+    from pairphone_amd import MelpeEngine, load_library, synth_signal
+    lib = load_library()
+    C, nsf = 96, 14
+    rng = np.random.default_rng(11)
+    x = np.stack([synth_signal(9, c, nsf * 540) for c in range(C)]).reshape(C, nsf, 540)
+    # silent stretches (low noise) so that the gate closes on some superframes
+    for c in range(C):
+        for k in rng.choice(nsf, size=rng.integers(0, 6), replace=False):
+            x[c, k] = rng.integers(-20, 21, 540)
+    lengths = rng.integers(3, nsf + 1, C)
+    want_votes = np.zeros((C, nsf), np.uint8)
+    for c in range(C):
+        L = lengths[c]
+        want_votes[c, :L] = ref_vad(x[c, :L].reshape(1, -1), L)[0]
+
+    def ref_bits(c):
+        L = lengths[c]
+        pcm, gate, out = (str(tmp_path / ("%s%d" % (n, c))) for n in ("p", "g", "b"))
+        x[c, :L].tofile(pcm)
+        (want_votes[c, :L] > 0).astype(np.uint8).tofile(gate)
+        subprocess.run([ref_tool, "encgate", pcm, gate, out], check=True)
+        return np.fromfile(out, np.uint8).reshape(L, 11)
+    with ThreadPoolExecutor(8) as ex:
+        want_bits = list(ex.map(ref_bits, range(C)))
+
+    dev = torch.device("cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    eng = MelpeEngine(C)
+    st = torch.zeros(C * lib.melpe_vad_state_bytes(), dtype=torch.uint8, device=dev)
+    assert lib.melpe_vad_reset_dev(st.data_ptr(), C, None, s) == 0
+    d_x = torch.from_numpy(np.ascontiguousarray(x.transpose(1, 0, 2))).to(dev)   # nsf x C x 540
+    bits = torch.zeros((nsf, C, 11), dtype=torch.uint8, device=dev)
+    votes = torch.zeros((nsf, C), dtype=torch.uint8, device=dev)
+    gate = torch.zeros((nsf, C), dtype=torch.uint8, device=dev)
+    for k in range(nsf):
+        act = torch.from_numpy((lengths > k).astype(np.uint8)).to(dev)
+        eng.tx_dev(st.data_ptr(), bits[k].data_ptr(), d_x[k].data_ptr(), votes[k].data_ptr(),
+                   gate[k].data_ptr(), act.data_ptr(), s)
+    torch.cuda.synchronize()
+    got_votes = votes.cpu().numpy().T
+    got_gate = gate.cpu().numpy().T
+    got_bits = bits.cpu().numpy().transpose(1, 0, 2)
+    closed = 0
+    for c in range(C):
+        L = lengths[c]
+        assert np.array_equal(got_votes[c, :L], want_votes[c, :L]), c
+        assert np.array_equal(got_gate[c], (np.arange(nsf) < L) & (want_votes[c] > 0)), c
+        assert np.array_equal(got_bits[c, :L], want_bits[c]), c
+        assert not got_bits[c, L:].any()
+        closed += int((want_votes[c, :L] == 0).sum())
+    assert closed > 0      # the gate did close somewhere
