@@ -131,6 +131,22 @@ int melpe_vad_host(unsigned char *state, const int16_t *sp, uint8_t *votes, int 
  * all channels (ragged streams pass their mask). */
 int melpe_tx_dev(melpe_engine *e, void *d_vad_state, void *d_bits, void *d_sp, void *d_votes,
 		 void *d_gate, const void *d_active, void *hip_stream);
+/* The VAD-framed stream format of melpe_enc.c:55-72 / melpe_dec.c:33-49
+ * (host functions, no GPU).  Per superframe a silent channel writes 1 byte,
+ * its carried txbuf[0] with bit 1 set; a voiced channel writes its 11 bytes
+ * with bytes 0 and 10 swapped, so that the first byte (bit 80 only) never has
+ * bit 1 set.  melpe_stream_pack does one superframe for C channels: bits
+ * C x 11 and votes C in (melpe_vad_dev), last C bytes in/out (the carried
+ * txbuf[0]; zero at the start: melpe_enc.c leaves it uninitialised and
+ * melpe_dec.c reads only bit 1 of it), out C x 11 and lens C (1 or 11; 0
+ * for channels that active excludes).  melpe_stream_unpack parses one
+ * channel's stream: bits (max_sf x 11, swap undone; zeros for silence) and
+ * voiced (1 = melpe_s it, 0 = 540 zero samples); returns the number of
+ * superframes, or < 0 for a truncated voiced frame. */
+int melpe_stream_pack(const unsigned char *bits, const uint8_t *votes, uint8_t *last,
+		      unsigned char *out, uint8_t *lens, int channels, const uint8_t *active);
+long melpe_stream_unpack(const unsigned char *stream, long nbytes, unsigned char *bits,
+			 uint8_t *voiced, long max_sf);
 const char *melpe_last_error(void);
 
 /* Diagnostics: per-stage wave-cycle totals of a profiling build

@@ -7,4 +7,4 @@ raises if the HIP library is missing.
 """
 from .codec import (MelpeEngine, Melpe, load_library, LIB_PATH,  # noqa: F401
                     SF_SAMPLES, SF_BYTES, FRAME_SAMPLES, synth_signal)
-from .codec import VoiceEnc, VoiceDec, Vad  # noqa: F401
+from .codec import VoiceEnc, VoiceDec, Vad, stream_pack, stream_unpack  # noqa: F401

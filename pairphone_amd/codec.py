@@ -59,6 +59,8 @@ def load_library(path=None):
         "melpe_vad_dev": (i32, [vp, vp, vp, i32, vp, vp]),
         "melpe_vad_host": (i32, [vp, vp, vp, i32, vp]),
         "melpe_tx_dev": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "melpe_stream_pack": (i32, [vp, vp, vp, vp, vp, i32, vp]),
+        "melpe_stream_unpack": (ctypes.c_long, [vp, ctypes.c_long, vp, vp, ctypes.c_long]),
         "melpe_i": (None, []),
         "melpe_a": (None, [vp, vp]),
         "melpe_s": (None, [vp, vp]),
@@ -116,6 +118,37 @@ def VoiceDec(pkts, counters, keys, invert=None):
     """crp.c:1004-1027: `invert[c]` nonzero = polarity flag finv < 0 (the
     81 bits are inverted first); keys = skey[16..31]."""
     return _crypt(pkts, counters, keys, invert, 1)
+
+
+def stream_pack(bits, votes):
+    """melpe_enc.c:55-72 framing of one channel: bits (nsf x 11) and VAD
+    votes (nsf) -> the framed byte stream (1 byte per silent superframe, 11
+    swapped bytes per voiced one)."""
+    lib = load_library()
+    bits = np.ascontiguousarray(bits, np.uint8).reshape(-1, SF_BYTES)
+    votes = np.ascontiguousarray(votes, np.uint8).reshape(-1)
+    last = np.zeros(1, np.uint8)
+    out = np.zeros(SF_BYTES, np.uint8)
+    n = np.zeros(1, np.uint8)
+    chunks = []
+    for k in range(bits.shape[0]):
+        _check(lib.melpe_stream_pack(_ptr(bits[k]), _ptr(votes[k:k + 1]), _ptr(last), _ptr(out),
+                                     _ptr(n), 1, None))
+        chunks.append(out[:n[0]].tobytes())
+    return b"".join(chunks)
+
+
+def stream_unpack(stream, max_sf=None):
+    """melpe_dec.c:33-49: framed bytes -> (bits nsf x 11, voiced nsf)"""
+    lib = load_library()
+    buf = np.frombuffer(bytes(stream), np.uint8)
+    max_sf = len(buf) if max_sf is None else max_sf
+    bits = np.zeros((max(max_sf, 1), SF_BYTES), np.uint8)
+    voiced = np.zeros(max(max_sf, 1), np.uint8)
+    k = lib.melpe_stream_unpack(_ptr(buf), len(buf), _ptr(bits), _ptr(voiced), max_sf)
+    if k < 0:
+        raise RuntimeError("libmelpe_amd: %s" % lib.melpe_last_error().decode())
+    return bits[:k], voiced[:k]
 
 
 class Vad:

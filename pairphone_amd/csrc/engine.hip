@@ -775,4 +775,57 @@ int melpe_tx_dev(melpe_engine *e, void *d_vad_state, void *d_bits, void *d_sp, v
 	return melpe_encode_dev(e, d_bits, d_sp, d_gate, hip_stream);
 }
 
+
+int melpe_stream_pack(const unsigned char *bits, const uint8_t *votes, uint8_t *last,
+		      unsigned char *out, uint8_t *lens, int channels, const uint8_t *active)
+{
+	if (!bits || !votes || !last || !out || !lens || channels <= 0)
+		return fail_msg("melpe_stream_pack: bad arguments");
+	for (int c = 0; c < channels; c++) {
+		const unsigned char *b = bits + (size_t) c * MELPE_SF_BYTES;
+		unsigned char *o = out + (size_t) c * MELPE_SF_BYTES;
+		if (active && !active[c]) {
+			lens[c] = 0;
+			continue;
+		}
+		if (votes[c] == 0) {	/* melpe_enc.c:57-59: VAD flag on the carried txbuf[0] */
+			last[c] |= 2;
+			o[0] = last[c];
+			lens[c] = 1;
+		} else {		/* melpe_enc.c:64-70: bytes 0 and 10 swapped */
+			memcpy(o, b, MELPE_SF_BYTES);
+			o[0] = b[10];
+			o[10] = b[0];
+			last[c] = o[0];
+			lens[c] = MELPE_SF_BYTES;
+		}
+	}
+	return 0;
+}
+
+long melpe_stream_unpack(const unsigned char *stream, long nbytes, unsigned char *bits,
+			 uint8_t *voiced, long max_sf)
+{
+	if (!stream || nbytes < 0 || !bits || !voiced || max_sf < 0)
+		return fail_msg("melpe_stream_unpack: bad arguments");
+	long pos = 0, k = 0;
+	while (pos < nbytes && k < max_sf) {	/* melpe_dec.c:33-48 */
+		unsigned char *b = bits + (size_t) k * MELPE_SF_BYTES;
+		if (stream[pos] & 2) {
+			memset(b, 0, MELPE_SF_BYTES);
+			voiced[k++] = 0;
+			pos += 1;
+			continue;
+		}
+		if (pos + MELPE_SF_BYTES > nbytes)
+			return fail_msg("melpe_stream_unpack: truncated voiced frame");
+		memcpy(b, stream + pos, MELPE_SF_BYTES);
+		b[0] = stream[pos + 10];
+		b[10] = stream[pos];
+		voiced[k++] = 1;
+		pos += MELPE_SF_BYTES;
+	}
+	return k;
+}
+
 }  // extern "C"
