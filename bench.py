@@ -285,6 +285,12 @@ def main():
             dec["roofline_frac"] = oc["W_dec_per_sf"] * C / (dec["kernel_ms"] / 1e3) / 1e12 / PEAK_VALU_TOPS
             dec["W_per_channel_superframe"] = oc["W_dec_per_sf"]
             dec["traffic"] = pmc_traffic("k_decode", C)
+    if oc and oc.get("W_vad_per_sf"):
+        vach = oc["W_vad_per_sf"] * C / (vgate["kernel_ms"] / 1e3) / 1e12
+        vgate["roofline"] = {"bound": "valu", "W_per_channel_superframe": oc["W_vad_per_sf"],
+                             "achieved": vach, "peak": PEAK_VALU_TOPS,
+                             "unit": "T basic-ops/s (INT32 VALU lane-ops)",
+                             "frac": vach / PEAK_VALU_TOPS}
     base, parity = (None, None)
     if world == 1:
         base, parity = cpu_baseline(args, bits[:W + K, :args.cpu_sample_channels].cpu().numpy())

@@ -229,6 +229,23 @@ int emu_voice_crypt(unsigned char *pkts, const uint32_t *counters, const unsigne
 	return 0;
 }
 
+#if defined(MELPE_OPCOUNT)
+uint64_t melpe_vad_ops;
+int melpe_vad_depth;
+#endif
+
+/* VAD basic-op census since the last call (count build only; else 0) */
+uint64_t emu_vad_opcount(void)
+{
+#if defined(MELPE_OPCOUNT)
+	uint64_t n = melpe_vad_ops;
+	melpe_vad_ops = 0;
+	return n;
+#else
+	return 0;
+#endif
+}
+
 int emu_vad_state_bytes(void)
 {
 	return (int) sizeof(VadState);

@@ -44,6 +44,25 @@ struct VadState {
 	int32_t LTP_flag;	/* never set on the MELPe path (LTP_flag_update is AMR-only) */
 };
 
+/* basic-op census (host count build only, tools/opcount.py): every AMR
+ * basic op entered from VAD code, nested op calls not counted (SURVEY.md
+ * §8(d) rule) */
+#if defined(MELPE_OPCOUNT) && !defined(__HIP__)
+extern "C" uint64_t melpe_vad_ops;
+extern "C" int melpe_vad_depth;
+struct VaOpScope {
+	VaOpScope()
+	{
+		if (!melpe_vad_depth++)
+			melpe_vad_ops++;
+	}
+	~VaOpScope() { melpe_vad_depth--; }
+};
+#define VA_OP() VaOpScope va_op_scope_
+#else
+#define VA_OP()
+#endif
+
 /* ---- AMR basic ops (vad/basicop2.c) ---------------------------------- */
 #define VA_MAX32 ((int32_t) 0x7fffffff)
 #define VA_MIN32 ((int32_t) 0x80000000)
@@ -56,10 +75,11 @@ VA_FN int32_t va_sat32(int64_t x)
 {
 	return x > VA_MAX32 ? VA_MAX32 : (x < VA_MIN32 ? VA_MIN32 : (int32_t) x);
 }
-VA_FN int16_t va_add(int16_t a, int16_t b) { return va_sat((int32_t) a + b); }	/* :134 */
-VA_FN int16_t va_sub(int16_t a, int16_t b) { return va_sat((int32_t) a - b); }	/* :181 */
+VA_FN int16_t va_add(int16_t a, int16_t b) { VA_OP(); return va_sat((int32_t) a + b); }	/* :134 */
+VA_FN int16_t va_sub(int16_t a, int16_t b) { VA_OP(); return va_sat((int32_t) a - b); }	/* :181 */
 VA_FN int16_t va_abs_s(int16_t a)	/* :222 */
 {
+	VA_OP();
 	return a == (int16_t) -32768 ? (int16_t) 32767 : (int16_t) (a < 0 ? -a : a);
 }
 VA_FN int16_t va_shr_pos(int16_t v, int n)	/* shr, n >= 0 (:354) */
@@ -77,34 +97,39 @@ VA_FN int16_t va_shl_pos(int16_t v, int n)	/* shl, n >= 0 (:282) */
 }
 VA_FN int16_t va_shl(int16_t v, int16_t n)
 {
+	VA_OP();
 	if (n < 0)
 		return va_shr_pos(v, n < -16 ? 16 : -n);
 	return va_shl_pos(v, n);
 }
 VA_FN int16_t va_shr(int16_t v, int16_t n)
 {
+	VA_OP();
 	if (n < 0)
 		return va_shl_pos(v, n < -16 ? 16 : -n);
 	return va_shr_pos(v, n);
 }
 VA_FN int16_t va_mult(int16_t a, int16_t b)	/* :427 */
 {
+	VA_OP();
 	return va_sat(((int32_t) a * b) >> 15);
 }
 VA_FN int16_t va_mult_r(int16_t a, int16_t b)	/* :1285 */
 {
+	VA_OP();
 	return va_sat(((int32_t) a * b + 0x4000) >> 15);
 }
 VA_FN int32_t va_L_mult(int16_t a, int16_t b)	/* :481 */
 {
+	VA_OP();
 	int32_t p = (int32_t) a * b;
 	return p == 0x40000000 ? VA_MAX32 : p * 2;
 }
-VA_FN int32_t va_L_add(int32_t a, int32_t b) { return va_sat32((int64_t) a + b); }	/* :927 */
-VA_FN int32_t va_L_sub(int32_t a, int32_t b) { return va_sat32((int64_t) a - b); }	/* :979 */
-VA_FN int32_t va_L_mac(int32_t c, int16_t a, int16_t b) { return va_L_add(c, va_L_mult(a, b)); }
-VA_FN int32_t va_L_msu(int32_t c, int16_t a, int16_t b) { return va_L_sub(c, va_L_mult(a, b)); }
-VA_FN int32_t va_L_negate(int32_t x) { return x == VA_MIN32 ? VA_MAX32 : -x; }	/* :1240 */
+VA_FN int32_t va_L_add(int32_t a, int32_t b) { VA_OP(); return va_sat32((int64_t) a + b); }	/* :927 */
+VA_FN int32_t va_L_sub(int32_t a, int32_t b) { VA_OP(); return va_sat32((int64_t) a - b); }	/* :979 */
+VA_FN int32_t va_L_mac(int32_t c, int16_t a, int16_t b) { VA_OP(); return va_L_add(c, va_L_mult(a, b)); }
+VA_FN int32_t va_L_msu(int32_t c, int16_t a, int16_t b) { VA_OP(); return va_L_sub(c, va_L_mult(a, b)); }
+VA_FN int32_t va_L_negate(int32_t x) { VA_OP(); return x == VA_MIN32 ? VA_MAX32 : -x; }	/* :1240 */
 VA_FN int32_t va_L_shr_pos(int32_t x, int n)	/* L_shr, n >= 0 (:1416) */
 {
 	return n >= 31 ? (x < 0 ? -1 : 0) : (x >> n);
@@ -121,18 +146,21 @@ VA_FN int32_t va_L_shl_pos(int32_t x, int n)
 }
 VA_FN int32_t va_L_shl(int32_t x, int16_t n)
 {
+	VA_OP();
 	if (n <= 0)
 		return va_L_shr_pos(x, n < -32 ? 32 : -n);
 	return va_L_shl_pos(x, n);
 }
 VA_FN int32_t va_L_shr(int32_t x, int16_t n)
 {
+	VA_OP();
 	if (n < 0)
 		return va_L_shl_pos(x, n < -32 ? 32 : -n);
 	return va_L_shr_pos(x, n);
 }
 VA_FN int16_t va_shr_r(int16_t v, int16_t n)	/* :1495 */
 {
+	VA_OP();
 	if (n > 15)
 		return 0;
 	int16_t r = va_shr(v, n);
@@ -142,6 +170,7 @@ VA_FN int16_t va_shr_r(int16_t v, int16_t n)	/* :1495 */
 }
 VA_FN int32_t va_L_shr_r(int32_t x, int16_t n)	/* :1764 */
 {
+	VA_OP();
 	if (n > 31)
 		return 0;
 	int32_t r = va_L_shr(x, n);
@@ -149,12 +178,13 @@ VA_FN int32_t va_L_shr_r(int32_t x, int16_t n)	/* :1764 */
 		r++;
 	return r;
 }
-VA_FN int16_t va_extract_h(int32_t x) { return (int16_t) (x >> 16); }
-VA_FN int16_t va_extract_l(int32_t x) { return (int16_t) x; }
-VA_FN int32_t va_L_deposit_h(int16_t v) { return (int32_t) ((uint32_t) (int32_t) v << 16); }
-VA_FN int16_t va_round(int32_t x) { return va_extract_h(va_L_add(x, 0x8000)); }	/* bround :652 */
+VA_FN int16_t va_extract_h(int32_t x) { VA_OP(); return (int16_t) (x >> 16); }
+VA_FN int16_t va_extract_l(int32_t x) { VA_OP(); return (int16_t) x; }
+VA_FN int32_t va_L_deposit_h(int16_t v) { VA_OP(); return (int32_t) ((uint32_t) (int32_t) v << 16); }
+VA_FN int16_t va_round(int32_t x) { VA_OP(); return va_extract_h(va_L_add(x, 0x8000)); }	/* bround :652 */
 VA_FN int16_t va_norm_s(int16_t v)	/* :1938 */
 {
+	VA_OP();
 	if (v == 0)
 		return 0;
 	if (v == -1)
@@ -164,6 +194,7 @@ VA_FN int16_t va_norm_s(int16_t v)	/* :1938 */
 }
 VA_FN int16_t va_norm_l(int32_t x)	/* :2105 */
 {
+	VA_OP();
 	if (x == 0)
 		return 0;
 	if (x == -1)
@@ -174,6 +205,7 @@ VA_FN int16_t va_norm_l(int32_t x)	/* :2105 */
 /* div_s (:2008); callers guarantee 0 < num <= den */
 VA_FN int16_t va_div_s(int16_t num, int16_t den)
 {
+	VA_OP();
 	if (num == 0)
 		return 0;
 	if (num == den)
@@ -328,10 +360,10 @@ VA_FN void va_r_fft(int16_t *x)
 				int32_t fi = va_L_mult(x[kj + 1], phs[ji]);
 				fi = va_L_mac(fi, x[kj], phs[ji + 1]);
 				int16_t t1 = va_round(fr), t2 = va_round(fi);
-				x[kj] = va_shr_pos(va_sub(x[k], t1), 1);
-				x[kj + 1] = va_shr_pos(va_sub(x[k + 1], t2), 1);
-				x[k] = va_shr_pos(va_add(x[k], t1), 1);
-				x[k + 1] = va_shr_pos(va_add(x[k + 1], t2), 1);
+				x[kj] = va_shr(va_sub(x[k], t1), 1);
+				x[kj + 1] = va_shr(va_sub(x[k + 1], t2), 1);
+				x[k] = va_shr(va_add(x[k], t1), 1);
+				x[k + 1] = va_shr(va_add(x[k + 1], t2), 1);
 			}
 			ji += ii2;
 		}
@@ -348,17 +380,17 @@ VA_FN void va_r_fft(int16_t *x)
 		int32_t L1r = va_L_deposit_h(f1r), L1i = va_L_deposit_h(f1i), L;
 		L = va_L_mac(L1r, f2r, phs[i]);
 		L = va_L_msu(L, f2i, phs[i + 1]);
-		x[i] = va_round(va_L_shr_pos(L, 1));
+		x[i] = va_round(va_L_shr(L, 1));
 		L = va_L_mac(L1i, f2i, phs[i]);
 		L = va_L_mac(L, f2r, phs[i + 1]);
-		x[i + 1] = va_round(va_L_shr_pos(L, 1));
+		x[i + 1] = va_round(va_L_shr(L, 1));
 		L = va_L_mac(L1r, f2r, phs[j]);
 		L = va_L_mac(L, f2i, phs[j + 1]);
-		x[j] = va_round(va_L_shr_pos(L, 1));
+		x[j] = va_round(va_L_shr(L, 1));
 		L = va_L_negate(L1i);
 		L = va_L_msu(L, f2i, phs[j]);
 		L = va_L_mac(L, f2r, phs[j + 1]);
-		x[j + 1] = va_round(va_L_shr_pos(L, 1));
+		x[j + 1] = va_round(va_L_shr(L, 1));
 	}
 }
 

@@ -19,6 +19,34 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def vad_census(lib, x, nsf):
+    """W of the TX VAD gate (six vad2 windows per superframe, vad.h) on the
+    same input, same counting rule over the AMR basic ops"""
+    lib.emu_vad_opcount.restype = ctypes.c_uint64
+    C = x.shape[0]
+    st = np.zeros(C * lib.emu_vad_state_bytes(), np.uint8)
+    votes = np.zeros((C, nsf), np.uint8)
+    x = np.ascontiguousarray(x, np.int16)
+    lib.emu_vad_opcount()
+    lib.emu_vad(ctypes.c_void_p(st.ctypes.data), ctypes.c_void_p(x.ctypes.data),
+                ctypes.c_void_p(votes.ctypes.data), C, nsf)
+    return {"W_vad_per_sf": float(lib.emu_vad_opcount()) / (C * nsf)}
+
+
+def vad_only(channels=32, nsf=149):
+    """refresh only W_vad_per_sf in profiles/opcount.json"""
+    from pairphone_amd.build import build_opcount
+    from pairphone_amd import synth_signal
+    import bench
+    lib = ctypes.CDLL(build_opcount())
+    x = np.stack([synth_signal(bench.RUN_SEED, c, nsf * 540) for c in range(channels)])
+    path = os.path.join(ROOT, "profiles", "opcount.json")
+    res = json.load(open(path))
+    res.update(vad_census(lib, x, nsf))
+    json.dump(res, open(path, "w"), indent=1)
+    print("W_vad %.0f ops/superframe" % res["W_vad_per_sf"])
+
+
 def main(channels=32, nsf=149):
     from pairphone_amd.build import build_opcount
     from pairphone_amd import synth_signal
@@ -69,10 +97,14 @@ def main(channels=32, nsf=149):
         "enc_by_op": {names[i]: float(enc[i]) / n for i in np.argsort(-enc.astype(np.float64))[:len(names)] if enc[i]},
         "dec_by_op": {names[i]: float(dec[i]) / n for i in np.argsort(-dec.astype(np.float64))[:len(names)] if dec[i]},
     }
+    res.update(vad_census(lib, x, nsf))
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     json.dump(res, open(os.path.join(ROOT, "profiles", "opcount.json"), "w"), indent=1)
     print("W_enc %.0f  W_dec %.0f ops/superframe" % (res["W_enc_per_sf"], res["W_dec_per_sf"]))
 
 
 if __name__ == "__main__":
-    main(*[int(a) for a in sys.argv[1:]])
+    if sys.argv[1:2] == ["--vad"]:
+        vad_only(*[int(a) for a in sys.argv[2:]])
+    else:
+        main(*[int(a) for a in sys.argv[1:]])
