@@ -9,6 +9,14 @@
  * active channel, exactly as melpe_a / melpe_s (melpe/melpe.c:91-107) would
  * in that channel's own process.
  *
+ * Process semantics: a channel's encoder and decoder do NOT share
+ * melp_par / quant_par / chbuf (the reference process shares them,
+ * melpe/global.c:28-37).  A batched channel therefore behaves as the
+ * standalone melpe_enc (encode-only process) and melpe_dec (decode-only
+ * process) do.  PairPhone's duplex pp, which runs melpe_a and melpe_s in one
+ * process, is reproduced by the single-stream drop-in (melpe.h), not by an
+ * engine channel that interleaves encode and decode.
+ *
  * Buffers: PCM is channel-major, C x 540 int16 (sample s of channel c at
  * [c*540 + s]); bitstreams are C x 11 bytes.  The *_host calls take host
  * pointers and copy; the *_dev calls take device pointers (e.g. from torch)
@@ -18,6 +26,13 @@
  *
  * All functions return 0 on success and a negative code on error;
  * melpe_last_error() describes the last error of the calling thread.
+ *
+ * Ordering: the *_dev calls are ordered by their stream only.  The *_host
+ * calls, melpe_engine_reset and the state export/import synchronise the
+ * device first, so they run after every *_dev call already enqueued on any
+ * stream.  To reset channels in stream order (no host sync), use
+ * melpe_engine_reset_dev on the stream that carries the encode/decode work.
+ * Entry points restore the calling thread's current HIP device on return.
  */
 #ifndef MELPE_AMD_BATCH_H
 #define MELPE_AMD_BATCH_H
@@ -42,6 +57,20 @@ int melpe_engine_channels(const melpe_engine *e);
 /* fresh-process state for the channels selected by `mask` (NULL = all);
  * which: 1 = encoder (incl. NPP), 2 = decoder, 3 = both */
 int melpe_engine_reset(melpe_engine *e, const uint8_t *mask_host, int which);
+/* the same, enqueued on `hip_stream` (d_mask: device C-byte mask or NULL) */
+int melpe_engine_reset_dev(melpe_engine *e, const void *d_mask, int which, void *hip_stream);
+
+/* Per-channel state records, for checkpoint / resume and for moving channels
+ * between engines or GPUs (e.g. re-balancing ragged streams).  which: 1 =
+ * encoder (EncState), 2 = decoder (DecState).  melpe_engine_state_bytes gives
+ * the record size; export copies records [first, first+count) to host memory
+ * (count * bytes), import writes them back into any engine of the same
+ * library build.  A record is opaque and carries a channel's complete codec
+ * state: continuing an imported channel gives the bits / PCM the exporting
+ * engine would have produced. */
+long melpe_engine_state_bytes(int which);
+int melpe_engine_export(melpe_engine *e, int which, int first, int count, void *host_out);
+int melpe_engine_import(melpe_engine *e, int which, int first, int count, const void *host_in);
 
 /* melpe_a on every active channel: sp (C x 540, in/out: overwritten with the
  * NPP output), bits (C x 11, out) */
@@ -148,6 +177,14 @@ int melpe_stream_pack(const unsigned char *bits, const uint8_t *votes, uint8_t *
 long melpe_stream_unpack(const unsigned char *stream, long nbytes, unsigned char *bits,
 			 uint8_t *voiced, long max_sf);
 const char *melpe_last_error(void);
+
+/* Device basic-op self-test: out[i] = op(a[i], b[i], c[i]) evaluated by the
+ * device build of the saturating basic operators, op ids of
+ * pairphone_amd/csrc/ops_eval.h (a int64, b and c int32 or NULL, out int64,
+ * all device pointers).  tests/test_device_ops.py compares it with the
+ * reference's operators. */
+int melpe_ops_eval_dev(int op, const void *d_a, const void *d_b, const void *d_c, void *d_out,
+		       long n, void *hip_stream);
 
 /* Diagnostics: per-stage wave-cycle totals of a profiling build
  * (libmelpe_amd_prof.so, -DMELPE_PROF; tools/stage_prof.py), read and

@@ -121,9 +121,36 @@ def build_opcount(force=False):
     return out
 
 
+DROPIN = os.path.join(ROOT, "build", "dropin")
+
+
+def build_dropin(force=False):
+    """The reference's own callers of melpe.h -- melpe/encoder.c,
+    melpe/decoder.c and melpe_dec.c, compiled unchanged where they lie --
+    linked against libmelpe_amd.so instead of the reference's libmelpe.a
+    (INTEGRATION.md §1).  Test infrastructure: tests/test_dropin.py runs them
+    on the GPU box.  Only where the reference sources exist; the binaries
+    travel with the tree."""
+    if not os.path.isdir(REF):
+        return
+    os.makedirs(DROPIN, exist_ok=True)
+    srcs = {"encoder": os.path.join(REF, "encoder.c"), "decoder": os.path.join(REF, "decoder.c"),
+            "melpe_dec": os.path.join(os.path.dirname(REF), "melpe_dec.c")}
+    for name, src in srcs.items():
+        out = os.path.join(DROPIN, name)
+        if not force and not _newer(out, [src, LIB]):
+            continue
+        # -include: our include/melpe.h is seen first; the reference header the
+        # source includes itself then only repeats the same prototypes
+        _run(["gcc", "-O2", "-w", "-include", os.path.join(ROOT, "include", "melpe.h"), src,
+              "-L" + os.path.dirname(LIB), "-lmelpe_amd", "-Wl,-rpath-link,/opt/rocm/lib",
+              "-Wl,-rpath,$ORIGIN/../../pairphone_amd", "-o", out])
+
+
 def build_all(force=False):
     build_oracle()
     build_engine(force)
+    build_dropin(force)
     if os.path.exists(os.path.join(CSRC, "hostemu.cpp")):
         build_hostemu(force)
 

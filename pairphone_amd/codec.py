@@ -37,6 +37,11 @@ def load_library(path=None):
         "melpe_engine_destroy": (i32, [vp]),
         "melpe_engine_channels": (i32, [vp]),
         "melpe_engine_reset": (i32, [vp, vp, i32]),
+        "melpe_engine_reset_dev": (i32, [vp, vp, i32, vp]),
+        "melpe_engine_state_bytes": (ctypes.c_long, [i32]),
+        "melpe_engine_export": (i32, [vp, i32, i32, i32, vp]),
+        "melpe_engine_import": (i32, [vp, i32, i32, i32, vp]),
+        "melpe_ops_eval_dev": (i32, [i32, vp, vp, vp, vp, ctypes.c_long, vp]),
         "melpe_encode_host": (i32, [vp, vp, vp, vp]),
         "melpe_encode_dev": (i32, [vp, vp, vp, vp, vp]),
         "melpe_encode_npp_dev": (i32, [vp, vp, vp, vp]),
@@ -197,6 +202,24 @@ class MelpeEngine:
     def reset(self, mask=None, which=3):
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
         _check(self.lib.melpe_engine_reset(self.h, _ptr(m), which))
+
+    def reset_dev(self, d_mask=None, which=3, stream=None):
+        """reset enqueued on `stream` (ordered with the *_dev calls on it)"""
+        _check(self.lib.melpe_engine_reset_dev(self.h, d_mask, which, stream))
+
+    def export_state(self, which, first=0, count=None):
+        """channel records [first, first+count) as a uint8 [count, bytes]
+        array (which: 1 encoder, 2 decoder)"""
+        count = self.channels - first if count is None else count
+        rec = self.lib.melpe_engine_state_bytes(which)
+        out = np.zeros((count, rec), np.uint8)
+        _check(self.lib.melpe_engine_export(self.h, which, first, count, _ptr(out)))
+        return out
+
+    def import_state(self, which, records, first=0):
+        rec = np.ascontiguousarray(records, np.uint8)
+        assert rec.ndim == 2 and rec.shape[1] == self.lib.melpe_engine_state_bytes(which)
+        _check(self.lib.melpe_engine_import(self.h, which, first, rec.shape[0], _ptr(rec)))
 
     def _mask(self, active):
         if active is None:

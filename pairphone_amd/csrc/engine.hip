@@ -26,6 +26,7 @@
 #include "synth.h"
 #include "voice_crypt.h"
 #include "vad.h"
+#include "ops_eval.h"
 #include "../../include/melpe.h"
 #include "../../include/melpe_batch.h"
 
@@ -189,6 +190,26 @@ __global__ __launch_bounds__(WAVE) void k_vad_reset(VadState *st, const uint8_t 
 	st[c] = z;
 }
 
+/* device basic-op parity test: out[i] = op(a[i], b[i], c[i]) with the
+ * device build of ops.h (ops_eval.h) */
+__global__ __launch_bounds__(256) void k_ops_eval(int op, const int64_t *A, const int32_t *B,
+						  const int32_t *C, int64_t *out, long n)
+{
+	long i = blockIdx.x * (long) blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	int64_t a = A[i];
+	int32_t b = B ? B[i] : 0, c = C ? C[i] : 0;
+	int64_t r = 0;
+	switch (op) {
+#define OPS_CASE(id, name, call) case id: r = (int64_t) (call); break;
+	MELPE_OPS_EVAL_LIST(OPS_CASE)
+#undef OPS_CASE
+	default: r = 0;
+	}
+	out[i] = r;
+}
+
 /* ------------------------------------------------------------------ */
 /* host side                                                          */
 /* ------------------------------------------------------------------ */
@@ -209,6 +230,55 @@ static int fail_msg(const std::string &m)
 
 #define HIPCHK(expr) do { hipError_t _e = (expr); if (_e != hipSuccess) return fail(#expr, _e); } while (0)
 
+/* Every entry point that selects a device restores the caller's current
+ * device on return, so a multi-GPU host process (or torch's default device)
+ * never sees its current device move under it. */
+struct DevGuard {
+	int prev = -1;
+	hipError_t err = hipSuccess;
+	explicit DevGuard(int dev)
+	{
+		int cur = -1;
+		if (hipGetDevice(&cur) == hipSuccess && cur == dev)
+			return;
+		err = hipSetDevice(dev);
+		prev = cur;
+	}
+	~DevGuard()
+	{
+		if (prev >= 0)
+			hipSetDevice(prev);
+	}
+};
+#define DEVGUARD(dev) DevGuard _dg(dev); HIPCHK(_dg.err)
+
+/* device staging of the engine-less *_host calls (VAD, voice crypt): one
+ * buffer per device, grown on demand and kept, instead of a hipMalloc /
+ * hipFree pair per call */
+struct HostStage {
+	std::mutex mu;
+	void *p = nullptr;
+	size_t n = 0;
+};
+static HostStage g_stage[64];
+
+static int stage_get(int dev, size_t bytes, void **out)
+{
+	if (dev < 0 || dev >= 64)
+		return fail_msg("bad device index");
+	HostStage &h = g_stage[dev];
+	if (h.n < bytes) {
+		if (h.p)
+			HIPCHK(hipFree(h.p));
+		h.p = nullptr;
+		h.n = 0;
+		HIPCHK(hipMalloc(&h.p, bytes));
+		h.n = bytes;
+	}
+	*out = h.p;
+	return 0;
+}
+
 struct melpe_engine {
 	int device = 0;
 	int channels = 0;
@@ -220,6 +290,8 @@ struct melpe_engine {
 	int16_t *d_pcm = nullptr;	/* staging for *_host calls */
 	unsigned char *d_bits = nullptr;
 	uint8_t *d_mask = nullptr;
+	int16_t *d_npp = nullptr;	/* staging of melpe_npp_host, grown on demand */
+	size_t npp_bytes = 0;
 	float last_ms = 0.f;
 };
 
@@ -236,7 +308,7 @@ static int ensure_device_tables(int dev)
 	size_t bytes = (size_t) (melpe_tables_blob_end - melpe_tables_blob);
 	if (bytes != sizeof(int16_t) * MELPE_TABLE_WORDS)
 		return fail_msg("embedded table blob has the wrong size");
-	HIPCHK(hipSetDevice(dev));
+	DEVGUARD(dev);
 	int (*up[])(const void *, size_t) = {melpe_tu_eng_upload, melpe_tu_npp_upload,
 					     melpe_tu_ana_upload, melpe_tu_dec_upload};
 	for (auto f : up)
@@ -280,30 +352,47 @@ int melpe_engine_create(melpe_engine **out, int device, int channels)
 	int rc = ensure_device_tables(device);
 	if (rc)
 		return rc;
+	DEVGUARD(device);
 	melpe_engine *e = new melpe_engine();
 	e->device = device;
 	e->channels = channels;
-	HIPCHK(hipSetDevice(device));
-	HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-	HIPCHK(hipEventCreate(&e->ev0));
-	HIPCHK(hipEventCreate(&e->ev1));
-	HIPCHK(hipMalloc(&e->d_enc, sizeof(EncState) * (size_t) channels));
-	HIPCHK(hipMalloc(&e->d_dec, sizeof(DecState) * (size_t) channels));
-	HIPCHK(hipMalloc(&e->d_syn, sizeof(synth_state) * (size_t) channels));
-	HIPCHK(hipMalloc(&e->d_pcm, sizeof(int16_t) * MELPE_SF_SAMPLES * (size_t) channels));
-	HIPCHK(hipMalloc(&e->d_bits, (size_t) MELPE_SF_BYTES * channels));
-	HIPCHK(hipMalloc(&e->d_mask, (size_t) channels));
+	hipError_t er = hipSuccess;
+	const char *what = nullptr;
+#define CREATE_STEP(expr) if (er == hipSuccess && (er = (expr)) != hipSuccess) what = #expr
+	CREATE_STEP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+	CREATE_STEP(hipEventCreate(&e->ev0));
+	CREATE_STEP(hipEventCreate(&e->ev1));
+	CREATE_STEP(hipMalloc(&e->d_enc, sizeof(EncState) * (size_t) channels));
+	CREATE_STEP(hipMalloc(&e->d_dec, sizeof(DecState) * (size_t) channels));
+	CREATE_STEP(hipMalloc(&e->d_syn, sizeof(synth_state) * (size_t) channels));
+	CREATE_STEP(hipMalloc(&e->d_pcm, sizeof(int16_t) * MELPE_SF_SAMPLES * (size_t) channels));
+	CREATE_STEP(hipMalloc(&e->d_bits, (size_t) MELPE_SF_BYTES * channels));
+	CREATE_STEP(hipMalloc(&e->d_mask, (size_t) channels));
+#undef CREATE_STEP
+	if (er != hipSuccess) {
+		int r = fail(what, er);
+		melpe_engine_destroy(e);	/* frees whatever was allocated */
+		return r;
+	}
+	int r = melpe_engine_reset(e, nullptr, 3);
+	if (r) {
+		std::string m = g_err;
+		melpe_engine_destroy(e);
+		g_err = m;
+		return r;
+	}
 	*out = e;
-	return melpe_engine_reset(e, nullptr, 3);
+	return 0;
 }
 
 int melpe_engine_destroy(melpe_engine *e)
 {
 	if (!e)
 		return 0;
-	hipSetDevice(e->device);
+	DevGuard dg(e->device);
 	if (e->stream)
 		hipStreamSynchronize(e->stream);
+	hipFree(e->d_npp);
 	hipFree(e->d_enc);
 	hipFree(e->d_dec);
 	hipFree(e->d_syn);
@@ -337,11 +426,25 @@ static const uint8_t *stage_mask(melpe_engine *e, const uint8_t *mask_host, int 
 	return e->d_mask;
 }
 
+int melpe_engine_reset_dev(melpe_engine *e, const void *d_mask, int which, void *hip_stream)
+{
+	if (!e || which < 1 || which > 3)
+		return fail_msg("melpe_engine_reset_dev: bad arguments");
+	DEVGUARD(e->device);
+	k_reset<<<grid_for(e->channels), WAVE, 0, (hipStream_t) hip_stream>>>(
+		e->d_enc, e->d_dec, (const uint8_t *) d_mask, e->channels, which);
+	HIPCHK(hipGetLastError());
+	return 0;
+}
+
 int melpe_engine_reset(melpe_engine *e, const uint8_t *mask_host, int which)
 {
-	if (!e)
-		return fail_msg("null engine");
-	HIPCHK(hipSetDevice(e->device));
+	if (!e || which < 1 || which > 3)
+		return fail_msg("melpe_engine_reset: bad arguments");
+	DEVGUARD(e->device);
+	/* ordered after every *_dev call already enqueued on any stream of the
+	 * device: those read and write the same channel records */
+	HIPCHK(hipDeviceSynchronize());
 	int rc;
 	const uint8_t *m = stage_mask(e, mask_host, &rc);
 	if (rc)
@@ -358,7 +461,7 @@ static int npp_launch(melpe_engine *e, int16_t *d_sp, int frames, int stride,
 {
 	if (frames <= 0 || stride < frames * MELPE_FRAME_SAMPLES)
 		return fail_msg("melpe_npp: bad frames/stride");
-	HIPCHK(hipSetDevice(e->device));
+	DEVGUARD(e->device);
 	ev_begin(e, s);
 	HIPCHK((hipError_t) kl_npp(e->d_enc, d_sp, frames, stride, d_act, e->channels, rate1200, s));
 	ev_end(e, s, sync);
@@ -376,12 +479,19 @@ int melpe_npp_dev(melpe_engine *e, void *d_sp, int frames, int stride, const voi
 
 int melpe_npp_host(melpe_engine *e, int16_t *sp, int frames, int stride, const uint8_t *active)
 {
-	if (!e || !sp)
-		return fail_msg("melpe_npp_host: null argument");
-	HIPCHK(hipSetDevice(e->device));
+	if (!e || !sp || stride <= 0)
+		return fail_msg("melpe_npp_host: bad arguments");
+	DEVGUARD(e->device);
+	HIPCHK(hipDeviceSynchronize());
 	size_t bytes = sizeof(int16_t) * (size_t) stride * e->channels;
-	int16_t *d = nullptr;
-	HIPCHK(hipMalloc(&d, bytes));
+	if (e->npp_bytes < bytes) {
+		HIPCHK(hipFree(e->d_npp));
+		e->d_npp = nullptr;
+		e->npp_bytes = 0;
+		HIPCHK(hipMalloc(&e->d_npp, bytes));
+		e->npp_bytes = bytes;
+	}
+	int16_t *d = e->d_npp;
 	int rc;
 	const uint8_t *m = stage_mask(e, active, &rc);
 	if (!rc) {
@@ -395,14 +505,13 @@ int melpe_npp_host(melpe_engine *e, int16_t *sp, int frames, int stride, const u
 				rc = fail("npp copy back", er);
 		}
 	}
-	hipFree(d);
 	return rc;
 }
 
 static int encode_launch(melpe_engine *e, unsigned char *d_bits, int16_t *d_sp,
 			 const uint8_t *d_act, hipStream_t s, bool sync)
 {
-	HIPCHK(hipSetDevice(e->device));
+	DEVGUARD(e->device);
 	ev_begin(e, s);
 	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, d_sp, d_act, e->channels, s));
 	HIPCHK((hipError_t) kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, s));
@@ -423,7 +532,7 @@ int melpe_encode_npp_dev(melpe_engine *e, void *d_sp, const void *d_active, void
 {
 	if (!e || !d_sp)
 		return fail_msg("melpe_encode_npp_dev: null argument");
-	HIPCHK(hipSetDevice(e->device));
+	DEVGUARD(e->device);
 	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, (int16_t *) d_sp, (const uint8_t *) d_active,
 				       e->channels, (hipStream_t) hip_stream));
 	return 0;
@@ -434,7 +543,7 @@ int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const 
 {
 	if (!e || !d_bits || !d_sp)
 		return fail_msg("melpe_encode_ana_dev: null argument");
-	HIPCHK(hipSetDevice(e->device));
+	DEVGUARD(e->device);
 	HIPCHK((hipError_t) kl_enc_ana(e->d_enc, (const int16_t *) d_sp, (uint8_t *) d_bits,
 				       (const uint8_t *) d_active, e->channels,
 				       (hipStream_t) hip_stream));
@@ -445,7 +554,8 @@ int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const u
 {
 	if (!e || !bits || !sp)
 		return fail_msg("melpe_encode_host: null argument");
-	HIPCHK(hipSetDevice(e->device));
+	DEVGUARD(e->device);
+	HIPCHK(hipDeviceSynchronize());
 	size_t pb = sizeof(int16_t) * BLOCK * (size_t) e->channels;
 	size_t bb = (size_t) 11 * e->channels;
 	int rc;
@@ -467,7 +577,7 @@ int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const u
 static int decode_launch(melpe_engine *e, int16_t *d_sp, const unsigned char *d_bits,
 			 const uint8_t *d_act, hipStream_t s, bool sync)
 {
-	HIPCHK(hipSetDevice(e->device));
+	DEVGUARD(e->device);
 	ev_begin(e, s);
 	HIPCHK((hipError_t) kl_decode(e->d_dec, d_sp, d_bits, d_act, e->channels, s));
 	ev_end(e, s, sync);
@@ -488,7 +598,8 @@ int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
 {
 	if (!e || !bits || !sp)
 		return fail_msg("melpe_decode_host: null argument");
-	HIPCHK(hipSetDevice(e->device));
+	DEVGUARD(e->device);
+	HIPCHK(hipDeviceSynchronize());
 	size_t pb = sizeof(int16_t) * BLOCK * (size_t) e->channels;
 	size_t bb = (size_t) 11 * e->channels;
 	int rc;
@@ -506,11 +617,56 @@ int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
 	return 0;
 }
 
+/* per-channel state records (checkpoint / migration between engines) */
+static int state_geom(melpe_engine *e, int which, int first, int count, size_t *rec,
+		      char **base)
+{
+	if (!e || (which != 1 && which != 2) || first < 0 || count < 0 ||
+	    first + (long) count > e->channels)
+		return fail_msg("melpe_engine_state: bad arguments");
+	*rec = which == 1 ? sizeof(EncState) : sizeof(DecState);
+	*base = which == 1 ? (char *) e->d_enc : (char *) e->d_dec;
+	return 0;
+}
+
+long melpe_engine_state_bytes(int which)
+{
+	return which == 1 ? (long) sizeof(EncState) : which == 2 ? (long) sizeof(DecState) : -1;
+}
+
+int melpe_engine_export(melpe_engine *e, int which, int first, int count, void *host_out)
+{
+	size_t rec;
+	char *base;
+	if (int r = state_geom(e, which, first, count, &rec, &base))
+		return r;
+	if (!host_out && count)
+		return fail_msg("melpe_engine_export: null buffer");
+	DEVGUARD(e->device);
+	HIPCHK(hipDeviceSynchronize());
+	HIPCHK(hipMemcpy(host_out, base + rec * first, rec * count, hipMemcpyDeviceToHost));
+	return 0;
+}
+
+int melpe_engine_import(melpe_engine *e, int which, int first, int count, const void *host_in)
+{
+	size_t rec;
+	char *base;
+	if (int r = state_geom(e, which, first, count, &rec, &base))
+		return r;
+	if (!host_in && count)
+		return fail_msg("melpe_engine_import: null buffer");
+	DEVGUARD(e->device);
+	HIPCHK(hipDeviceSynchronize());
+	HIPCHK(hipMemcpy(base + rec * first, host_in, rec * count, hipMemcpyHostToDevice));
+	return 0;
+}
+
 int melpe_synth_seed(melpe_engine *e, uint32_t run_seed, uint32_t first_channel)
 {
 	if (!e)
 		return fail_msg("null engine");
-	HIPCHK(hipSetDevice(e->device));
+	DEVGUARD(e->device);
 	k_synth_seed<<<grid_for(e->channels), WAVE, 0, e->stream>>>(e->d_syn, run_seed,
 								      first_channel, e->channels);
 	HIPCHK(hipGetLastError());
@@ -522,7 +678,7 @@ int melpe_synth_dev(melpe_engine *e, void *d_sp, int samples, void *hip_stream)
 {
 	if (!e || !d_sp || samples <= 0)
 		return fail_msg("melpe_synth_dev: bad arguments");
-	HIPCHK(hipSetDevice(e->device));
+	DEVGUARD(e->device);
 	k_synth<<<grid_for(e->channels), WAVE, 0, (hipStream_t) hip_stream>>>(
 		e->d_syn, (int16_t *) d_sp, samples, e->channels);
 	HIPCHK(hipGetLastError());
@@ -539,7 +695,9 @@ int melpe_synth_host(uint32_t run_seed, uint32_t channel, int16_t *out, int samp
 
 int melpe_debug_encode_stage(melpe_engine *e, void *d_sp, int upto)
 {
-	HIPCHK(hipSetDevice(e->device));
+	if (!e || !d_sp)
+		return fail_msg("melpe_debug_encode_stage: null argument");
+	DEVGUARD(e->device);
 	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, (int16_t *) d_sp, nullptr, e->channels, e->stream));
 	if (upto > 0)
 		HIPCHK((hipError_t) kl_enc_ana_dbg(e->d_enc, (int16_t *) d_sp, e->channels, upto,
@@ -580,6 +738,7 @@ double melpe_last_kernel_ms(const melpe_engine *ce)
 
 static melpe_engine *g_single = nullptr;
 static bool g_single_rate1200 = false;	/* melpe_i sets rate = RATE1200 */
+static bool g_single_npp_started = false;	/* npp's static first_time has fired */
 
 static melpe_engine *single_engine(void)
 {
@@ -595,29 +754,34 @@ static melpe_engine *single_engine(void)
 void melpe_n(short *sp)
 {
 	melpe_engine *e = single_engine();
-	int16_t buf[256];
-	/* the first call reads 256 samples (melpe/npp.c:178-179) */
-	memcpy(buf, sp, sizeof(int16_t) * 180);
-	memcpy(buf + 180, sp + 180, sizeof(int16_t) * 76);
+	DevGuard dg(e->device);
+	/* npp reads 256 samples only on its very first call (from melpe_n or
+	 * melpe_a) and only when rate == RATE1200 (melpe/npp.c:176-179);
+	 * every other call reads the caller's 180 */
+	size_t n = (!g_single_npp_started && g_single_rate1200) ? 256 : 180;
 	int16_t *d = e->d_pcm;
-	if (hipMemcpy(d, buf, sizeof(buf), hipMemcpyHostToDevice) != hipSuccess ||
+	if (dg.err != hipSuccess ||
+	    hipMemcpy(d, sp, sizeof(int16_t) * n, hipMemcpyHostToDevice) != hipSuccess ||
 	    npp_launch(e, d, 1, 256, nullptr, e->stream, true, g_single_rate1200 ? 1 : 0) ||
 	    hipMemcpy(sp, d, sizeof(int16_t) * 180, hipMemcpyDeviceToHost) != hipSuccess) {
 		fprintf(stderr, "libmelpe_amd: melpe_n failed: %s\n", g_err.c_str());
 		abort();
 	}
+	g_single_npp_started = true;
 }
 
 int melpe_single_reset(void)
 {
 	melpe_engine *e = single_engine();
 	g_single_rate1200 = false;
+	g_single_npp_started = false;
 	return melpe_engine_reset(e, nullptr, 3);
 }
 
 void melpe_i(void)
 {
 	melpe_engine *e = single_engine();
+	DevGuard dg(e->device);
 	k_melpe_i<<<1, WAVE, 0, e->stream>>>(e->d_enc, e->d_dec);
 	if (hipGetLastError() != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess) {
 		fprintf(stderr, "libmelpe_amd: melpe_i failed\n");
@@ -633,11 +797,13 @@ void melpe_a(unsigned char *buf, short *sp)
 		fprintf(stderr, "libmelpe_amd: melpe_a failed: %s\n", g_err.c_str());
 		abort();
 	}
+	g_single_npp_started = true;
 }
 
 void melpe_s(short *sp, unsigned char *buf)
 {
 	melpe_engine *e = single_engine();
+	DevGuard dg(e->device);
 	k_share_params<<<1, WAVE, 0, e->stream>>>(e->d_enc, e->d_dec, 0);
 	int rc = hipGetLastError() != hipSuccess;
 	if (!rc)
@@ -652,6 +818,19 @@ void melpe_s(short *sp, unsigned char *buf)
 	}
 }
 
+
+int melpe_ops_eval_dev(int op, const void *d_a, const void *d_b, const void *d_c, void *d_out,
+		       long n, void *hip_stream)
+{
+	if (op < 0 || op >= MELPE_OPS_EVAL_COUNT || !d_a || !d_out || n <= 0 ||
+	    (n + 255) / 256 > 0x7fffffffL)
+		return fail_msg("melpe_ops_eval_dev: bad arguments");
+	k_ops_eval<<<(unsigned) ((n + 255) / 256), 256, 0, (hipStream_t) hip_stream>>>(
+		op, (const int64_t *) d_a, (const int32_t *) d_b, (const int32_t *) d_c,
+		(int64_t *) d_out, n);
+	HIPCHK(hipGetLastError());
+	return 0;
+}
 
 int melpe_voice_crypt_dev(void *d_pkts, const void *d_counters, const void *d_keys,
 			  const void *d_invert, int channels, int packets, int dir,
@@ -682,8 +861,12 @@ int melpe_voice_crypt_host(unsigned char *pkts, const uint32_t *counters,
 		return fail_msg("melpe_voice_crypt_host: bad arguments");
 	size_t pb = (size_t) channels * packets * VC_PKT_BYTES;
 	size_t kb = (size_t) channels * VC_KEY_BYTES, cb = (size_t) channels * 4;
+	int dev = 0;
+	HIPCHK(hipGetDevice(&dev));
+	std::lock_guard<std::mutex> lk(g_stage[dev & 63].mu);
 	unsigned char *d = nullptr;
-	HIPCHK(hipMalloc(&d, kb + cb + channels + pb));
+	if (int r = stage_get(dev, kb + cb + channels + pb, (void **) &d))
+		return r;
 	unsigned char *dk = d, *dc = d + kb, *di = dc + cb, *dp = di + channels;
 	int rc = 0;
 	hipError_t he;
@@ -697,7 +880,6 @@ int melpe_voice_crypt_host(unsigned char *pkts, const uint32_t *counters,
 					   dir, nullptr);
 	if (!rc && (he = hipMemcpy(pkts, dp, pb, hipMemcpyDeviceToHost)) != hipSuccess)
 		rc = fail("melpe_voice_crypt_host: download", he);
-	hipFree(d);
 	return rc;
 }
 
@@ -740,8 +922,12 @@ int melpe_vad_host(unsigned char *state, const int16_t *sp, uint8_t *votes, int 
 		return fail_msg("melpe_vad_host: bad arguments");
 	size_t sb = sizeof(VadState) * (size_t) channels;
 	size_t pb = sizeof(int16_t) * MELPE_SF_SAMPLES * (size_t) channels;
+	int dev = 0;
+	HIPCHK(hipGetDevice(&dev));
+	std::lock_guard<std::mutex> lk(g_stage[dev & 63].mu);
 	unsigned char *d = nullptr;
-	HIPCHK(hipMalloc(&d, sb + pb + 2 * (size_t) channels));
+	if (int r = stage_get(dev, sb + pb + 2 * (size_t) channels, (void **) &d))
+		return r;
 	unsigned char *ds = d, *dp = d + sb, *dv = dp + pb, *da = dv + channels;
 	int rc = 0;
 	hipError_t he;
@@ -755,7 +941,6 @@ int melpe_vad_host(unsigned char *state, const int16_t *sp, uint8_t *votes, int 
 	if (!rc && ((he = hipMemcpy(state, ds, sb, hipMemcpyDeviceToHost)) != hipSuccess ||
 		    (he = hipMemcpy(votes, dv, channels, hipMemcpyDeviceToHost)) != hipSuccess))
 		rc = fail("melpe_vad_host: download", he);
-	hipFree(d);
 	return rc;
 }
 
@@ -767,7 +952,7 @@ int melpe_tx_dev(melpe_engine *e, void *d_vad_state, void *d_bits, void *d_sp, v
 		return fail_msg("melpe_tx_dev: bad arguments");
 	if ((uintptr_t) d_vad_state & 3)
 		return fail_msg("melpe_tx_dev: state must be 4-byte aligned");
-	HIPCHK(hipSetDevice(e->device));
+	DEVGUARD(e->device);
 	k_vad<<<grid_for(e->channels), WAVE, 0, (hipStream_t) hip_stream>>>(
 		(VadState *) d_vad_state, (const int16_t *) d_sp, (uint8_t *) d_votes,
 		(uint8_t *) d_gate, (const uint8_t *) d_active, e->channels);
