@@ -1,40 +1,51 @@
 #!/usr/bin/env python3
 """Benchmark: MELPe-1200 channel-seconds encoded per second on MI355X.
 
-Workload (BASELINE.json config 4 at N=1): 262,144 independent 8 kHz channels
-per GPU, each step = one melpe_a superframe (540 samples -> 81 bits) of every
-channel, i.e. 262,144 x 67.5 ms = 17,694 channel-seconds of audio per GPU per
-step.  Channels are sharded statically across ranks (rank r owns channels
-[r*C, (r+1)*C)) with no collective on the data path: weak scaling.
+Headline (BASELINE.json metric, config 4 at N=1): every step is one melpe_a
+superframe (540 samples -> 81 bits) of each of C channels per GPU (default
+262,144 = 17,694 channel-seconds of audio per GPU per step); channels are
+sharded statically across ranks (rank r owns channels [r*C, (r+1)*C)) with no
+collective on the data path: "scaling": "weak".  Beside it, the strong-
+scaling leg of config 4 as BASELINE states it: --total-channels (262,144)
+split across the N ranks with channel_range (32,768 per GPU at N=8).
 
 Inputs: the integer speech-like generator (pairphone_amd/csrc/synth.h) run on
 the device before the timed region, so every step's PCM is resident in HBM;
-bitstreams stay on the device.  The decode leg (melpe_s of the bits just
-produced) is timed the same way and reported beside the headline.
+bitstreams stay on the device until one all_gather after the timed region.
+The decode leg (melpe_s of the bits just produced), the TX front end (VAD
+gate + melpe_a on ragged streams, config 5), the voice-frame crypt and the
+VAD alone are timed the same way and reported beside the headline.
 
 A step is two kernels on one stream: k_enc_npp (noise pre-processor, one
-wavefront per channel) then k_enc_ana (analysis + packing, one lane per
-channel); both are timed with HIP events around each launch.
+wavefront per channel) then k_enc_ana (analysis + packing); each launch is
+bracketed by HIP events on that stream.
 
 Roofline: the codec is bit-exact saturating int16/int32 arithmetic with
 serial recursions per channel, so it is bounded by INT VALU issue, not HBM
 and not MFMA.  For the dominant kernel (k_enc_ana) achieved =
-W_ana (the reference's basic ops per channel-superframe of the analysis,
-profiles/opcount.json, counted by tools/opcount.py on this same input) x
-channels / its average launch duration; peak = 256 CUs x 4 SIMDs x 32
-lanes/clk x 2.4 GHz = 78.6 T lane-ops/s.  traffic = HBM bytes per launch
-from the committed rocprofv3 --pmc passes at this channel count.
+W_ana x channels / its average launch duration, W_ana = the reference's basic
+ops per channel-superframe of the analysis averaged over exactly the
+superframes this run times (profiles/opcount.json W_enc_ana_by_sf, counted by
+tools/opcount.py on this same input); peak = 256 CUs x 4 SIMDs x 32
+lanes/clk x 2.4 GHz = 78.6 T lane-ops/s.  traffic = HBM bytes per launch from
+the committed rocprofv3 --pmc passes at this channel count
+(profiles/pmc_latest.json, which names its source file).
 
-cpu_baseline: the reference codec itself (oracle/_ref/ref_tool, compiled
-from /root/reference by oracle/Makefile), one process per core on a bounded
-sample of the same channels; its bitstreams double as a parity spot check of
-the timed GPU output.
+cpu_baseline: the reference codec itself (oracle/_ref/ref_tool, compiled from
+/root/reference by oracle/Makefile), one single-channel process per core on a
+bounded sample of the same channels; its bitstreams double as a parity spot
+check of the timed GPU output.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C]
+                  [--total-channels T]
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N
+rank processes itself (before touching the GPU); under torch.distributed.run
+it is one of them.
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import tempfile
@@ -55,26 +66,184 @@ PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12     # INT32 lane-ops/s, T
 # 24 rot, chi 75 (not, and, xor per lane), iota 1 = 155 64-bit ops; x 24 rounds
 VC_OPS_PER_PACKET = 2 * 155 * 24
 REF_TOOL = os.path.join(ROOT, "oracle", "_ref", "ref_tool")
+BOX_CPU_SHARE = 16      # host cores a one-GPU job may use on the GPU box
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--channels", type=int, default=262144, help="channels per GPU")
+    ap.add_argument("--channels", type=int, default=262144, help="channels per GPU (weak)")
+    ap.add_argument("--total-channels", type=int, default=262144,
+                    help="config 4 strong-scaling leg: channels split across the ranks "
+                         "(0 = skip)")
+    ap.add_argument("--tx-channels", type=int, default=65536,
+                    help="config 5 TX front end leg, channels per GPU (0 = skip)")
     ap.add_argument("--no-decode", action="store_true")
+    ap.add_argument("--no-side-legs", action="store_true", help="skip crypt and VAD legs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-channels", type=int, default=128)
-    ap.add_argument("--cpu-jobs", type=int, default=0, help="0 = min(16, usable cores)")
-    return ap.parse_args()
+    ap.add_argument("--cpu-jobs", type=int, default=0,
+                    help="0 = min(%d, usable cores)" % BOX_CPU_SHARE)
+    return ap.parse_args(argv)
 
+
+def log(msg):
+    print("[bench] " + msg, file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------- launch --
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn(argv, n):
+    """--gpus N without a launcher: start N rank processes (one GPU each) and
+    wait.  Runs before this process touches the GPU."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs)
+
+
+# ----------------------------------------------------------- device rigs --
+
+class GpuRig:
+    """torch device, the stream every engine call is enqueued on, HIP events
+    on that stream, barrier + max over ranks"""
+
+    def __init__(self, local, world):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.world = torch, dist, world
+        if not torch.cuda.is_available():
+            sys.exit("bench.py needs a HIP device (MI355X)")
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        self.stream = torch.cuda.current_stream(self.dev)
+        self.sptr = self.stream.cuda_stream
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def event(self):
+        return self.torch.cuda.Event(enable_timing=True)
+
+    def record(self, ev):
+        ev.record(self.stream)
+
+    @staticmethod
+    def elapsed_ms(a, b):
+        return a.elapsed_time(b)
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max_over_ranks(self, x):
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def timed(rig, fns, K, W):
+    """W untimed steps, then K timed steps bracketed by barrier + sync; each
+    step runs the launches in `fns` (callables of the step index) in order,
+    with an event recorded around each launch.  Returns (wall seconds for K
+    steps, max over ranks; mean ms per launch of each fn)."""
+    for s in range(W):
+        for fn in fns:
+            fn(s)
+    rig.sync()
+    rig.barrier()
+    rig.sync()
+    ev = [[rig.event() for _ in range(len(fns) + 1)] for _ in range(K)]
+    t0 = time.perf_counter()
+    for i in range(K):
+        rig.record(ev[i][0])
+        for j, fn in enumerate(fns):
+            fn(W + i)
+            rig.record(ev[i][j + 1])
+    rig.sync()
+    rig.barrier()
+    rig.sync()
+    dt = time.perf_counter() - t0
+    kms = [float(np.mean([rig.elapsed_ms(ev[i][j], ev[i][j + 1]) for i in range(K)]))
+           for j in range(len(fns))]
+    return rig.max_over_ranks(dt), kms
+
+
+# -------------------------------------------------------------- workload --
+
+class EngineWorkload:
+    """C channels (global ids first..first+C-1) on one engine; PCM of every
+    step generated on the device up front; bits stay on the device."""
+
+    def __init__(self, rig, C, first, steps):
+        import torch
+        from pairphone_amd import MelpeEngine
+        self.rig, self.C, self.first, self.steps = rig, C, first, steps
+        self.eng = MelpeEngine(C, device=rig.dev.index)
+        self.lib = self.eng.lib
+        self.pcm = torch.empty((steps, C, SF_SAMPLES), dtype=torch.int16, device=rig.dev)
+        self.bits = torch.zeros((steps, C, SF_BYTES), dtype=torch.uint8, device=rig.dev)
+        self.out = None
+        self.regen_pcm()
+
+    def regen_pcm(self):
+        """the raw synthetic PCM of every step (melpe_a overwrites it in place
+        with the NPP output, melpe/melpe.c:94-96)"""
+        self.eng.synth_seed(RUN_SEED, first_channel=self.first)
+        for s in range(self.steps):
+            self.eng.synth_dev(self.pcm[s].data_ptr(), SF_SAMPLES, self.rig.sptr)
+        self.rig.sync()
+
+    def npp(self, s):
+        self.eng.encode_npp_dev(self.pcm[s].data_ptr(), None, self.rig.sptr)
+
+    def ana(self, s):
+        self.eng.encode_ana_dev(self.bits[s].data_ptr(), self.pcm[s].data_ptr(), None,
+                                self.rig.sptr)
+
+    def dec(self, s):
+        if self.out is None:
+            self.out = self.rig.torch.empty_like(self.pcm)
+        self.eng.decode_dev(self.out[s].data_ptr(), self.bits[s].data_ptr(), None,
+                            self.rig.sptr)
+
+    def close(self):
+        self.eng.close()
+        self.pcm = self.bits = self.out = None
+
+
+# ------------------------------------------------------------ roofline W --
 
 def opcount():
     p = os.path.join(ROOT, "profiles", "opcount.json")
-    if not os.path.exists(p):
-        return None
-    return json.load(open(p))
+    return json.load(open(p)) if os.path.exists(p) else None
+
+
+def w_over(oc, key, lo, hi):
+    """mean W per channel-superframe over superframe indices [lo, hi) (the
+    ones this run times); the 149-superframe mean where the census does not
+    reach that far"""
+    by = oc.get(key + "_by_sf")
+    if by and hi <= len(by):
+        return float(np.mean(by[lo:hi])), "superframes %d..%d (the timed ones)" % (lo, hi - 1)
+    return oc[key + "_per_sf"], "149-superframe mean (timed range not in the census)"
 
 
 def pmc_traffic(kernel, channels):
@@ -83,25 +252,41 @@ def pmc_traffic(kernel, channels):
     they were taken at this channel count; else None."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(p):
-        return None
+        return None, None
     d = json.load(open(p))
     if d.get("channels") != channels:
-        return None
+        return None, None
     k = d.get("kernels", {}).get(kernel)
-    return None if k is None else k["bytes_per_launch"]
+    return (None if k is None else k["bytes_per_launch"]), d.get("source")
+
+
+def kroof(kernel, W_sf, C, kms, in_b, out_b, traffic_key=None):
+    ach = W_sf * C / (kms / 1e3) / 1e12
+    traffic, src = pmc_traffic(traffic_key or kernel, C)
+    return {"kernel": kernel, "kernel_ms": kms, "W_per_channel_superframe": W_sf,
+            "achieved": ach, "frac": ach / PEAK_VALU_TOPS,
+            "algorithmic_hbm_bytes_per_launch": C * (in_b + out_b),
+            "traffic": traffic, "traffic_source": src}
+
+
+# ----------------------------------------------------------- CPU baseline --
+
+def usable_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def cpu_baseline(args, gpu_bits):
-    """Reference codec, one process per core, on channels 0..S-1 of the same
-    synthetic input.  Returns (baseline dict, parity dict)."""
+    """Reference codec, one single-channel process per core, on channels
+    0..S-1 of the same synthetic input.  Returns (baseline dict, parity
+    dict)."""
     if args.no_cpu_baseline or not os.path.exists(REF_TOOL):
         return None, None
-    try:
-        usable = len(os.sched_getaffinity(0))
-    except AttributeError:
-        usable = os.cpu_count() or 1
-    jobs = args.cpu_jobs or min(16, usable)
-    S = args.cpu_sample_channels
+    usable = usable_cores()
+    jobs = args.cpu_jobs or min(BOX_CPU_SHARE, usable)
+    S = max(args.cpu_sample_channels, 4 * jobs)
     nsf = max(149, gpu_bits.shape[0])
     with tempfile.TemporaryDirectory() as tmp:
         out = os.path.join(tmp, "b.bits")
@@ -110,10 +295,15 @@ def cpu_baseline(args, gpu_bits):
                         str(nsf), out], check=True)
         dt = time.perf_counter() - t0
         ref = np.fromfile(out, dtype=np.uint8).reshape(S, nsf * SF_BYTES)
-    base = {"value": S * nsf * SF_SECONDS / dt, "unit": "channel-s/s", "cores": jobs,
-            "kind": "reference",
-            "sample": "%d channels x %d superframes (%.1f s of audio each), melpe_a, "
-                      "one forked reference process per channel, %d at a time, %.1f s wall"
+    value = S * nsf * SF_SECONDS / dt
+    base = {"value": value, "unit": "channel-s/s", "cores": jobs, "kind": "reference",
+            "per_core": value / jobs, "host_cores_visible": usable,
+            "host_cores_note": "the GPU box gives a one-GPU job a %d-core share of the host; "
+                               "per_core x host_cores_visible is the whole-host extrapolation"
+                               % BOX_CPU_SHARE,
+            "host_extrapolated": value / jobs * usable,
+            "sample": "%d channels x %d superframes (%.1f s of audio each), melpe_a, one forked "
+                      "single-channel reference process per channel, %d at a time, %.1f s wall"
                       % (S, nsf, nsf * SF_SECONDS, jobs, dt)}
     n = min(S, gpu_bits.shape[1])
     k = gpu_bits.shape[0]
@@ -123,178 +313,165 @@ def cpu_baseline(args, gpu_bits):
     return base, parity
 
 
-def log(msg):
-    print("[bench] " + msg, file=sys.stderr, flush=True)
+# ------------------------------------------------------------------ legs --
+
+def encode_leg(rig, wl, K, W):
+    return timed(rig, [wl.npp, wl.ana], K, W)
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def tx_leg(rig, args, rank, world):
+    """BASELINE config 5: the TX front end (tx.c:232-246: VAD gate, then
+    melpe_a on the superframes it opens) on ragged streams, per-channel
+    lengths uniform in [1 s, 20 s] (seeded), channels of this rank only.
+    One step = one superframe of every channel whose stream is still
+    running; the job is done when the longest stream ends.  Whole-job
+    throughput = channel-seconds of all streams / wall time."""
     import torch
-    import torch.distributed as dist
-    if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
-    if not torch.cuda.is_available():
-        sys.exit("bench.py needs a HIP device (MI355X)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
     from pairphone_amd import MelpeEngine
+    C = args.tx_channels
+    lo = rank * C
+    g = np.random.default_rng(RUN_SEED + 5)
+    lengths = g.integers(15, 297, size=world * C)[lo:lo + C]     # 1 s .. 20 s
+    nsf = int(lengths.max())
+    eng = MelpeEngine(C, device=rig.dev.index)
+    lib = eng.lib
+    pcm = torch.empty((nsf, C, SF_SAMPLES), dtype=torch.int16, device=rig.dev)
+    eng.synth_seed(RUN_SEED, first_channel=lo)
+    for s in range(nsf):
+        eng.synth_dev(pcm[s].data_ptr(), SF_SAMPLES, rig.sptr)
+    act = (torch.arange(nsf, device=rig.dev)[:, None] <
+           torch.from_numpy(lengths).to(rig.dev)[None, :]).to(torch.uint8).contiguous()
+    bits = torch.zeros((nsf, C, SF_BYTES), dtype=torch.uint8, device=rig.dev)
+    votes = torch.zeros((nsf, C), dtype=torch.uint8, device=rig.dev)
+    gate = torch.zeros((nsf, C), dtype=torch.uint8, device=rig.dev)
+    vst = torch.zeros(C * lib.melpe_vad_state_bytes(), dtype=torch.uint8, device=rig.dev)
+    if lib.melpe_vad_reset_dev(vst.data_ptr(), C, None, rig.sptr):
+        raise RuntimeError(lib.melpe_last_error().decode())
+    rig.sync()
+
+    def step(s):
+        eng.tx_dev(vst.data_ptr(), bits[s].data_ptr(), pcm[s].data_ptr(), votes[s].data_ptr(),
+                   gate[s].data_ptr(), act[s].data_ptr(), rig.sptr)
+    dt, (kms,) = timed(rig, [step], nsf, 0)
+    chs = float(lengths.sum()) * SF_SECONDS
+    tot = torch.tensor([chs], dtype=torch.float64, device=rig.dev)
+    if world > 1:
+        rig.dist.all_reduce(tot)
+    res = {"workload": "config 5: %d channels per GPU, ragged lengths uniform in [1 s, 20 s] "
+                       "(seed %d), VAD2 gate + melpe_a on the opened superframes" % (C, RUN_SEED + 5),
+           "value": float(tot.item()) / dt, "unit": "channel-s/s (whole streams)",
+           "wall_s": dt, "steps": nsf, "mean_step_ms": kms,
+           "channel_seconds": float(tot.item()),
+           "gated_open_fraction": float(gate.float().sum().item() / act.float().sum().item()),
+           "sharding": "contiguous channel ranges per rank"}
+    eng.close()
+    return res
+
+
+def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=None):
+    """one rank of the benchmark; returns the JSON line on rank 0.  rig_cls /
+    workload_cls replace the device plumbing in the CPU tests (gloo ranks,
+    tests/test_shard.py); the timing, sharding, gather and reporting code is
+    this one."""
+    import torch.distributed as dist
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group(backend)
+    rig = (rig_cls or GpuRig)(local, world)
+    Workload = workload_cls or EngineWorkload
     C, K, W = args.channels, args.steps, args.warmup
-    eng = MelpeEngine(C, device=local)
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
 
-    # every step's PCM generated on the device before the timed region
-    pcm = torch.empty((W + K, C, SF_SAMPLES), dtype=torch.int16, device=dev)
-    bits = torch.zeros((W + K, C, SF_BYTES), dtype=torch.uint8, device=dev)
-    eng.synth_seed(RUN_SEED, first_channel=rank * C)
-    for s in range(W + K):
-        eng.synth_dev(pcm[s].data_ptr(), SF_SAMPLES, sptr)
-    torch.cuda.synchronize(dev)
+    wl = Workload(rig, C, rank * C, W + K)
     log("rank %d: %d channels x %d superframes of input resident" % (rank, C, W + K))
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    def timed(fns):
-        """W untimed steps, then K timed steps bracketed by barrier + sync;
-        each step runs the launches in `fns` (callables of the step index)
-        in order on `stream`, with a HIP event around each launch.  Returns
-        (wall seconds for K steps, max over ranks; mean ms per launch)."""
-        for s in range(W):
-            for fn in fns:
-                fn(s)
-        torch.cuda.synchronize(dev)
-        barrier()
-        torch.cuda.synchronize(dev)
-        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(fns) + 1)]
-              for _ in range(K)]
-        t0 = time.perf_counter()
-        for i in range(K):
-            ev[i][0].record(stream)
-            for j, fn in enumerate(fns):
-                fn(W + i)
-                ev[i][j + 1].record(stream)
-        torch.cuda.synchronize(dev)
-        barrier()
-        torch.cuda.synchronize(dev)
-        dt = time.perf_counter() - t0
-        kms = [float(np.mean([ev[i][j].elapsed_time(ev[i][j + 1]) for i in range(K)]))
-               for j in range(len(fns))]
-        if world > 1:
-            t = torch.tensor([dt], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        return dt, kms
-
     # one step = melpe_a on every channel = k_enc_npp then k_enc_ana
-    # (melpe_encode_npp_dev + melpe_encode_ana_dev == melpe_encode_dev)
-    enc_s, (npp_kms, ana_kms) = timed([
-        lambda s: eng.encode_npp_dev(pcm[s].data_ptr(), None, sptr),
-        lambda s: eng.encode_ana_dev(bits[s].data_ptr(), pcm[s].data_ptr(), None, sptr)])
+    enc_s, (npp_kms, ana_kms) = encode_leg(rig, wl, K, W)
     enc_kms = npp_kms + ana_kms
     log("encode: %.1f ms/step (k_enc_npp %.1f ms + k_enc_ana %.1f ms)"
         % (1e3 * enc_s / K, npp_kms, ana_kms))
     # end-of-run bitstream gather (the only collective, outside the timed
     # region): every rank's K x C x 11 bytes to every rank, rank 0 keeps them
-    from pairphone_amd.shard import gather_bitstreams
-    torch.cuda.synchronize(dev)
+    from pairphone_amd.shard import gather_bitstreams, channel_range
+    rig.sync()
     t0 = time.perf_counter()
-    allbits = gather_bitstreams(bits[W:], world * C)
-    torch.cuda.synchronize(dev)
-    gather_ms = 1e3 * (time.perf_counter() - t0)
-    gathered = {"bytes": int(allbits.numel()), "ms": gather_ms,
+    allbits = gather_bitstreams(wl.bits[W:], world * C)
+    rig.sync()
+    gathered = {"bytes": int(allbits.numel()), "ms": 1e3 * (time.perf_counter() - t0),
                 "collective": "all_gather" if world > 1 else "none (1 rank)"}
+    del allbits
     dec = None
     if not args.no_decode:
-        out = torch.empty((W + K, C, SF_SAMPLES), dtype=torch.int16, device=dev)
-        dec_s, (dec_kms,) = timed([lambda s: eng.decode_dev(out[s].data_ptr(), bits[s].data_ptr(),
-                                                            None, sptr)])
+        dec_s, (dec_kms,) = timed(rig, [wl.dec], K, W)
         dec = {"value": world * C * K * SF_SECONDS / dec_s, "unit": "channel-s/s decoded",
                "ms_per_step": 1e3 * dec_s / K, "kernel_ms": dec_kms}
         log("decode: %.1f ms/step (kernel %.1f ms)" % (1e3 * dec_s / K, dec_kms))
+    cpu_bits = wl.bits[:W + K, :args.cpu_sample_channels].cpu().numpy() if rank == 0 else None
 
-    # voice-frame crypt (VoiceEnc, crp.c:986-1000) of each superframe's
-    # packets, the TX step after melpe_a: one packet per channel per launch
-    lib = eng.lib
-    g = torch.Generator().manual_seed(RUN_SEED + rank)
-    keys = torch.randint(0, 256, (C, 16), dtype=torch.uint8, generator=g).to(dev)
-    ctrs = torch.randint(0, 2**31, (C,), dtype=torch.int32, generator=g).to(dev)
-    cbits = bits.clone()
+    side = {}
+    if not args.no_side_legs:
+        side = side_legs(rig, wl, C, K, W, rank, world)
+    wl.close()
 
-    def crypt(s):
-        if lib.melpe_voice_crypt_dev(cbits[s].data_ptr(), ctrs.data_ptr(), keys.data_ptr(),
-                                     None, C, 1, 0, sptr):
-            raise RuntimeError(lib.melpe_last_error().decode())
-    crypt_s, (crypt_kms,) = timed([crypt])
-    crypt_ach = VC_OPS_PER_PACKET * C / (crypt_kms / 1e3) / 1e12
-    vcrypt = {"kernel": "k_voice_crypt", "value": world * C * K / crypt_s, "unit": "packets/s",
-              "kernel_ms": crypt_kms, "packets_per_launch": C,
-              "roofline": {"bound": "valu", "ops_per_packet": VC_OPS_PER_PACKET,
-                           "achieved": crypt_ach, "peak": PEAK_VALU_TOPS,
-                           "unit": "T INT32 VALU lane-ops/s", "frac": crypt_ach / PEAK_VALU_TOPS,
-                           "algorithmic_hbm_bytes_per_launch": C * (2 * SF_BYTES + 16 + 4)}}
-    log("voice crypt: kernel %.3f ms per %d packets" % (crypt_kms, C))
-    # TX voice-activity gate (vad2 x6 per superframe, tx.c:234-239) on the
-    # same PCM, one superframe per channel per launch, state resident
-    vst = torch.zeros(C * lib.melpe_vad_state_bytes(), dtype=torch.uint8, device=dev)
-    votes = torch.zeros((W + K, C), dtype=torch.uint8, device=dev)
-    if lib.melpe_vad_reset_dev(vst.data_ptr(), C, None, sptr):
-        raise RuntimeError(lib.melpe_last_error().decode())
+    strong = None
+    if args.total_channels:
+        lo, hi = channel_range(rank, world, args.total_channels)
+        if hi - lo == C:
+            strong = {"ms_per_step": 1e3 * enc_s / K, "kernel_ms": enc_kms}
+        else:
+            sw = Workload(rig, hi - lo, lo, W + K)
+            st_s, (snpp, sana) = encode_leg(rig, sw, K, W)
+            sw.close()
+            strong = {"ms_per_step": 1e3 * st_s / K, "kernel_ms": snpp + sana,
+                      "k_enc_npp_ms": snpp, "k_enc_ana_ms": sana}
+        strong.update({"total_channels": args.total_channels,
+                       "channels_per_gpu_max": -(-args.total_channels // world),
+                       "value": args.total_channels * K * SF_SECONDS / (strong["ms_per_step"] / 1e3 * K),
+                       "unit": "channel-s/s", "scaling": "strong",
+                       "sharding": "shard.channel_range: contiguous, balanced"})
+        log("strong (%d total): %.1f ms/step" % (args.total_channels, strong["ms_per_step"]))
 
-    def vad(s):
-        if lib.melpe_vad_dev(vst.data_ptr(), pcm[s].data_ptr(), votes[s].data_ptr(), C, None,
-                             sptr):
-            raise RuntimeError(lib.melpe_last_error().decode())
-    vad_s, (vad_kms,) = timed([vad])
-    vgate = {"kernel": "k_vad", "value": world * C * K * SF_SECONDS / vad_s,
-             "unit": "channel-s/s gated", "kernel_ms": vad_kms,
-             "silent_fraction": float((votes[W:] == 0).float().mean().item())}
-    log("vad: kernel %.3f ms per %d channel-superframes" % (vad_kms, C))
+    tx = None
+    if args.tx_channels:
+        tx = tx_leg(rig, args, rank, world)
+        log("tx front end: %.0f channel-s/s over %d steps" % (tx["value"], tx["steps"]))
 
     if rank != 0:
-        return
+        return None
     value = world * C * K * SF_SECONDS / enc_s
     oc = opcount()
     roof = None
     if oc:
-        def kroof(kernel, W_sf, kms, in_b, out_b):
-            ach = W_sf * C / (kms / 1e3) / 1e12
-            return {"kernel": kernel, "kernel_ms": kms, "W_per_channel_superframe": W_sf,
-                    "achieved": ach, "frac": ach / PEAK_VALU_TOPS,
-                    "algorithmic_hbm_bytes_per_launch": C * (in_b + out_b),
-                    "traffic": pmc_traffic(kernel, C)}
+        w_ana, w_src = w_over(oc, "W_enc_ana", W, W + K)
+        w_npp, _ = w_over(oc, "W_enc_npp", W, W + K)
         # the dominant kernel of the step (analysis) carries the headline
         # roofline; the NPP kernel and the whole step are listed beside it
-        ana = kroof("k_enc_ana", oc["W_enc_ana_per_sf"], ana_kms, 2 * SF_SAMPLES, SF_BYTES)
-        npp = kroof("k_enc_npp", oc["W_enc_npp_per_sf"], npp_kms, 2 * SF_SAMPLES, 2 * SF_SAMPLES)
-        step_ach = oc["W_enc_per_sf"] * C / (enc_kms / 1e3) / 1e12
+        ana = kroof("k_enc_ana", w_ana, C, ana_kms, 2 * SF_SAMPLES, SF_BYTES)
+        npp = kroof("k_enc_npp", w_npp, C, npp_kms, 2 * SF_SAMPLES, 2 * SF_SAMPLES)
+        step_ach = (w_ana + w_npp) * C / (enc_kms / 1e3) / 1e12
         roof = {"bound": "valu", "achieved": ana["achieved"], "peak": PEAK_VALU_TOPS,
                 "unit": "T basic-ops/s (INT32 VALU lane-ops)", "frac": ana["frac"],
-                "traffic": ana["traffic"], "kernel": "k_enc_ana", "kernel_ms": ana_kms,
-                "W_per_channel_superframe": ana["W_per_channel_superframe"],
+                "traffic": ana["traffic"], "traffic_source": ana["traffic_source"],
+                "kernel": "k_enc_ana", "kernel_ms": ana_kms,
+                "W_per_channel_superframe": w_ana, "W_source": w_src,
                 "algorithmic_hbm_bytes_per_launch": ana["algorithmic_hbm_bytes_per_launch"],
                 "kernels": [ana, npp],
-                "encode_step": {"W_per_channel_superframe": oc["W_enc_per_sf"],
+                "encode_step": {"W_per_channel_superframe": w_ana + w_npp,
                                 "kernel_ms": enc_kms, "achieved": step_ach,
                                 "frac": step_ach / PEAK_VALU_TOPS}}
         if dec:
-            dec["roofline_frac"] = oc["W_dec_per_sf"] * C / (dec["kernel_ms"] / 1e3) / 1e12 / PEAK_VALU_TOPS
-            dec["W_per_channel_superframe"] = oc["W_dec_per_sf"]
-            dec["traffic"] = pmc_traffic("k_decode", C)
-    if oc and oc.get("W_vad_per_sf"):
-        vach = oc["W_vad_per_sf"] * C / (vgate["kernel_ms"] / 1e3) / 1e12
-        vgate["roofline"] = {"bound": "valu", "W_per_channel_superframe": oc["W_vad_per_sf"],
+            w_dec, _ = w_over(oc, "W_dec", W, W + K)
+            dec["W_per_channel_superframe"] = w_dec
+            dec["roofline_frac"] = w_dec * C / (dec["kernel_ms"] / 1e3) / 1e12 / PEAK_VALU_TOPS
+            dec["traffic"], _ = pmc_traffic("k_decode", C)
+        if side.get("vad") and oc.get("W_vad_per_sf"):
+            v = side["vad"]
+            vach = oc["W_vad_per_sf"] * C / (v["kernel_ms"] / 1e3) / 1e12
+            v["roofline"] = {"bound": "valu", "W_per_channel_superframe": oc["W_vad_per_sf"],
                              "achieved": vach, "peak": PEAK_VALU_TOPS,
                              "unit": "T basic-ops/s (INT32 VALU lane-ops)",
                              "frac": vach / PEAK_VALU_TOPS}
     base, parity = (None, None)
     if world == 1:
-        base, parity = cpu_baseline(args, bits[:W + K, :args.cpu_sample_channels].cpu().numpy())
-    line = {
+        base, parity = cpu_baseline(args, cpu_bits)
+    return {
         "metric": "MELPe-1200 channel-seconds encoded/sec (node)",
         "value": value, "unit": "channel-s/s", "n_gpus": world, "steps": K, "warmup": W,
         "ms_per_step": 1e3 * enc_s / K, "higher_is_better": True, "scaling": "weak",
@@ -306,9 +483,70 @@ def main():
                    "parallelism": "channel shards, %d GPU(s), no collective" % world},
         "realtime_factor": value / (world * C),
         "roofline": roof, "cpu_baseline": base, "decode": dec, "parity_spot_check": parity,
-        "bitstream_gather": gathered, "voice_crypt": vcrypt, "vad": vgate,
+        "strong_scaling": strong, "tx_front_end": tx,
+        "bitstream_gather": gathered, "voice_crypt": side.get("crypt"), "vad": side.get("vad"),
     }
-    print(json.dumps(line), flush=True)
+
+
+def side_legs(rig, wl, C, K, W, rank, world):
+    """voice-frame crypt of each superframe's packets (VoiceEnc, crp.c:986,
+    the TX step after melpe_a) and the VAD gate alone (vad2 x6 per
+    superframe, tx.c:234-239) on the raw PCM"""
+    import torch
+    lib = wl.lib
+    g = torch.Generator().manual_seed(RUN_SEED + rank)
+    keys = torch.randint(0, 256, (C, 16), dtype=torch.uint8, generator=g).to(rig.dev)
+    ctrs = torch.randint(0, 2**31, (C,), dtype=torch.int32, generator=g).to(rig.dev)
+    cbits = wl.bits.clone()
+
+    def crypt(s):
+        if lib.melpe_voice_crypt_dev(cbits[s].data_ptr(), ctrs.data_ptr(), keys.data_ptr(),
+                                     None, C, 1, 0, rig.sptr):
+            raise RuntimeError(lib.melpe_last_error().decode())
+    crypt_s, (crypt_kms,) = timed(rig, [crypt], K, W)
+    del cbits
+    ach = VC_OPS_PER_PACKET * C / (crypt_kms / 1e3) / 1e12
+    vcrypt = {"kernel": "k_voice_crypt", "value": world * C * K / crypt_s, "unit": "packets/s",
+              "kernel_ms": crypt_kms, "packets_per_launch": C,
+              "roofline": {"bound": "valu", "ops_per_packet": VC_OPS_PER_PACKET,
+                           "achieved": ach, "peak": PEAK_VALU_TOPS,
+                           "unit": "T INT32 VALU lane-ops/s", "frac": ach / PEAK_VALU_TOPS,
+                           "algorithmic_hbm_bytes_per_launch": C * (2 * SF_BYTES + 16 + 4)}}
+    log("voice crypt: kernel %.3f ms per %d packets" % (crypt_kms, C))
+    # the encode leg overwrote the PCM with the NPP output: regenerate the raw
+    # input, which is what tx.c's vad2 sees
+    wl.regen_pcm()
+    vst = torch.zeros(C * lib.melpe_vad_state_bytes(), dtype=torch.uint8, device=rig.dev)
+    votes = torch.zeros((W + K, C), dtype=torch.uint8, device=rig.dev)
+    if lib.melpe_vad_reset_dev(vst.data_ptr(), C, None, rig.sptr):
+        raise RuntimeError(lib.melpe_last_error().decode())
+
+    def vad(s):
+        if lib.melpe_vad_dev(vst.data_ptr(), wl.pcm[s].data_ptr(), votes[s].data_ptr(), C, None,
+                             rig.sptr):
+            raise RuntimeError(lib.melpe_last_error().decode())
+    vad_s, (vad_kms,) = timed(rig, [vad], K, W)
+    vgate = {"kernel": "k_vad", "value": world * C * K * SF_SECONDS / vad_s,
+             "unit": "channel-s/s gated", "kernel_ms": vad_kms,
+             "silent_fraction": float((votes[W:] == 0).float().mean().item()),
+             "input": "raw synthetic PCM (before NPP)"}
+    log("vad: kernel %.3f ms per %d channel-superframes" % (vad_kms, C))
+    return {"crypt": vcrypt, "vad": vgate}
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn(argv, args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("WORLD_SIZE %d overrides --gpus %d" % (world, args.gpus))
+    line = run(args, rank, world, local)
+    if line is not None:
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -78,3 +78,110 @@ def test_gather_world2_gloo(C):
                         for s in range(steps)]).numpy()
     assert (got == want).all()
     assert tmax == 2.0
+
+
+class CpuRig:
+    """bench.GpuRig's interface on the CPU (perf_counter events, gloo)"""
+
+    def __init__(self, local, world):
+        import torch
+        self.torch, self.dist, self.world = torch, dist, world
+        self.dev = torch.device("cpu")
+
+    def sync(self):
+        pass
+
+    def event(self):
+        return [0.0]
+
+    def record(self, ev):
+        import time
+        ev[0] = time.perf_counter()
+
+    @staticmethod
+    def elapsed_ms(a, b):
+        return 1e3 * (b[0] - a[0])
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def max_over_ranks(self, x):
+        t = torch.tensor([x], dtype=torch.float64)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+class FakeWorkload:
+    """stands in for the engine where there is no GPU: 'encodes' a channel's
+    superframe s into bytes that depend only on (global channel, s)"""
+
+    def __init__(self, rig, C, first, steps):
+        self.C, self.first, self.steps = C, first, steps
+        self.bits = torch.zeros((steps, C, 11), dtype=torch.uint8)
+        self.calls = []
+
+    def npp(self, s):
+        self.calls.append(("npp", s))
+
+    def ana(self, s):
+        g = torch.arange(self.first, self.first + self.C, dtype=torch.int64)
+        self.bits[s] = ((g[:, None] * 31 + s * 7 + torch.arange(11)) % 251).to(torch.uint8)
+
+    def dec(self, s):
+        pass
+
+    def close(self):
+        pass
+
+
+def _bench_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    import pairphone_amd.shard as shard
+    got = {}
+    real = shard.gather_bitstreams
+
+    def spy(bits, total):
+        out = real(bits, total)
+        got["all"] = out.clone()
+        return out
+    shard.gather_bitstreams = spy
+    args = bench.parse(["--gpus", str(world), "--steps", "3", "--warmup", "1", "--channels", "5",
+                        "--total-channels", "13", "--tx-channels", "0", "--no-side-legs",
+                        "--no-cpu-baseline"])
+    line = bench.run(args, rank, world, rank, rig_cls=CpuRig, workload_cls=FakeWorkload)
+    if rank == 0:
+        q.put((line, got["all"].numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_run_world2_gloo():
+    """bench.run itself on two gloo ranks (engine stubbed on the CPU): the
+    JSON line has n_gpus 2, the weak value counts both ranks' channels, the
+    strong leg splits --total-channels with channel_range, and the gathered
+    bitstreams are every rank's channels in global order"""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    line, allbits = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["channels_total"] == 10
+    assert abs(line["value"] - 10 * 3 * 0.0675 / (line["ms_per_step"] * 3 / 1e3)) < 1e-6 * line["value"]
+    st = line["strong_scaling"]
+    assert st["total_channels"] == 13 and st["channels_per_gpu_max"] == 7
+    assert line["bitstream_gather"]["collective"] == "all_gather"
+    g = torch.arange(10, dtype=torch.int64)
+    want = torch.stack([((g[:, None] * 31 + s * 7 + torch.arange(11)) % 251).to(torch.uint8)
+                        for s in range(1, 4)]).numpy()
+    assert allbits.shape == (3, 10, 11) and (allbits == want).all()

@@ -69,6 +69,7 @@ def main(channels=32, nsf=149):
     lib.emu_encode_npp.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     lib.emu_encode_ana.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     npp = np.zeros(64, np.uint64)
+    by_sf = {"npp": [], "ana": [], "dec": []}
     for k in range(nsf):
         sp = np.ascontiguousarray(x[:, k * 540:(k + 1) * 540])
         b = np.zeros((channels, 11), np.uint8)
@@ -76,13 +77,16 @@ def main(channels=32, nsf=149):
         lib.emu_opcount(cnt.ctypes.data, 64)
         npp += cnt
         enc += cnt
+        by_sf["npp"].append(float(cnt.sum()) / channels)
         lib.emu_encode_ana(e, b.ctypes.data, sp.ctypes.data)
         lib.emu_opcount(cnt.ctypes.data, 64)
         enc += cnt
+        by_sf["ana"].append(float(cnt.sum()) / channels)
         out = np.zeros((channels, 540), np.int16)
         lib.emu_decode(e, out.ctypes.data, b.ctypes.data)
         lib.emu_opcount(cnt.ctypes.data, 64)
         dec += cnt
+        by_sf["dec"].append(float(cnt.sum()) / channels)
     n = channels * nsf
     res = {
         "rule": "saturating basic ops entered from codec code (nested op calls not counted), "
@@ -95,6 +99,11 @@ def main(channels=32, nsf=149):
         "W_enc_ana_per_sf": float(enc.sum() - npp.sum()) / n,
         "W_dec_per_sf": float(dec.sum()) / n,
         "enc_by_op": {names[i]: float(enc[i]) / n for i in np.argsort(-enc.astype(np.float64))[:len(names)] if enc[i]},
+        # per superframe index (mean over the channels): bench.py averages
+        # these over exactly the superframes it times
+        "W_enc_npp_by_sf": by_sf["npp"],
+        "W_enc_ana_by_sf": by_sf["ana"],
+        "W_dec_by_sf": by_sf["dec"],
         "dec_by_op": {names[i]: float(dec[i]) / n for i in np.argsort(-dec.astype(np.float64))[:len(names)] if dec[i]},
     }
     res.update(vad_census(lib, x, nsf))
