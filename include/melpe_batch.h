@@ -178,6 +178,32 @@ long melpe_stream_unpack(const unsigned char *stream, long nbytes, unsigned char
 			 uint8_t *voiced, long max_sf);
 const char *melpe_last_error(void);
 
+/* The pseudo-voice BPSK modem, PairPhone's TX step after the voice-frame
+ * crypt (Modulate, modem/modem.c:136, tx.c:271) and its RX step before it
+ * (Demodulate, modem/modem.c:186, rx.c:294-297).  state: C records of
+ * melpe_modem_state_bytes() (device, 4-byte aligned) = the modem's file
+ * statics (modem.c:48-73) per channel; melpe_modem_reset_dev gives a fresh
+ * process's values (mask: device C bytes or NULL = all).
+ * melpe_modulate_dev: pkts C x K x 11 bytes (81 bits each) -> pcm C x K x
+ *   3240 int16 at 48 kHz (4-byte aligned), K packets per channel in order.
+ * melpe_demodulate_dev: `calls` successive Demodulate calls per channel, as
+ *   rx.c makes them: channel c's samples are pcm[c*stride ...]; pos[c]
+ *   (int32, in/out) is the sample offset of its next call and advances by
+ *   each call's return value (216 +- 9); data C x 12 (in/out) is the
+ *   persistent buf of rx.c (payload bytes 0..10, lag in byte 10's upper bits,
+ *   status in byte 11: 0x80 packet ready, 0x40 block locked, 0x20 phase
+ *   locked, 0x10 frequency locked, low nibble symbol errors).  Optional
+ *   out C x calls x 12 gets data after every call, ret C x calls int32 the
+ *   return values.  A call needs 1080 samples from pos (rx.c:246); one that
+ *   would read past stride returns -1 and ends that channel's launch. */
+int melpe_modem_state_bytes(void);
+int melpe_modem_reset_dev(void *d_state, int channels, const void *d_mask, void *hip_stream);
+int melpe_modulate_dev(void *d_state, const void *d_pkts, void *d_pcm, int channels, int packets,
+		       const void *d_active, void *hip_stream);
+int melpe_demodulate_dev(void *d_state, const void *d_pcm, long stride, void *d_pos, void *d_data,
+			 void *d_out, void *d_ret, int channels, int calls, const void *d_active,
+			 void *hip_stream);
+
 /* Device basic-op self-test: out[i] = op(a[i], b[i], c[i]) evaluated by the
  * device build of the saturating basic operators, op ids of
  * pairphone_amd/csrc/ops_eval.h (a int64, b and c int32 or NULL, out int64,

@@ -41,6 +41,10 @@ def load_library(path=None):
         "melpe_engine_state_bytes": (ctypes.c_long, [i32]),
         "melpe_engine_export": (i32, [vp, i32, i32, i32, vp]),
         "melpe_engine_import": (i32, [vp, i32, i32, i32, vp]),
+        "melpe_modem_state_bytes": (i32, []),
+        "melpe_modem_reset_dev": (i32, [vp, i32, vp, vp]),
+        "melpe_modulate_dev": (i32, [vp, vp, vp, i32, i32, vp, vp]),
+        "melpe_demodulate_dev": (i32, [vp, vp, ctypes.c_long, vp, vp, vp, vp, i32, i32, vp, vp]),
         "melpe_ops_eval_dev": (i32, [i32, vp, vp, vp, vp, ctypes.c_long, vp]),
         "melpe_encode_host": (i32, [vp, vp, vp, vp]),
         "melpe_encode_dev": (i32, [vp, vp, vp, vp, vp]),

@@ -27,6 +27,8 @@
 #include "voice_crypt.h"
 #include "vad.h"
 #include "ops_eval.h"
+#define MODEM_FN __host__ __device__ static inline
+#include "modem.h"
 #include "../../include/melpe.h"
 #include "../../include/melpe_batch.h"
 
@@ -187,6 +189,94 @@ __global__ __launch_bounds__(WAVE) void k_vad_reset(VadState *st, const uint8_t 
 		return;
 	VadState z;
 	memset(&z, 0, sizeof z);
+	st[c] = z;
+}
+
+/* Modulate (modem.h, modem/modem.c:136): one wave per (channel, packet).
+ * The packet's starting state follows from the channel's state at launch:
+ * the previous bit is the last bit of the previous packet (its parity bit
+ * 89) and the muting flag alternates per packet.  Lane pairs of samples are
+ * stored as dwords: coalesced 6,480-byte rows per packet. */
+__global__ __launch_bounds__(256) void k_modulate(ModemState *st, const uint8_t *pkts, int16_t *pcm,
+						  int channels, int packets, const uint8_t *active)
+{
+	long w = blockIdx.x * 4L + threadIdx.x / WAVE;
+	int lane = threadIdx.x % WAVE;
+	if (w >= (long) channels * packets)
+		return;
+	int c = (int) (w / packets), k = (int) (w - (long) c * packets);
+	if (active && !active[c])
+		return;
+	const uint8_t *d = pkts + w * 11;
+	int prev0 = k ? modem_tx_bit(d - 11, MODEM_BITS - 1) : st[c].lastb;
+	int vad = st[c].vadtr ^ (k & 1);
+	uint32_t *o = (uint32_t *) (pcm + w * MODEM_PKT_SAMPLES);
+	for (int q = lane; q < MODEM_PKT_SAMPLES / 2; q += WAVE) {
+		int s0 = 2 * q, t = s0 / 36, ii = s0 - 36 * t;
+		int b = modem_tx_bit(d, t);
+		int prev = t ? modem_tx_bit(d, t - 1) : prev0;
+		uint32_t lo = (uint16_t) modem_sample(b, prev, vad, ii);
+		uint32_t hi = (uint16_t) modem_sample(b, prev, vad, ii + 1);
+		o[q] = lo | (hi << 16);
+	}
+}
+
+/* the state update of a whole modulate launch, after k_modulate has read it */
+__global__ __launch_bounds__(WAVE) void k_modulate_state(ModemState *st, const uint8_t *pkts,
+							 int channels, int packets, const uint8_t *active)
+{
+	int c = blockIdx.x * WAVE + threadIdx.x;
+	if (c >= channels || (active && !active[c]))
+		return;
+	st[c].lastb = modem_tx_bit(pkts + ((long) c * packets + packets - 1) * 11, MODEM_BITS - 1);
+	st[c].vadtr ^= packets & 1;
+}
+
+/* Demodulate (modem.h, modem/modem.c:186): one lane per channel, `calls`
+ * successive calls as rx.c:294-297 makes them (pos advances by the return
+ * value, data persists); a call that would read past the channel's stride
+ * returns -1 and stops the channel */
+__global__ __launch_bounds__(WAVE) void k_demodulate(ModemState *st, const int16_t *pcm, long stride,
+						     int32_t *pos, uint8_t *data, uint8_t *out,
+						     int32_t *ret, int channels, int calls,
+						     const uint8_t *active)
+{
+	int c = blockIdx.x * WAVE + threadIdx.x;
+	if (c >= channels || (active && !active[c]))
+		return;
+	ModemState S = st[c];
+	uint8_t d[12];
+	for (int i = 0; i < 12; i++)
+		d[i] = data[12L * c + i];
+	int32_t p = pos[c];
+	const int16_t *x = pcm + (long) c * stride;
+	for (int k = 0; k < calls; k++) {
+		int32_t r = -1;
+		if (p >= 0 && p + MODEM_LOOKAHEAD <= stride) {
+			r = modem_demod(&S, x + p, d);
+			p += r;
+		}
+		if (out)
+			for (int i = 0; i < 12; i++)
+				out[((long) c * calls + k) * 12 + i] = d[i];
+		if (ret)
+			ret[(long) c * calls + k] = r;
+		if (r < 0)
+			break;
+	}
+	st[c] = S;
+	pos[c] = p;
+	for (int i = 0; i < 12; i++)
+		data[12L * c + i] = d[i];
+}
+
+__global__ __launch_bounds__(WAVE) void k_modem_reset(ModemState *st, const uint8_t *mask, int channels)
+{
+	int c = blockIdx.x * WAVE + threadIdx.x;
+	if (c >= channels || (mask && !mask[c]))
+		return;
+	ModemState z;
+	modem_reset(&z);
 	st[c] = z;
 }
 
@@ -818,6 +908,69 @@ void melpe_s(short *sp, unsigned char *buf)
 	}
 }
 
+
+int melpe_modem_state_bytes(void)
+{
+	return (int) sizeof(ModemState);
+}
+
+static int modem_state_ok(const void *d_state, int channels)
+{
+	if (!d_state || channels <= 0)
+		return fail_msg("modem: bad arguments");
+	if ((uintptr_t) d_state & 3)
+		return fail_msg("modem: state must be 4-byte aligned");
+	return 0;
+}
+
+int melpe_modem_reset_dev(void *d_state, int channels, const void *d_mask, void *hip_stream)
+{
+	if (int r = modem_state_ok(d_state, channels))
+		return r;
+	k_modem_reset<<<grid_for(channels), WAVE, 0, (hipStream_t) hip_stream>>>(
+		(ModemState *) d_state, (const uint8_t *) d_mask, channels);
+	HIPCHK(hipGetLastError());
+	return 0;
+}
+
+int melpe_modulate_dev(void *d_state, const void *d_pkts, void *d_pcm, int channels, int packets,
+		       const void *d_active, void *hip_stream)
+{
+	if (int r = modem_state_ok(d_state, channels))
+		return r;
+	if (!d_pkts || !d_pcm || packets <= 0 || ((uintptr_t) d_pcm & 3))
+		return fail_msg("melpe_modulate_dev: bad arguments (pcm must be 4-byte aligned)");
+	long waves = (long) channels * packets;
+	if ((waves + 3) / 4 > 0x7fffffffL)
+		return fail_msg("melpe_modulate_dev: too many packets");
+	hipStream_t s = (hipStream_t) hip_stream;
+	k_modulate<<<(unsigned) ((waves + 3) / 4), 256, 0, s>>>(
+		(ModemState *) d_state, (const uint8_t *) d_pkts, (int16_t *) d_pcm, channels, packets,
+		(const uint8_t *) d_active);
+	HIPCHK(hipGetLastError());
+	k_modulate_state<<<grid_for(channels), WAVE, 0, s>>>(
+		(ModemState *) d_state, (const uint8_t *) d_pkts, channels, packets,
+		(const uint8_t *) d_active);
+	HIPCHK(hipGetLastError());
+	return 0;
+}
+
+int melpe_demodulate_dev(void *d_state, const void *d_pcm, long stride, void *d_pos, void *d_data,
+			 void *d_out, void *d_ret, int channels, int calls, const void *d_active,
+			 void *hip_stream)
+{
+	if (int r = modem_state_ok(d_state, channels))
+		return r;
+	if (!d_pcm || !d_pos || !d_data || calls <= 0 || stride < MODEM_LOOKAHEAD ||
+	    ((uintptr_t) d_pos & 3) || ((uintptr_t) d_ret & 3))
+		return fail_msg("melpe_demodulate_dev: bad arguments");
+	k_demodulate<<<grid_for(channels), WAVE, 0, (hipStream_t) hip_stream>>>(
+		(ModemState *) d_state, (const int16_t *) d_pcm, stride, (int32_t *) d_pos,
+		(uint8_t *) d_data, (uint8_t *) d_out, (int32_t *) d_ret, channels, calls,
+		(const uint8_t *) d_active);
+	HIPCHK(hipGetLastError());
+	return 0;
+}
 
 int melpe_ops_eval_dev(int op, const void *d_a, const void *d_b, const void *d_c, void *d_out,
 		       long n, void *hip_stream)

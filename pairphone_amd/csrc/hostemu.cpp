@@ -16,6 +16,7 @@
 #include "codec.h"
 #include "voice_crypt.h"
 #include "vad.h"
+#include "modem.h"
 
 using namespace mlp;
 
@@ -260,6 +261,63 @@ int emu_vad(unsigned char *state, const int16_t *sp, uint8_t *votes, int channel
 		for (int k = 0; k < nsf; k++)
 			votes[(size_t) c * nsf + k] = (uint8_t) va_superframe(
 				sp + ((size_t) c * nsf + k) * 540, &st[c]);
+	return 0;
+}
+
+/* host build of the modem (modem.h) */
+int emu_modem_state_bytes(void)
+{
+	return (int) sizeof(ModemState);
+}
+
+void emu_modem_reset(unsigned char *state, int channels)
+{
+	for (int c = 0; c < channels; c++)
+		modem_reset((ModemState *) state + c);
+}
+
+/* pkts C x K x 11 -> pcm C x K x 3240 */
+int emu_modulate(unsigned char *state, const uint8_t *pkts, int16_t *pcm, int channels, int packets)
+{
+	for (int c = 0; c < channels; c++) {
+		ModemState *S = (ModemState *) state + c;
+		for (int k = 0; k < packets; k++) {
+			const uint8_t *d = pkts + ((size_t) c * packets + k) * 11;
+			int16_t *o = pcm + ((size_t) c * packets + k) * MODEM_PKT_SAMPLES;
+			int prev = S->lastb;
+			for (int t = 0; t < MODEM_BITS; t++) {
+				int b = modem_tx_bit(d, t);
+				for (int ii = 0; ii < 36; ii++)
+					o[t * 36 + ii] = modem_sample(b, prev, S->vadtr, ii);
+				prev = b;
+			}
+			S->lastb = prev;
+			S->vadtr ^= 1;
+		}
+	}
+	return 0;
+}
+
+/* `calls` Demodulate calls per channel on pcm C x stride from pos[c];
+ * data C x 12 in/out, out C x calls x 12, ret C x calls */
+int emu_demodulate(unsigned char *state, const int16_t *pcm, long stride, int32_t *pos,
+		   uint8_t *data, uint8_t *out, int32_t *ret, int channels, int calls)
+{
+	for (int c = 0; c < channels; c++) {
+		ModemState *S = (ModemState *) state + c;
+		for (int k = 0; k < calls; k++) {
+			int32_t r = -1;
+			if (pos[c] >= 0 && pos[c] + MODEM_LOOKAHEAD <= stride) {
+				r = modem_demod(S, pcm + (size_t) c * stride + pos[c], data + 12 * (size_t) c);
+				pos[c] += r;
+			}
+			for (int i = 0; i < 12; i++)
+				out[((size_t) c * calls + k) * 12 + i] = data[12 * (size_t) c + i];
+			ret[(size_t) c * calls + k] = r;
+			if (r < 0)
+				break;
+		}
+	}
 	return 0;
 }
 

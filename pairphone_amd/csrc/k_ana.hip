@@ -4,6 +4,7 @@
  * the quantisers and channel packing, one lane per channel, reading the
  * NPP output k_enc_npp left in the caller's PCM.
  */
+#include <stdlib.h>
 #include "kern.h"
 
 MELPE_TU(ana)
@@ -44,10 +45,22 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana_dbg(EncState 
 	lane_copy((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, ENC_ANA_BYTES);
 }
 
+/* MELPE_ANA_LDS (diagnostic): reserve that many bytes of LDS per wave to cap
+ * the resident waves per CU (occupancy experiments) */
+static unsigned ana_lds_bytes(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("MELPE_ANA_LDS");
+		v = e ? atoi(e) : 0;
+	}
+	return (unsigned) v;
+}
+
 extern "C" int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
 			  int n, hipStream_t s)
 {
-	k_enc_ana<<<grid_for(n), WAVE, 0, s>>>(enc, sp, bits, active, n);
+	k_enc_ana<<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n);
 	return (int) hipGetLastError();
 }
 
