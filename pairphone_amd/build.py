@@ -91,10 +91,56 @@ def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=
     bad = [tu for tu, p in procs if p.wait() != 0]
     if bad:
         raise RuntimeError("hipcc failed for " + ", ".join(bad))
+    check_no_flat(objdir)
     tmp = out + ".tmp"
     _run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", tmp])
     os.replace(tmp, out)
     return out
+
+
+LLVM_BIN = "/opt/rocm/lib/llvm/bin"
+
+
+def device_disassembly(obj):
+    """gfx950 disassembly of one hipcc object (its offload bundle), as
+    {kernel symbol: [instruction lines]}"""
+    import tempfile
+    with tempfile.TemporaryDirectory() as tmp:
+        fat, elf = os.path.join(tmp, "fat.bin"), os.path.join(tmp, "dev.elf")
+        subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=" + fat, obj], check=True)
+        subprocess.run([os.path.join(LLVM_BIN, "clang-offload-bundler"), "--unbundle", "--type=o",
+                        "--input=" + fat, "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                        "--output=" + elf], check=True)
+        txt = subprocess.run([os.path.join(LLVM_BIN, "llvm-objdump"), "-d", "--no-show-raw-insn",
+                              elf], check=True, capture_output=True, text=True).stdout
+    out, cur = {}, None
+    for line in txt.splitlines():
+        if line.endswith(">:") and "<" in line:
+            cur = line[line.index("<") + 1:-2]
+            out[cur] = []
+        elif cur and line.startswith("\t"):
+            out[cur].append(line.strip())
+    return out
+
+
+# codec kernels that must not contain generic (FLAT) accesses: a FLAT access
+# to the private segment is aperture-checked before its offset is added,
+# which faulted on gfx950 (kern.h FLAT_GUARD_BYTES, DESIGN.md)
+NO_FLAT = ("k_enc_ana", "k_decode", "k_vad", "k_enc_npp", "k_npp", "k_demodulate")
+
+
+def check_no_flat(objdir):
+    bad = []
+    for f in sorted(os.listdir(objdir)):
+        if not f.endswith(".o"):
+            continue
+        for sym, ins in device_disassembly(os.path.join(objdir, f)).items():
+            if any(k in sym for k in NO_FLAT):
+                n = sum(1 for i in ins if i.startswith("flat_"))
+                if n:
+                    bad.append("%s: %d flat_ instructions" % (sym, n))
+    if bad:
+        raise RuntimeError("generic FLAT accesses in codec kernels: " + "; ".join(bad))
 
 
 def build_hostemu(force=False):

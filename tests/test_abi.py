@@ -37,3 +37,15 @@ def test_no_oracle_in_product():
         assert re.search(r"\b%s\b" % bad, out) is None, bad
     deps = subprocess.run(["ldd", LIB], capture_output=True, text=True).stdout
     assert "hostemu" not in deps and "ref_" not in deps
+
+
+def test_codec_kernels_have_no_flat_accesses():
+    """the build-time guard (pairphone_amd/build.py check_no_flat): the
+    codec kernels reach private memory only through scratch_ instructions,
+    never generic flat_ ones (the FLAT aperture fault, kern.h)"""
+    from pairphone_amd.build import check_no_flat, device_disassembly
+    objdir = os.path.join(ROOT, "build", "obj", "libmelpe_amd")
+    assert os.path.isdir(objdir), "run __graft_entry__.build() first"
+    check_no_flat(objdir)
+    dis = device_disassembly(os.path.join(objdir, "k_ana.o"))
+    assert any("k_enc_ana" in k for k in dis)
