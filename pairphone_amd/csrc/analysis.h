@@ -1286,7 +1286,7 @@ MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *
 MN void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, int len)
 {
 	PROF_SCOPE(12);
-	int16_t hb[1024];
+	uint32_t hb[512];	/* 512 packed complex bins (re | im << 16) */
 	Word32 Lm[NUM_HARM];
 	Word16 mx = 0;
 	for (int i = 0; i < len; i++) {
@@ -1296,10 +1296,18 @@ MN void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, in
 	}
 	Word16 sh = norm_s(mx);
 	v_set(fsmag, 8192, nh);
-	v_zero(hb, 1024);
-	for (int i = 0; i < len; i++)
-		hb[i] = shl(in[i], sh);
-	rfft(hb, 512);
+	/* the 512 real input points as 256 complex pairs, zero padded past len;
+	 * the scaled input's max |x| is the first guard test's block_max */
+	Word16 smx = 0;
+	for (int k = 0; k < 256; k++) {
+		Word16 a = 2 * k < len ? shl(in[2 * k], sh) : (Word16) 0;
+		Word16 b = 2 * k + 1 < len ? shl(in[2 * k + 1], sh) : (Word16) 0;
+		hb[k] = pk(a, b);
+		smx = pk_amax(hb[k], smx);
+	}
+	for (int k = 256; k < 512; k++)
+		hb[k] = 0;
+	rfft_pk(hb, 512, smx);
 	Word16 fw = shr(divide_s(512, pitch), 2);
 	Word16 iw = shr(fw, 6);
 	Word16 i2 = shr(iw, 1);
@@ -1312,7 +1320,7 @@ MN void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, in
 		Word32 Lmax = 0;
 		for (int j = 0; j < iw; j++) {
 			Word16 b = add(i0, (Word16) j);
-			Word16 re = hb[2 * b], im = hb[2 * b + 1];
+			Word16 re = pk_re(hb[b]), im = pk_im(hb[b]);
 			Word32 t = L_add(L_mult(re, re), L_mult(im, im));
 			Lmax = Max_(Lmax, t);
 		}

@@ -1439,6 +1439,188 @@ MN void rfft(int16_t *d, Word16 n)
 	}
 }
 
+/* ------------------------------------------------------------------ */
+/* Packed FFT for the lane-per-channel analysis (find_harm): complex    */
+/* sample k is one dword (re | im << 16), so every butterfly moves two  */
+/* dwords instead of four shorts, and the block-floating-point guard of */
+/* each stage (block_max, then a shift of every sample) is fused into   */
+/* the passes: the max is tracked while the previous stage writes, the  */
+/* shift is applied as the next stage reads.  Same values, same order   */
+/* of saturating operations per output as cfft / rfft above.            */
+/* ------------------------------------------------------------------ */
+MD Word16 pk_re(uint32_t w) { return (Word16) (int16_t) (w & 0xffffu); }
+MD Word16 pk_im(uint32_t w) { return (Word16) (int16_t) (w >> 16); }
+MD uint32_t pk(Word16 re, Word16 im) { return (uint32_t) (uint16_t) re | ((uint32_t) (uint16_t) im << 16); }
+MD Word16 pk_amax(uint32_t w, Word16 m)
+{
+	Word16 a = abs_s(pk_re(w)), b = abs_s(pk_im(w));
+	m = a > m ? a : m;
+	return b > m ? b : m;
+}
+MD uint32_t pk_shr(uint32_t w, Word16 s) { return s ? pk(shr(pk_re(w), s), shr(pk_im(w), s)) : w; }
+
+/* cfft :115 on nn complex samples x[0..nn); `mx` = max |x| of the input
+ * (as block_max over its 2nn shorts); returns the halvings, and the max |x|
+ * of the output in *omx (for the caller's next guard test) */
+MN Word16 cfft_pk(uint32_t *x, int nn, Word16 mx, Word16 *omx)
+{
+	PROF_SCOPE(30);
+	const int16_t *wrt = g_der.wr, *wit = g_der.wi;
+	Word16 g = 0;
+	/* bit reversal (the reference's j recurrence on 1-based short indices) */
+	{
+		int n = 2 * nn, j = 1;
+		for (int i = 1; i < n; i += 2) {
+			if (j > i) {
+				uint32_t t = x[(j - 1) >> 1];
+				x[(j - 1) >> 1] = x[(i - 1) >> 1];
+				x[(i - 1) >> 1] = t;
+			}
+			int m = nn;
+			while (m >= 2 && j > m) {
+				j -= m;
+				m >>= 1;
+			}
+			j += m;
+		}
+	}
+	Word16 s = 0;
+	if (mx > 16383) {
+		g += 1;
+		s = 1;
+	}
+	/* stage 1: pairs */
+	mx = 0;
+	for (int k = 0; k < nn; k += 2) {
+		uint32_t p = pk_shr(x[k], s), q = pk_shr(x[k + 1], s);
+		Word16 pr = pk_re(p), pi = pk_im(p), qr = pk_re(q), qi = pk_im(q);
+		uint32_t a = pk(add(pr, qr), add(pi, qi)), b = pk(sub(pr, qr), sub(pi, qi));
+		x[k] = a;
+		x[k + 1] = b;
+		mx = pk_amax(b, pk_amax(a, mx));
+	}
+	s = 0;
+	if (mx > 16383) {
+		g += 1;
+		s = 1;
+	}
+	/* stage 2: quads, the second pair with the -j twiddle */
+	mx = 0;
+	for (int k = 0; k < nn; k += 4) {
+		uint32_t p0 = pk_shr(x[k], s), p1 = pk_shr(x[k + 1], s);
+		uint32_t q0 = pk_shr(x[k + 2], s), q1 = pk_shr(x[k + 3], s);
+		Word16 pr = pk_re(p0), pi = pk_im(p0), qr = pk_re(q0), qi = pk_im(q0);
+		uint32_t a0 = pk(add(pr, qr), add(pi, qi)), b0 = pk(sub(pr, qr), sub(pi, qi));
+		pr = pk_re(p1);
+		pi = pk_im(p1);
+		qr = pk_re(q1);
+		qi = pk_im(q1);
+		uint32_t a1 = pk(add(pr, qi), sub(pi, qr)), b1 = pk(sub(pr, qi), add(pi, qr));
+		x[k] = a0;
+		x[k + 2] = b0;
+		x[k + 1] = a1;
+		x[k + 3] = b1;
+		mx = pk_amax(b1, pk_amax(a1, pk_amax(b0, pk_amax(a0, mx))));
+	}
+	/* radix-2 stages; half = the reference's mmax / 2 in complex samples */
+	int istep_idx = nn >> 1;
+	for (int half = 4; half < nn; half <<= 1) {
+		s = 0;
+		if (mx > 16383) {
+			g += 2;
+			s = 2;
+		} else if (mx > 8191) {
+			g += 1;
+			s = 1;
+		}
+		istep_idx >>= 1;
+		int idx = 0;
+		Word16 wr = SW_MAX_, wi = 0;
+		Word16 nmx = 0;
+		for (int m = 0; m < half; m++) {
+			for (int ci = m; ci < nn; ci += 2 * half) {
+				int cj = ci + half;
+				uint32_t P = pk_shr(x[ci], s), Q = pk_shr(x[cj], s);
+				Word16 pr = pk_re(P), pi = pk_im(P), qr = pk_re(Q), qi = pk_im(Q);
+				Word32 tr = L_add(L_mult(wr, qr), L_mult(wi, qi));
+				tr = L_add(tr, 0x8000);
+				tr = L_shl(L_shr(tr, 16), 16);
+				Word32 ti = L_sub(L_mult(wi, qr), L_mult(wr, qi));
+				ti = L_add(ti, 0x8000);
+				ti = L_shl(L_shr(ti, 16), 16);
+				uint32_t a = pk(extract_h(L_add(L_deposit_h(pr), tr)),
+						extract_h(L_sub(L_deposit_h(pi), ti)));
+				uint32_t b = pk(extract_h(L_sub(L_deposit_h(pr), tr)),
+						extract_h(L_add(L_deposit_h(pi), ti)));
+				x[ci] = a;
+				x[cj] = b;
+				nmx = pk_amax(b, pk_amax(a, nmx));
+			}
+			idx += istep_idx;
+			wr = wrt[idx];
+			wi = wit[idx];
+		}
+		mx = nmx;
+	}
+	*omx = mx;
+	return g;
+}
+
+/* rfft :33 on n real points held as n/2 packed complex samples in
+ * x[0..n/2), output n packed complex bins in x[0..n); `mx` = max |x| of
+ * the input */
+MN void rfft_pk(uint32_t *x, int n, Word16 mx)
+{
+	PROF_SCOPE(31);
+	const int16_t *wrt = g_der.wr, *wit = g_der.wi;
+	const int n2 = n >> 1;		/* complex points of the inner FFT */
+	cfft_pk(x, n2, mx, &mx);
+	Word16 s = mx > 16383 ? 1 : 0;
+	for (int k = 1; k < n2 / 2; k++) {
+		uint32_t A = pk_shr(x[k], s), B = pk_shr(x[n2 - k], s);
+		Word16 ar = pk_re(A), ai = pk_im(A), br = pk_re(B), bi = pk_im(B);
+		Word16 r1 = add_shr(ar, br);
+		Word32 a = L_shl(L_sub(ai, bi), 16);
+		Word16 r2 = add_shr(ai, bi);
+		Word32 b = L_shl(L_sub(ar, br), 16);
+		x[k] = pk(r1, r2);
+		x[n2 - k] = pk(r1, r2);
+		Word16 bh = extract_h(L_shr(b, 1)), ah = extract_h(L_shr(a, 1));
+		b = L_negate(b);
+		a = L_negate(a);
+		x[n - k] = pk(ah, bh);
+		x[n2 + k] = pk(extract_h(L_shr(a, 1)), extract_h(L_shr(b, 1)));
+	}
+	x[n2 + n2 / 2] = 0;
+	x[n2 / 2] = pk_shr(x[n2 / 2], s);
+	uint32_t z = pk_shr(x[0], s);
+	x[0] = pk(add(pk_re(z), pk_im(z)), 0);
+	x[n2] = pk(sub(pk_re(z), pk_im(z)), 0);
+	int idx = 1;
+	Word16 wr = wrt[idx], wi = wit[idx];
+	for (int k = 1; k < n2; k++) {
+		uint32_t A = x[k], B = x[n - k];
+		Word16 a1 = pk_re(A), a2 = pk_im(A), b1 = pk_re(B), b2 = pk_im(B);
+		Word32 t = L_deposit_h(a1);
+		t = L_add(t, L_mult(a2, wr));
+		t = L_add(t, 0x8000);
+		t = L_shl(L_shr(t, 16), 16);
+		t = L_sub(t, L_mult(b2, wi));
+		t = L_add(t, 0x8000);
+		Word32 u = L_deposit_h(b1);
+		u = L_sub(u, L_mult(a2, wi));
+		u = L_add(u, 0x8000);
+		u = L_shl(L_shr(u, 16), 16);
+		u = L_sub(u, L_mult(b2, wr));
+		u = L_add(u, 0x8000);
+		x[k] = pk(extract_h(t), extract_h(u));
+		x[n - k] = pk(extract_h(t), extract_h(L_negate(u)));
+		idx += 1;
+		wr = wrt[idx];
+		wi = wit[idx];
+	}
+}
+
 }  // namespace mlp
 
 #endif
