@@ -485,6 +485,7 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
         "roofline": roof, "cpu_baseline": base, "decode": dec, "parity_spot_check": parity,
         "strong_scaling": strong, "tx_front_end": tx,
         "bitstream_gather": gathered, "voice_crypt": side.get("crypt"), "vad": side.get("vad"),
+        "modem": side.get("modem"),
     }
 
 
@@ -531,7 +532,80 @@ def side_legs(rig, wl, C, K, W, rank, world):
              "silent_fraction": float((votes[W:] == 0).float().mean().item()),
              "input": "raw synthetic PCM (before NPP)"}
     log("vad: kernel %.3f ms per %d channel-superframes" % (vad_kms, C))
-    return {"crypt": vcrypt, "vad": vgate}
+    del vst, votes
+    return {"crypt": vcrypt, "vad": vgate, "modem": modem_leg(rig, wl, C, K, W, world)}
+
+
+MODEM_PKT = 3240          # 48 kHz samples per 81-bit packet (modem/modem.c:136)
+MODEM_CALLS = 15          # Demodulate calls per packet time (216 samples each)
+
+
+def modem_leg(rig, wl, C, K, W, world):
+    """PairPhone's pseudo-voice modem on the encoded packets: Modulate (tx.c:271)
+    one packet per channel per step, and Demodulate (rx.c:294) the 15 calls
+    of one packet time per channel per step on the modulated streams.  Both
+    are byte-moving kernels: roofline = HBM bytes / launch time."""
+    import torch
+    lib = wl.lib
+    sb = lib.melpe_modem_state_bytes()
+    st = torch.zeros(C * sb, dtype=torch.uint8, device=rig.dev)
+    if lib.melpe_modem_reset_dev(st.data_ptr(), C, None, rig.sptr):
+        raise RuntimeError(lib.melpe_last_error().decode())
+    out = torch.empty((C, MODEM_PKT), dtype=torch.int16, device=rig.dev)
+
+    def mod(s):
+        if lib.melpe_modulate_dev(st.data_ptr(), wl.bits[s].data_ptr(), out.data_ptr(), C, 1, None,
+                                  rig.sptr):
+            raise RuntimeError(lib.melpe_last_error().decode())
+    mod_s, (mod_kms,) = timed(rig, [mod], K, W)
+    del out
+    # the receive side: every channel's modulated stream of all W + K
+    # packets, made before the timed region
+    steps = W + K
+    stride = steps * MODEM_PKT + 2048
+    stream = torch.zeros((C, stride), dtype=torch.int16, device=rig.dev)
+    pk = wl.bits.transpose(0, 1).contiguous()            # C x steps x 11
+    if lib.melpe_modem_reset_dev(st.data_ptr(), C, None, rig.sptr):
+        raise RuntimeError(lib.melpe_last_error().decode())
+    if lib.melpe_modulate_dev(st.data_ptr(), pk.data_ptr(), stream.data_ptr(), C, steps, None,
+                              rig.sptr):
+        raise RuntimeError(lib.melpe_last_error().decode())
+    # modulate wrote C x steps x 3240 contiguously; spread rows to the stride
+    flat = stream.view(-1)[:C * steps * MODEM_PKT].view(C, steps * MODEM_PKT).clone()
+    stream.zero_()
+    stream[:, :steps * MODEM_PKT] = flat
+    del flat, pk
+    if lib.melpe_modem_reset_dev(st.data_ptr(), C, None, rig.sptr):
+        raise RuntimeError(lib.melpe_last_error().decode())
+    pos = torch.zeros(C, dtype=torch.int32, device=rig.dev)
+    data = torch.zeros((C, 12), dtype=torch.uint8, device=rig.dev)
+
+    def demod(s):
+        if lib.melpe_demodulate_dev(st.data_ptr(), stream.data_ptr(), stride, pos.data_ptr(),
+                                    data.data_ptr(), None, None, C, MODEM_CALLS, None, rig.sptr):
+            raise RuntimeError(lib.melpe_last_error().decode())
+    dem_s, (dem_kms,) = timed(rig, [demod], K, W)
+    locked = float(((data[:, 11] & 0x40) > 0).float().mean().item())
+    del stream
+    mod_bytes = C * (SF_BYTES + 2 * MODEM_PKT)
+    dem_bytes = C * MODEM_CALLS * (2 * 216 + 12) + 2 * C * sb
+    res = {"modulate": {"kernel": "k_modulate", "kernel_ms": mod_kms,
+                        "value": world * C * K / mod_s, "unit": "packets/s",
+                        "roofline": {"bound": "hbm", "achieved": mod_bytes / (mod_kms / 1e3) / 1e9,
+                                     "peak": 8000.0, "unit": "GB/s",
+                                     "frac": mod_bytes / (mod_kms / 1e3) / 1e9 / 8000.0,
+                                     "bytes_per_launch": mod_bytes}},
+           "demodulate": {"kernel": "k_demodulate", "kernel_ms": dem_kms,
+                          "value": world * C * K / dem_s, "unit": "packet times/s",
+                          "calls_per_launch": MODEM_CALLS, "block_locked_fraction": locked,
+                          "roofline": {"bound": "hbm", "achieved": dem_bytes / (dem_kms / 1e3) / 1e9,
+                                       "peak": 8000.0, "unit": "GB/s",
+                                       "frac": dem_bytes / (dem_kms / 1e3) / 1e9 / 8000.0,
+                                       "bytes_per_launch": dem_bytes,
+                                       "bytes_note": "unique samples + 12-byte outputs + state "
+                                                     "read and write"}}}
+    log("modem: modulate %.3f ms, demodulate %.3f ms per %d channels" % (mod_kms, dem_kms, C))
+    return res
 
 
 def main(argv=None):

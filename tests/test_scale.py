@@ -131,3 +131,73 @@ def test_channel_independence():
             got = eng.encode(sp)
             np.testing.assert_array_equal(got[0], b[k, c], err_msg="channel %d sf %d" % (c, k))
         eng.close()
+
+
+@pytest.mark.gpu
+def test_config5_tx_front_end_ragged_at_scale(tmp_path, ref_tool):
+    """BASELINE config 5 at the bench's per-GPU size: 65,536 channels with
+    stream lengths uniform in [1 s, 20 s] (15..296 superframes, the bench's
+    seed), the VAD gate + melpe_a on the superframes it opens
+    (melpe_tx_dev, tx.c:232-246) for every channel's whole stream; 64
+    sampled channels against the reference VAD and the reference codec run
+    on the gated superframes (ref_tool encgate), over their full lengths."""
+    import sys
+    import torch
+    import bench
+    from conftest import GOLDEN
+    from pairphone_amd import MelpeEngine, load_library, synth_signal
+    sys.path.insert(0, GOLDEN)
+    from make_vad_golden import ref_vad
+    lib = load_library()
+    C = 65536
+    lengths = np.random.default_rng(bench.RUN_SEED + 5).integers(15, 297, size=C)
+    nsf = int(lengths.max())
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    eng = MelpeEngine(C)
+    pcm = torch.empty((nsf, C, 540), dtype=torch.int16, device=dev)
+    eng.synth_seed(bench.RUN_SEED)
+    for k in range(nsf):
+        eng.synth_dev(pcm[k].data_ptr(), 540, s)
+    act = (torch.arange(nsf, device=dev)[:, None] <
+           torch.from_numpy(lengths).to(dev)[None, :]).to(torch.uint8).contiguous()
+    bits = torch.zeros((nsf, C, 11), dtype=torch.uint8, device=dev)
+    votes = torch.zeros((nsf, C), dtype=torch.uint8, device=dev)
+    gate = torch.zeros((nsf, C), dtype=torch.uint8, device=dev)
+    vst = torch.zeros(C * lib.melpe_vad_state_bytes(), dtype=torch.uint8, device=dev)
+    assert lib.melpe_vad_reset_dev(vst.data_ptr(), C, None, s) == 0
+    for k in range(nsf):
+        eng.tx_dev(vst.data_ptr(), bits[k].data_ptr(), pcm[k].data_ptr(), votes[k].data_ptr(),
+                   gate[k].data_ptr(), act[k].data_ptr(), s)
+    torch.cuda.synchronize(dev)
+    chans = _sampled(C, 64)
+    # include the longest and the shortest streams
+    chans = sorted(set(chans) | {int(lengths.argmax()), int(lengths.argmin())})
+    gb = bits[:, chans].cpu().numpy()
+    gv = votes[:, chans].cpu().numpy()
+    gg = gate[:, chans].cpu().numpy()
+    del pcm, bits
+    eng.close()
+
+    def ref(c):
+        L = int(lengths[c])
+        x = synth_signal(bench.RUN_SEED, c, L * 540)
+        v = ref_vad(x.reshape(1, -1), L)[0]
+        p, g, o = (str(tmp_path / ("%s%d" % (n, c))) for n in ("p", "g", "b"))
+        x.tofile(p)
+        (v > 0).astype(np.uint8).tofile(g)
+        subprocess.run([REF_TOOL, "encgate", p, g, o], check=True)
+        return v, np.fromfile(o, np.uint8).reshape(L, 11)
+    with concurrent.futures.ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(ref, chans))
+    closed = 0
+    for i, c in enumerate(chans):
+        L = int(lengths[c])
+        v, b = want[i]
+        np.testing.assert_array_equal(gv[:L, i], v, err_msg="votes, channel %d" % c)
+        np.testing.assert_array_equal(gg[:, i], (np.arange(nsf) < L) & (np.pad(v, (0, nsf - L)) > 0),
+                                      err_msg="gate, channel %d" % c)
+        np.testing.assert_array_equal(gb[:L, i], b, err_msg="bits, channel %d" % c)
+        assert not gb[L:, i].any()
+        closed += int((v == 0).sum())
+    assert closed > 0
