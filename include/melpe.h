@@ -11,6 +11,13 @@
  *                                reference (melpe/melpe.c:94-96)
  *   melpe_s   melpe/melpe.c:102  11 bytes -> 540 samples
  *
+ * The 2400 bps entry points the reference declares but never defines
+ * (melpe/melpe.c:57-58) are provided as their names and the reference's
+ * RATE2400 code define them:
+ *   melpe_i2  initialise at 2400 bps (melpe_i with rate = RATE2400)
+ *   melpe_al  180 samples -> 54 bits (7 bytes), sp overwritten with the NPP
+ *             output; after melpe_i2, melpe_s decodes 7 bytes -> 180 samples
+ *
  * As in the reference, the encoder and decoder of the one process-global
  * instance share melp_par / quant_par / chbuf (melpe/global.c:28-37), so an
  * interleaved melpe_a / melpe_s sequence (PairPhone's duplex pp) decodes as
@@ -30,6 +37,8 @@ void melpe_n(short *sp);
 void melpe_i(void);
 void melpe_a(unsigned char *buf, short *sp);
 void melpe_s(short *sp, unsigned char *buf);
+void melpe_i2(void);
+void melpe_al(unsigned char *buf, short *sp);
 
 #ifdef __cplusplus
 }

@@ -48,6 +48,7 @@ typedef struct melpe_engine melpe_engine;
 #define MELPE_SF_SAMPLES 540
 #define MELPE_SF_BYTES 11
 #define MELPE_FRAME_SAMPLES 180
+#define MELPE_R24_BYTES 7
 
 /* create an engine of `channels` channels on HIP device `device` */
 int melpe_engine_create(melpe_engine **out, int device, int channels);
@@ -93,6 +94,21 @@ int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
 		      const uint8_t *active);
 int melpe_decode_dev(melpe_engine *e, void *d_sp, const void *d_bits,
 		     const void *d_active, void *hip_stream);
+
+/* The 2400 bps MELP mode (54 bits per 180-sample frame, in 7 bytes), which
+ * the reference compiles but cannot reach through melpe_i (melpe/melpe.c:76
+ * pins RATE1200): per active channel, encode2400 = npp of the frame at
+ * RATE2400 + analysis + melp_chn_write (sp C x 180 in/out, bits C x 7 out);
+ * decode2400 = melp_chn_read + synthesis of one frame (bits C x 7 in, sp C x
+ * 180 out).  A channel runs either mode from its reset, not both. */
+int melpe_encode2400_dev(melpe_engine *e, void *d_bits, void *d_sp, const void *d_active,
+			 void *hip_stream);
+int melpe_decode2400_dev(melpe_engine *e, void *d_sp, const void *d_bits, const void *d_active,
+			 void *hip_stream);
+int melpe_encode2400_host(melpe_engine *e, unsigned char *bits, int16_t *sp,
+			  const uint8_t *active);
+int melpe_decode2400_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
+			  const uint8_t *active);
 
 /* melpe_n on `frames` consecutive 180-sample frames of every active channel.
  * sp is C x stride int16 (stride >= frames*180), in place.  A channel's first

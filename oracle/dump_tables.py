@@ -75,6 +75,10 @@ TABLES = [
     ("gain_vq_cb", "qnt12_cb", "gain_vq_cb", 6144),
     ("pitch_vq_cb_vvv", "qnt12_cb", "pitch_vq_cb_vvv", 6144),
     ("res256x64x64x64", "qnt12_cb", "res256x64x64x64", 8960),
+    # 2400 bps MELP (melpe/msvq_cb.c:37,41): the 4-stage LSF MSVQ, Q17, and
+    # its mean vector, Q15 (appended: earlier offsets are unchanged)
+    ("msvq_cb_mean", "msvq_cb", "msvq_cb_mean", 10),
+    ("msvq_cb", "msvq_cb", "msvq_cb", 3200),
 ]
 
 

@@ -27,6 +27,16 @@
  *          bitstreams concatenated channel-major (nch*nsf*11 bytes)
  *   decgen <in.bits> <nch> <nsf> <out.pcm>
  *          decodes nch independent channel bitstreams (channel-major)
+ *   enc24gen <seed> <ch0> <nch> <nfr> <out.bits> [<out.npp.pcm>]
+ *   dec24gen <in.bits> <nch> <nfr> <out.pcm>
+ *          the 2400 bps MELP path, which the reference
+ *          compiles but never reaches: melpe_i pins rate = RATE1200
+ *          (melpe/melpe.c:76) and the 2400 entry points melpe_i2 / melpe_al
+ *          it declares (melpe/melpe.c:57-58) have no bodies.  The harness
+ *          sets the globals as melpe_i would for RATE2400 (frameSize =
+ *          FRAME, 54 bits in 7 bytes) and calls the reference's own
+ *          npp + analysis per 180-sample frame (melpe_a's body for one
+ *          frame) and synthesis per 7-byte frame (melpe_s's body)
  *   jobs   <n>   (prefix option: max parallel children, default 8)
  */
 #include <stdio.h>
@@ -37,8 +47,12 @@
 #include <sys/wait.h>
 
 #include "sc1200.h"
+#include "global.h"
 #include "melpe.h"
+#include "npp.h"
 #include "synth.h"
+
+extern int16_t mode, chwordsize, bitBufSize, bitBufSize12, bitBufSize24;
 
 extern struct melp_param melp_par[];
 extern struct quant_param quant_par;
@@ -133,6 +147,51 @@ static void decode_buffer(const unsigned char *bits, long nsf, int16_t *pcm,
 	}
 }
 
+/* RATE2400 initialisation: melpe_i (melpe/melpe.c:72-88) with rate =
+ * RATE2400 and one-frame blocks */
+static void init2400(void)
+{
+	mode = ANA_SYN;
+	rate = RATE2400;
+	frameSize = (int16_t) FRAME;
+	chwordsize = 8;
+	bitNum12 = 81;
+	bitNum24 = 54;
+	bitBufSize12 = 11;
+	bitBufSize24 = 7;
+	bitBufSize = bitBufSize24;
+	melp_ana_init();
+	melp_syn_init();
+}
+
+/* 2400 bps encode of n samples: per 180-sample frame npp in place, then
+ * analysis (one frame at RATE2400), 7 bytes of chbuf out */
+static long encode2400(const int16_t *pcm, long n, unsigned char *bits, int16_t *npp_out)
+{
+	short sp[FRAME];
+	long k, nfr = n / FRAME;
+	init2400();
+	for (k = 0; k < nfr; k++) {
+		memcpy(sp, pcm + k * FRAME, sizeof(sp));
+		npp(sp, sp);
+		analysis(sp, melp_par);
+		memcpy(bits + k * 7, chbuf, 7);
+		if (npp_out)
+			memcpy(npp_out + k * FRAME, sp, sizeof(sp));
+	}
+	return nfr;
+}
+
+static void decode2400(const unsigned char *bits, long nfr, int16_t *pcm)
+{
+	long k;
+	init2400();
+	for (k = 0; k < nfr; k++) {
+		memcpy(chbuf, bits + k * 7, 7);
+		synthesis(melp_par, pcm + k * FRAME);
+	}
+}
+
 /* Runs fn(c) for c in [0,n) in forked children, at most g_jobs at a time. */
 static void run_children(long n, void (*fn)(long, void *), void *arg)
 {
@@ -215,6 +274,30 @@ static void decgen_one(long c, void *varg)
 	int16_t *pcm = (int16_t *) calloc(a->nsf * BLOCK, 2);
 	decode_buffer(a->bits + c * a->nsf * 11, a->nsf, pcm, NULL);
 	write_at(a->out, c * a->nsf * BLOCK * 2, pcm, a->nsf * BLOCK * 2);
+}
+
+static void enc24gen_one(long c, void *varg)
+{
+	struct encgen_arg *a = (struct encgen_arg *) varg;	/* nsf = frames */
+	long n = a->nsf * FRAME;
+	int16_t *pcm = (int16_t *) calloc(n + 256, 2);
+	int16_t *npp_o = (int16_t *) calloc(n, 2);
+	unsigned char *bits = (unsigned char *) calloc(a->nsf, 7);
+	synth_state st;
+	synth_init(&st, synth_mix(a->seed, (uint32_t) (a->ch0 + c)));
+	synth_block(&st, pcm, (int) n);
+	encode2400(pcm, n, bits, npp_o);
+	write_at(a->out_bits, c * a->nsf * 7, bits, a->nsf * 7);
+	if (a->out_npp)
+		write_at(a->out_npp, c * n * 2, npp_o, n * 2);
+}
+
+static void dec24gen_one(long c, void *varg)
+{
+	struct decgen_arg *a = (struct decgen_arg *) varg;	/* nsf = frames */
+	int16_t *pcm = (int16_t *) calloc(a->nsf * FRAME, 2);
+	decode2400(a->bits + c * a->nsf * 7, a->nsf, pcm);
+	write_at(a->out, c * a->nsf * FRAME * 2, pcm, a->nsf * FRAME * 2);
 }
 
 static void make_file(const char *path, long len)
@@ -374,6 +457,34 @@ int main(int argc, char **argv)
 		}
 		make_file(a.out, nch * a.nsf * BLOCK * 2);
 		run_children(nch, decgen_one, &a);
+		return 0;
+	}
+	if (!strcmp(argv[1], "enc24gen") && (argc == 7 || argc == 8)) {
+		struct encgen_arg a;
+		long nch = atol(argv[4]);
+		a.seed = (uint32_t) strtoul(argv[2], 0, 0);
+		a.ch0 = atol(argv[3]);
+		a.nsf = atol(argv[5]);
+		a.out_bits = argv[6];
+		a.out_npp = argc == 8 ? argv[7] : NULL;
+		make_file(a.out_bits, nch * a.nsf * 7);
+		if (a.out_npp)
+			make_file(a.out_npp, nch * a.nsf * FRAME * 2);
+		run_children(nch, enc24gen_one, &a);
+		return 0;
+	}
+	if (!strcmp(argv[1], "dec24gen") && argc == 6) {
+		struct decgen_arg a;
+		long len, nch = atol(argv[3]);
+		a.bits = (const unsigned char *) read_file(argv[2], &len);
+		a.nsf = atol(argv[4]);
+		a.out = argv[5];
+		if (len < nch * a.nsf * 7) {
+			fprintf(stderr, "short bitstream file\n");
+			return 2;
+		}
+		make_file(a.out, nch * a.nsf * FRAME * 2);
+		run_children(nch, dec24gen_one, &a);
 		return 0;
 	}
 	fprintf(stderr, "bad command\n");

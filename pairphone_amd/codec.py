@@ -70,6 +70,12 @@ def load_library(path=None):
         "melpe_tx_dev": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
         "melpe_stream_pack": (i32, [vp, vp, vp, vp, vp, i32, vp]),
         "melpe_stream_unpack": (ctypes.c_long, [vp, ctypes.c_long, vp, vp, ctypes.c_long]),
+        "melpe_encode2400_dev": (i32, [vp, vp, vp, vp, vp]),
+        "melpe_decode2400_dev": (i32, [vp, vp, vp, vp, vp]),
+        "melpe_encode2400_host": (i32, [vp, vp, vp, vp]),
+        "melpe_decode2400_host": (i32, [vp, vp, vp, vp]),
+        "melpe_i2": (None, []),
+        "melpe_al": (None, [vp, vp]),
         "melpe_i": (None, []),
         "melpe_a": (None, [vp, vp]),
         "melpe_s": (None, [vp, vp]),
@@ -255,6 +261,23 @@ class MelpeEngine:
         sp = np.zeros((self.channels, SF_SAMPLES), dtype=np.int16)
         m = self._mask(active)
         _check(self.lib.melpe_decode_host(self.h, _ptr(sp), _ptr(bits), _ptr(m)))
+        return sp
+
+    def encode2400(self, sp, active=None):
+        """2400 bps mode: one 180-sample frame per channel. sp: int16 [C, 180],
+        overwritten with the NPP output.  Returns uint8 [C, 7] (54 bits)."""
+        assert sp.dtype == np.int16 and sp.shape == (self.channels, FRAME_SAMPLES)
+        assert sp.flags.c_contiguous
+        bits = np.zeros((self.channels, 7), dtype=np.uint8)
+        _check(self.lib.melpe_encode2400_host(self.h, _ptr(bits), _ptr(sp), _ptr(self._mask(active))))
+        return bits
+
+    def decode2400(self, bits, active=None):
+        """2400 bps mode: uint8 [C, 7] -> int16 [C, 180]."""
+        bits = np.ascontiguousarray(bits, dtype=np.uint8)
+        assert bits.shape == (self.channels, 7)
+        sp = np.zeros((self.channels, FRAME_SAMPLES), dtype=np.int16)
+        _check(self.lib.melpe_decode2400_host(self.h, _ptr(sp), _ptr(bits), _ptr(self._mask(active))))
         return sp
 
     def npp(self, sp, frames, active=None):

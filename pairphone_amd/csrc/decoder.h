@@ -1062,6 +1062,9 @@ MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_
 /* ------------------------------------------------------------------ */
 /* melp_syn :160 -- pitch-synchronous synthesis of one frame          */
 /* ------------------------------------------------------------------ */
+/* R24: the reference's rate == RATE2400 frame (melp_syn.c:213: the
+ * unvoiced-frame parameter override is 1200 bps only) */
+template <bool R24>
 MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 {
 	PROF_SCOPE(18);
@@ -1088,7 +1091,7 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 			noise_sup(&par->gain[i], D->noise_gain, 5120, 1536, 768);
 		}
 	}
-	if (par->uv_flag) {
+	if (par->uv_flag && !R24) {
 		v_set(par->fs_mag, 8192, NUM_HARM);
 		par->pitch = UV_PITCH_Q7;
 		par->jitter = 8192;	/* X025_Q15 */
@@ -1220,7 +1223,7 @@ MN void decode_superframe(DecState *D, int16_t *out)
 		v_copy(out, D->sigsave, D->syn_begin);
 	D->erase = low_rate_chn_read(D);
 	for (int i = 0; i < NF; i++) {
-		melp_syn(D, &D->par[i], &out[i * FRAME]);
+		melp_syn<false>(D, &D->par[i], &out[i * FRAME]);
 		if (D->syn_begin > 0 && i < NF - 1)
 			v_copy(&out[(i + 1) * FRAME], D->sigsave, D->syn_begin);
 	}

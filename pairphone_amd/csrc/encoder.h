@@ -14,7 +14,12 @@
 namespace mlp {
 
 /* melp_ana :280 -- analysis of one 180-sample frame; `speech` points at
- * hpspeech[i*FRAME] (the window spans speech[0 .. FRAME_END+PITCHMAX]) */
+ * hpspeech[i*FRAME] (the window spans speech[0 .. FRAME_END+PITCHMAX]).
+ * R24: the reference's rate == RATE2400 branches (melp_ana.c:370-391, 411,
+ * 441, 460): LPC autocorrelation to order 10, LSFs of the unexpanded LPC
+ * (kept as top_lpc), no pitch tracking / classification, the 2400 gain
+ * window, and no voicing decision here (q_bpvc makes it) */
+template <bool R24>
 MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 {
 	PROF_SCOPE(1);
@@ -39,12 +44,18 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 	E->fpitch[1] = shl(E->fpitch[1], 7);
 	bpvc_ana(E, &speech[FRAME_END], E->fpitch, par->bpvc, &sub_pitch);
 	par->jitter = (par->bpvc[0] < VJIT_Q14) ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;
-	lpc_acor(&speech[FRAME_END - LPC_FRAME / 2], TB(win_cof), ac, 4, 16, LPC_FRAME);
+	lpc_acor(&speech[FRAME_END - LPC_FRAME / 2], TB(win_cof), ac, 4, R24 ? LPC_ORD : 16,
+		 LPC_FRAME);
 	lpc[0] = 4096;
 	lpc_schr(ac, &lpc[1], LPC_ORD);
-	lpc_bwex(&lpc[1], &lpc[1], 32571, LPC_ORD);
-	lpc_pred2lsp(&lpc[1], par->lsf, LPC_ORD);
-	lpc_clmp(par->lsf, 409, LPC_ORD);
+	if (R24) {
+		lpc_pred2lsp(&lpc[1], par->lsf, LPC_ORD);
+		v_copy(E->top_lpc, &lpc[1], LPC_ORD);
+	} else {
+		lpc_bwex(&lpc[1], &lpc[1], 32571, LPC_ORD);
+		lpc_pred2lsp(&lpc[1], par->lsf, LPC_ORD);
+		lpc_clmp(par->lsf, 409, LPC_ORD);
+	}
 	zerflt(&speech[PITCH_BEG], lpc, &sb[LPF_ORD], LPC_ORD, PITCH_FR);
 	t = peakiness(&sb[LPF_ORD + PITCHMAX / 2], PITCHMAX);
 	if (t > 5488)
@@ -53,12 +64,14 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 		par->bpvc[1] = 16384;
 		par->bpvc[2] = 16384;
 	}
-	int ct = CUR_TRACK + subnum * PIT_SUBNUM;
-	for (int i = 0; i < PIT_SUBNUM; i++) {
-		pitchAuto(E, &speech[FRAME_END + i * PIT_SUBFRAME + PIT_COR_LEN / 2],
-			  &E->pitTrack[ct + i + 1], &E->classStat[ct + i + 1]);
-		classify(E, &speech[FRAME_END + i * PIT_SUBFRAME + PIT_SUBFRAME / 2],
-			 &E->classStat[ct + i + 1], ac);
+	if (!R24) {
+		int ct = CUR_TRACK + subnum * PIT_SUBNUM;
+		for (int i = 0; i < PIT_SUBNUM; i++) {
+			pitchAuto(E, &speech[FRAME_END + i * PIT_SUBFRAME + PIT_COR_LEN / 2],
+				  &E->pitTrack[ct + i + 1], &E->classStat[ct + i + 1]);
+			classify(E, &speech[FRAME_END + i * PIT_SUBFRAME + PIT_SUBFRAME / 2],
+				 &E->classStat[ct + i + 1], ac);
+		}
 	}
 	par->pitch = pitch_ana(E, &speech[FRAME_END], &sb[LPF_ORD + PITCHMAX], sub_pitch,
 			       E->pitch_avg, &pcorr);
@@ -66,11 +79,13 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 		if (par->bpvc[0] > BPTHRESH_Q14)
 			par->gain[i] = gain_ana(&speech[FRAME_BEG + (i + 1) * 90], sub_pitch, 120, 320);
 		else
-			par->gain[i] = gain_ana(&speech[FRAME_BEG + (i + 1) * 90], 15258, 0, 320);
+			par->gain[i] = gain_ana(&speech[FRAME_BEG + (i + 1) * 90],
+						R24 ? 15257 : 15258, 0, 320);
 	}
 	t = (par->gain[NUM_GAINFR - 1] > 7680) ? pcorr : (Word16) 0;
 	E->pitch_avg = p_avg_update(E, par->pitch, t, VMIN_Q14);
-	par->uv_flag = (par->bpvc[0] > BPTHRESH_Q14) ? 0 : 1;
+	if (!R24)
+		par->uv_flag = (par->bpvc[0] > BPTHRESH_Q14) ? 0 : 1;
 	E->fpitch[0] = E->fpitch[1];
 }
 
@@ -334,7 +349,7 @@ MD void analysis_frame(EncState *E, const int16_t *sp_in, int i)
 {
 	dc_rmv(&sp_in[i * FRAME], &E->hpspeech[IN_BEG + i * FRAME], E->dcdelin,
 	       E->dcdelout_hi, E->dcdelout_lo, FRAME);
-	melp_ana(E, &E->hpspeech[i * FRAME], &E->par[i], i);
+	melp_ana<false>(E, &E->hpspeech[i * FRAME], &E->par[i], i);
 }
 
 MN void analysis_tail(EncState *E)
@@ -386,7 +401,7 @@ MN void analysis_upto(EncState *E, const int16_t *sp_in, int upto)
 	for (int i = 0; i < NF; i++) {
 		dc_rmv(&sp_in[i * FRAME], &E->hpspeech[IN_BEG + i * FRAME], E->dcdelin,
 		       E->dcdelout_hi, E->dcdelout_lo, FRAME);
-		melp_ana(E, &E->hpspeech[i * FRAME], &par[i], i);
+		melp_ana<false>(E, &E->hpspeech[i * FRAME], &par[i], i);
 	}
 	if (upto < 2)
 		return;

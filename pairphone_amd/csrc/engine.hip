@@ -55,6 +55,8 @@ extern "C" {
 int melpe_tu_npp_upload(const void *blob, size_t bytes);
 int melpe_tu_ana_upload(const void *blob, size_t bytes);
 int melpe_tu_dec_upload(const void *blob, size_t bytes);
+int melpe_tu_r24_upload(const void *blob, size_t bytes);
+int melpe_tu_r24_prof(uint64_t *acc);
 int melpe_tu_npp_prof(uint64_t *acc);
 int melpe_tu_ana_prof(uint64_t *acc);
 int melpe_tu_dec_prof(uint64_t *acc);
@@ -66,6 +68,10 @@ int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *a
 int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto, hipStream_t s);
 int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
 	      hipStream_t s);
+int kl_enc24(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
+	     hipStream_t s);
+int kl_dec24(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
+	     hipStream_t s);
 }
 
 /* ------------------------------------------------------------------ */
@@ -400,7 +406,8 @@ static int ensure_device_tables(int dev)
 		return fail_msg("embedded table blob has the wrong size");
 	DEVGUARD(dev);
 	int (*up[])(const void *, size_t) = {melpe_tu_eng_upload, melpe_tu_npp_upload,
-					     melpe_tu_ana_upload, melpe_tu_dec_upload};
+					     melpe_tu_ana_upload, melpe_tu_dec_upload,
+					     melpe_tu_r24_upload};
 	for (auto f : up)
 		if (int rc = f(melpe_tables_blob, bytes))
 			return fail("table upload", (hipError_t) rc);
@@ -707,6 +714,89 @@ int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
 	return 0;
 }
 
+/* 2400 bps mode (codec2400.h): NPP of one 180-sample frame at RATE2400
+ * (k_npp, melpe/npp.c:180-184 first-call branch), then analysis + 54-bit
+ * packing (k_enc24); decode = channel read + synthesis of one frame */
+static int encode24_launch(melpe_engine *e, unsigned char *d_bits, int16_t *d_sp,
+			   const uint8_t *d_act, hipStream_t s, bool sync)
+{
+	DEVGUARD(e->device);
+	ev_begin(e, s);
+	HIPCHK((hipError_t) kl_npp(e->d_enc, d_sp, 1, MELPE_FRAME_SAMPLES, d_act, e->channels, 0, s));
+	HIPCHK((hipError_t) kl_enc24(e->d_enc, d_sp, d_bits, d_act, e->channels, s));
+	ev_end(e, s, sync);
+	return 0;
+}
+
+int melpe_encode2400_dev(melpe_engine *e, void *d_bits, void *d_sp, const void *d_active,
+			 void *hip_stream)
+{
+	if (!e || !d_bits || !d_sp)
+		return fail_msg("melpe_encode2400_dev: null argument");
+	return encode24_launch(e, (unsigned char *) d_bits, (int16_t *) d_sp,
+			       (const uint8_t *) d_active, (hipStream_t) hip_stream, false);
+}
+
+int melpe_decode2400_dev(melpe_engine *e, void *d_sp, const void *d_bits, const void *d_active,
+			 void *hip_stream)
+{
+	if (!e || !d_sp || !d_bits)
+		return fail_msg("melpe_decode2400_dev: null argument");
+	DEVGUARD(e->device);
+	hipStream_t s = (hipStream_t) hip_stream;
+	ev_begin(e, s);
+	HIPCHK((hipError_t) kl_dec24(e->d_dec, (int16_t *) d_sp, (const uint8_t *) d_bits,
+				     (const uint8_t *) d_active, e->channels, s));
+	ev_end(e, s, false);
+	return 0;
+}
+
+int melpe_encode2400_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const uint8_t *active)
+{
+	if (!e || !bits || !sp)
+		return fail_msg("melpe_encode2400_host: null argument");
+	DEVGUARD(e->device);
+	HIPCHK(hipDeviceSynchronize());
+	size_t pb = sizeof(int16_t) * MELPE_FRAME_SAMPLES * (size_t) e->channels;
+	size_t bb = (size_t) MELPE_R24_BYTES * e->channels;
+	int rc;
+	const uint8_t *m = stage_mask(e, active, &rc);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(e->d_pcm, sp, pb, hipMemcpyHostToDevice, e->stream));
+	if (active)
+		HIPCHK(hipMemcpyAsync(e->d_bits, bits, bb, hipMemcpyHostToDevice, e->stream));
+	rc = encode24_launch(e, e->d_bits, e->d_pcm, m, e->stream, true);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(sp, e->d_pcm, pb, hipMemcpyDeviceToHost, e->stream));
+	HIPCHK(hipMemcpyAsync(bits, e->d_bits, bb, hipMemcpyDeviceToHost, e->stream));
+	HIPCHK(hipStreamSynchronize(e->stream));
+	return 0;
+}
+
+int melpe_decode2400_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
+			  const uint8_t *active)
+{
+	if (!e || !bits || !sp)
+		return fail_msg("melpe_decode2400_host: null argument");
+	DEVGUARD(e->device);
+	HIPCHK(hipDeviceSynchronize());
+	size_t pb = sizeof(int16_t) * MELPE_FRAME_SAMPLES * (size_t) e->channels;
+	size_t bb = (size_t) MELPE_R24_BYTES * e->channels;
+	int rc;
+	const uint8_t *m = stage_mask(e, active, &rc);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(e->d_bits, bits, bb, hipMemcpyHostToDevice, e->stream));
+	if (active)
+		HIPCHK(hipMemcpyAsync(e->d_pcm, sp, pb, hipMemcpyHostToDevice, e->stream));
+	HIPCHK((hipError_t) kl_dec24(e->d_dec, e->d_pcm, e->d_bits, m, e->channels, e->stream));
+	HIPCHK(hipMemcpyAsync(sp, e->d_pcm, pb, hipMemcpyDeviceToHost, e->stream));
+	HIPCHK(hipStreamSynchronize(e->stream));
+	return 0;
+}
+
 /* per-channel state records (checkpoint / migration between engines) */
 static int state_geom(melpe_engine *e, int which, int first, int count, size_t *rec,
 		      char **base)
@@ -800,7 +890,7 @@ int melpe_prof_read(uint64_t *out, int n)
 {
 	uint64_t acc[64] = {0};
 	int (*rd[])(uint64_t *) = {melpe_tu_eng_prof, melpe_tu_npp_prof, melpe_tu_ana_prof,
-				   melpe_tu_dec_prof};
+				   melpe_tu_dec_prof, melpe_tu_r24_prof};
 	for (auto f : rd)
 		if (f(acc))
 			return fail_msg("not a profiling build (-DMELPE_PROF)");
@@ -828,6 +918,7 @@ double melpe_last_kernel_ms(const melpe_engine *ce)
 
 static melpe_engine *g_single = nullptr;
 static bool g_single_rate1200 = false;	/* melpe_i sets rate = RATE1200 */
+static bool g_single_rate2400 = false;	/* melpe_i2 sets rate = RATE2400 */
 static bool g_single_npp_started = false;	/* npp's static first_time has fired */
 
 static melpe_engine *single_engine(void)
@@ -864,6 +955,7 @@ int melpe_single_reset(void)
 {
 	melpe_engine *e = single_engine();
 	g_single_rate1200 = false;
+	g_single_rate2400 = false;
 	g_single_npp_started = false;
 	return melpe_engine_reset(e, nullptr, 3);
 }
@@ -878,6 +970,40 @@ void melpe_i(void)
 		abort();
 	}
 	g_single_rate1200 = true;
+	g_single_rate2400 = false;
+}
+
+/* melpe_i2 / melpe_al: the 2400 bps entry points the reference declares
+ * (melpe/melpe.c:57-58) but never defines.  melpe_i2 = melpe_i at RATE2400
+ * (melp_ana_init + melp_syn_init, one-frame blocks); melpe_al = melpe_a's
+ * body for one 180-sample frame: npp in place, analysis, 7 bytes out.
+ * After melpe_i2, melpe_s decodes one 7-byte frame into 180 samples (the
+ * reference's synthesis() at RATE2400). */
+void melpe_i2(void)
+{
+	melpe_engine *e = single_engine();
+	DevGuard dg(e->device);
+	k_melpe_i<<<1, WAVE, 0, e->stream>>>(e->d_enc, e->d_dec);
+	if (hipGetLastError() != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess) {
+		fprintf(stderr, "libmelpe_amd: melpe_i2 failed\n");
+		abort();
+	}
+	g_single_rate1200 = false;
+	g_single_rate2400 = true;
+}
+
+void melpe_al(unsigned char *buf, short *sp)
+{
+	melpe_engine *e = single_engine();
+	if (!g_single_rate2400) {
+		fprintf(stderr, "libmelpe_amd: melpe_al needs melpe_i2 first\n");
+		abort();
+	}
+	if (melpe_encode2400_host(e, buf, sp, nullptr)) {
+		fprintf(stderr, "libmelpe_amd: melpe_al failed: %s\n", g_err.c_str());
+		abort();
+	}
+	g_single_npp_started = true;
 }
 
 void melpe_a(unsigned char *buf, short *sp)
@@ -894,6 +1020,20 @@ void melpe_s(short *sp, unsigned char *buf)
 {
 	melpe_engine *e = single_engine();
 	DevGuard dg(e->device);
+	if (g_single_rate2400) {	/* synthesis() at RATE2400: 7 bytes -> 180 samples */
+		k_share_params<<<1, WAVE, 0, e->stream>>>(e->d_enc, e->d_dec, 0);
+		int rc = hipGetLastError() != hipSuccess || melpe_decode2400_host(e, sp, buf, nullptr);
+		if (!rc) {
+			k_share_params<<<1, WAVE, 0, e->stream>>>(e->d_enc, e->d_dec, 1);
+			rc = hipGetLastError() != hipSuccess ||
+			     hipStreamSynchronize(e->stream) != hipSuccess;
+		}
+		if (rc) {
+			fprintf(stderr, "libmelpe_amd: melpe_s (2400) failed: %s\n", g_err.c_str());
+			abort();
+		}
+		return;
+	}
 	k_share_params<<<1, WAVE, 0, e->stream>>>(e->d_enc, e->d_dec, 0);
 	int rc = hipGetLastError() != hipSuccess;
 	if (!rc)

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "codec.h"
+#include "codec2400.h"
 #include "voice_crypt.h"
 #include "vad.h"
 #include "modem.h"
@@ -261,6 +262,30 @@ int emu_vad(unsigned char *state, const int16_t *sp, uint8_t *votes, int channel
 		for (int k = 0; k < nsf; k++)
 			votes[(size_t) c * nsf + k] = (uint8_t) va_superframe(
 				sp + ((size_t) c * nsf + k) * 540, &st[c]);
+	return 0;
+}
+
+/* 2400 bps mode (codec2400.h): sp C x 180 in/out (NPP at RATE2400, then
+ * analysis), bits C x 7 out; decode bits C x 7 -> sp C x 180 */
+int emu_encode2400(emu_engine *e, unsigned char *bits, int16_t *sp)
+{
+	for (int c = 0; c < e->channels; c++) {
+		EncState *S = &e->enc[c];
+		int16_t *x = sp + (size_t) c * FRAME;
+		npp_frame(&S->npp, &g_npp_scratch, x, x, false);
+		analysis24(S, x);
+		memcpy(bits + (size_t) c * R24_BYTES, S->chbuf, R24_BYTES);
+	}
+	return 0;
+}
+
+int emu_decode2400(emu_engine *e, int16_t *sp, const unsigned char *bits)
+{
+	for (int c = 0; c < e->channels; c++) {
+		DecState *D = &e->dec[c];
+		memcpy(D->chbuf, bits + (size_t) c * R24_BYTES, R24_BYTES);
+		decode_frame24(D, sp + (size_t) c * FRAME);
+	}
 	return 0;
 }
 

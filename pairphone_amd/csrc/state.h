@@ -131,6 +131,11 @@ struct EncState {
 	int16_t sync_bit;
 	int16_t pad_;
 	uint8_t chbuf[12];
+	/* 2400 bps path: melpe/melp_ana.c top_lpc, melpe/melp_sub.c q_gain
+	 * prev_gain */
+	int16_t top_lpc[LPC_ORD];
+	int16_t qg_prev_gain;
+	int16_t pad24_;
 };
 
 #define MIX_ORD 32
@@ -162,6 +167,8 @@ struct DecState {
 	uint8_t chbuf[12];
 	/* melpe/dsp_sub.c rand_minstdgen */
 	uint32_t seed;
+	/* 2400 bps path: melpe/melp_sub.c q_gain_dec prev_gain, prev_gain_err */
+	int16_t qgd_prev_gain, qgd_prev_err;
 };
 
 /* melp_ana_init, melpe/melp_ana.c:475-506 (the part melpe_i re-runs) */
