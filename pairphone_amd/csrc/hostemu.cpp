@@ -289,6 +289,21 @@ int emu_decode2400(emu_engine *e, int16_t *sp, const unsigned char *bits)
 	return 0;
 }
 
+/* raw state records (test diagnostics): which 1 = EncState, 2 = DecState */
+long emu_state_bytes(int which)
+{
+	return which == 1 ? (long) sizeof(EncState) : (long) sizeof(DecState);
+}
+
+int emu_export(emu_engine *e, int which, int c, void *out)
+{
+	if (which == 1)
+		memcpy(out, &e->enc[c], sizeof(EncState));
+	else
+		memcpy(out, &e->dec[c], sizeof(DecState));
+	return 0;
+}
+
 /* host build of the modem (modem.h) */
 int emu_modem_state_bytes(void)
 {

@@ -55,11 +55,16 @@ using namespace mlp;
 #define PIN_FRAME(obj) __asm__ volatile("" : : "v"(&(obj)) : "memory")
 
 /* per-lane copy between a channel's HBM record and the lane's private
- * segment, 4 bytes at a time (sizes and offsets are multiples of 4) */
+ * segment, 4 bytes at a time (sizes and offsets are multiples of 4).  The
+ * dwords are may_alias: the records are read and written field by field as
+ * int16/int32/uint8, and a plain uint32_t copy would let type-based alias
+ * analysis treat the last field stores before the copy-out as dead (it did,
+ * in k_dec24: the tail of melp_syn never reached HBM); u32_alias is in
+ * ops.h. */
 __device__ __forceinline__ void lane_copy(void *dst, const void *src, size_t bytes)
 {
-	uint32_t *d = (uint32_t *) dst;
-	const uint32_t *s = (const uint32_t *) src;
+	u32_alias *d = (u32_alias *) dst;
+	const u32_alias *s = (const u32_alias *) src;
 #pragma unroll 8
 	for (size_t i = 0; i < bytes / 4; i++)
 		d[i] = s[i];

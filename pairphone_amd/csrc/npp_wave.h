@@ -88,7 +88,7 @@ struct NppWave {
 	NppScratch w;	/* YY.., ybuf, temp_yy (int32 first: alignment) */
 	/* the channel's NppState up to its min-statistics memory (NPP_HOT_BYTES);
 	 * that memory stays in the HBM record (the `m` view below) */
-	uint32_t s_hot[NPP_HOT_BYTES / 4];
+	u32_alias s_hot[NPP_HOT_BYTES / 4];	/* an NppState image, read as fields */
 	int16_t Ymag[NPP_NB], Ymag_shift[NPP_NB], GainD[NPP_NB];
 	int16_t gk[NPP_NB], gks[NPP_NB];
 	int16_t bsp[NPP_NB], bsub[NPP_NB], bsh[NPP_NB], bsubsh[NPP_NB];
@@ -767,8 +767,8 @@ MD void wv_npp_frame(NppWave *W, NppState *m, int16_t *x, int avail, bool rate12
 MD void wv_state_in(NppWave *W, const NppState *g, int lane)
 {
 	PROF_SCOPE(35);
-	const uint32_t *src = (const uint32_t *) g;
-	uint32_t *dst = W->s_hot;
+	const u32_alias *src = (const u32_alias *) g;	/* kern.h: may_alias dwords */
+	u32_alias *dst = W->s_hot;
 	LANE_LOOP(i, (int) (NPP_HOT_BYTES / 4))
 		dst[i] = src[i];
 	wsync();
@@ -778,8 +778,8 @@ MD void wv_state_out(NppState *g, const NppWave *W, int lane)
 {
 	PROF_SCOPE(35);
 	wsync();
-	const uint32_t *src = W->s_hot;
-	uint32_t *dst = (uint32_t *) g;
+	const u32_alias *src = W->s_hot;
+	u32_alias *dst = (u32_alias *) g;
 	LANE_LOOP(i, (int) (NPP_HOT_BYTES / 4))
 		dst[i] = src[i];
 }

@@ -110,6 +110,10 @@ struct ProfScope {
 #endif
 #define MELPE_OP_NAMES "add sub L_add L_sub L_mult extract_h extract_l L_deposit_h L_deposit_l mult L_mac L_msu r_ound msu_r negate L_negate abs_s L_abs shl shr L_shr L_shl shift_r L_shift_r norm_l norm_s divide_s L40_add L40_sub L40_mac L40_msu L40_shl L40_shr L40_negate norm32 L_sat32 L_mpy_ls"
 
+/* a dword that may alias any type: record copies (kern.h lane_copy, the
+ * NPP state image) move int16/int32/uint8 fields as dwords */
+typedef uint32_t __attribute__((__may_alias__)) u32_alias;
+
 typedef int16_t Word16;
 typedef int32_t Word32;
 typedef int64_t Word40;
