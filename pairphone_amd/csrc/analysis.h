@@ -34,7 +34,16 @@ MN void remove_dc(const int16_t *in, int16_t *out, int16_t len)
 	Word16 up = sub(15, norm_s(len));
 	Word16 pdown = shl(1, sub(up, 1));
 	Word32 sum = 0;
-	for (int i = 0; i < len; i++)
+	P16 r;
+	int np = p16_open(r, in, len);
+	int i = 0;
+	#pragma unroll 4
+	for (int k = 0; k < np; k++, i += 2) {
+		uint32_t x = p16_next(r);
+		sum = L_add(sum, L_deposit_l(lo16(x)));
+		sum = L_add(sum, L_deposit_l(hi16(x)));
+	}
+	for (; i < len; i++)
 		sum = L_add(sum, L_deposit_l(in[i]));
 	sum = L_shr(sum, up);
 	Word16 off = mult(extract_l(sum), divide_s(pdown, len));
@@ -169,8 +178,16 @@ MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 	 * saturates and the sum is exact.  One pass, no data-dependent exit. */
 	{
 		int64_t sum = 0;
+		P16 r;
+		int np = p16_open(r, in, len);
+		int i = 0;
 		#pragma unroll 8
-		for (int i = 0; i < len; i++)
+		for (int k = 0; k < np; k++, i += 2) {
+			uint32_t x = p16_next(r);
+			sum += L_mult(lo16(x), lo16(x));
+			sum += L_mult(hi16(x), hi16(x));
+		}
+		for (; i < len; i++)
 			sum += L_mult(in[i], in[i]);
 		ovf = sum > (int64_t) LW_MAX_;
 		corr = (Word32) sum;
@@ -199,9 +216,7 @@ MD void fp_corr8(const int16_t *pa, const int16_t *pb, int len, Word32 *out)
 	Word32 acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 	int16_t A0 = pa[0], A1 = pa[1], A2 = pa[2], A3 = pa[3];
 	int16_t B0 = pb[0], B1 = pb[1], B2 = pb[2];
-	#pragma unroll 4
-	for (int j = 0; j < len; j++) {
-		int16_t A4 = pa[j + 4], B3 = pb[j + 3];
+	auto step = [&](int16_t A4, int16_t B3) {
 		acc[0] = L_mac(acc[0], A0, B3);
 		acc[1] = L_mac(acc[1], A1, B3);
 		acc[2] = L_mac(acc[2], A1, B2);
@@ -217,7 +232,20 @@ MD void fp_corr8(const int16_t *pa, const int16_t *pb, int len, Word32 *out)
 		B0 = B1;
 		B1 = B2;
 		B2 = B3;
+	};
+	/* the new samples pa[j + 4], pb[j + 3] two at a time (P16) */
+	P16 ra, rb;
+	int np = p16_open(ra, pa + 4, len), nb = p16_open(rb, pb + 3, len);
+	np = np < nb ? np : nb;
+	int j = 0;
+	#pragma unroll 4
+	for (int k = 0; k < np; k++, j += 2) {
+		uint32_t x = p16_next(ra), y = p16_next(rb);
+		step(lo16(x), lo16(y));
+		step(hi16(x), hi16(y));
 	}
+	for (; j < len; j++)
+		step(pa[j + 4], pb[j + 3]);
 	for (int k = 0; k < 8; k++)
 		out[k] = acc[k];
 }
@@ -328,9 +356,7 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 	{
 		const int16_t *pa = &sig[cb], *pb = &sig[cb + ip - 1];
 		int16_t b0 = pb[0], b1 = pb[1];
-		#pragma unroll 4
-		for (int j = 0; j < len; j++) {
-			int16_t a = pa[j], b2 = pb[j + 2];
+		auto step = [&](int16_t a, int16_t b2) {
 			msq = L_mac(msq, a, a);
 			m2 = L_mac(m2, b0, b0);
 			cm1 = L_mac(cm1, a, b0);
@@ -342,7 +368,20 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 			tt1m = L_mac(tt1m, b0, b1);
 			b0 = b1;
 			b1 = b2;
+		};
+		/* a_j and b_(j+2) two at a time (P16) */
+		P16 ra, rb;
+		int np = p16_open(ra, pa, len), nb = p16_open(rb, pb + 2, len);
+		np = np < nb ? np : nb;
+		int j = 0;
+		#pragma unroll 4
+		for (int k = 0; k < np; k++, j += 2) {
+			uint32_t x = p16_next(ra), y = p16_next(rb);
+			step(lo16(x), lo16(y));
+			step(hi16(x), hi16(y));
 		}
+		for (; j < len; j++)
+			step(pa[j], pb[j + 2]);
 	}
 	/* census: the reference's two L_v_magsq and six L_v_inner calls */
 	OPC_ADD(OP_L_mac, -len);
@@ -781,9 +820,7 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 			int64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 			int a0 = pa[0], a1 = pa[1], a2 = pa[2];
 			int q0 = pq[0], q1 = pq[1], q2 = pq[2], q3 = pq[3];
-			#pragma unroll 4
-			for (int t = 0; t < PW; t++) {
-				int a3 = pa[t + 3], q4 = pq[t + 4];
+			auto step = [&](int a3, int q4) {
 				acc[0] += (int64_t) (a0 * q4);
 				acc[1] += (int64_t) (a0 * q3);
 				acc[2] += (int64_t) (a1 * q3);
@@ -799,7 +836,20 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 				q1 = q2;
 				q2 = q3;
 				q3 = q4;
+			};
+			/* pa[t + 3], pq[t + 4] two at a time (P16) */
+			P16 ra, rq;
+			int np = p16_open(ra, pa + 3, PW), nq = p16_open(rq, pq + 4, PW);
+			np = np < nq ? np : nq;
+			int t = 0;
+			#pragma unroll 4
+			for (int k = 0; k < np; k++, t += 2) {
+				uint32_t x = p16_next(ra), y = p16_next(rq);
+				step(lo16(x), lo16(y));
+				step(hi16(x), hi16(y));
 			}
+			for (; t < PW; t++)
+				step(pa[t + 3], pq[t + 4]);
 			for (int k = 0; k < 8; k++)
 				blk[k] = 2 * acc[k];
 		}
@@ -1029,10 +1079,9 @@ MD void fc_corr10(const int16_t *in, int hp, int win, Word40 *A)
 		av[k] = pa[k];
 		bv[k] = pb[k];
 	}
-	#pragma unroll 2
-	for (int t = 0; t < win; t++) {
-		av[5] = pa[t + 5];
-		bv[5] = pb[t + 5];
+	auto step = [&](int a5, int b5) {
+		av[5] = a5;
+		bv[5] = b5;
 		#pragma unroll
 		for (int n = 0; n < 10; n++) {
 			int lon = ODD ? n / 2 + 1 : (n + 1) / 2;
@@ -1044,7 +1093,20 @@ MD void fc_corr10(const int16_t *in, int hp, int win, Word40 *A)
 			av[k] = av[k + 1];
 			bv[k] = bv[k + 1];
 		}
+	};
+	/* pa[t + 5], pb[t + 5] two at a time (P16) */
+	P16 ra, rb;
+	int np = p16_open(ra, pa + 5, win), nb = p16_open(rb, pb + 5, win);
+	np = np < nb ? np : nb;
+	int t = 0;
+	#pragma unroll 2
+	for (int k = 0; k < np; k++, t += 2) {
+		uint32_t x = p16_next(ra), y = p16_next(rb);
+		step(lo16(x), lo16(y));
+		step(hi16(x), hi16(y));
 	}
+	for (; t < win; t++)
+		step(pa[t + 5], pb[t + 5]);
 	for (int n = 0; n < 10; n++)
 		A[n] = 2 * acc[n];
 }

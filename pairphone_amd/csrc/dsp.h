@@ -16,14 +16,113 @@
 
 namespace mlp {
 
+/*
+ * Paired int16 streams.  The lane's private segment is swizzled per dword
+ * (kern.h), so a 16-bit scratch load costs one VMEM instruction and one
+ * 256-byte row of the wave, exactly like a 32-bit load.  P16 reads an int16
+ * stream p[0], p[1], ... two samples per dword load, which halves the VMEM
+ * instructions (and the rows fetched) of a pass.  A stream that starts at an
+ * odd sample -- a per-lane property, since offsets such as the pitch lag
+ * differ between channels -- is re-aligned with one byte permute.  The
+ * values and their order are unchanged, so every L_mac chain below is the
+ * reference's.
+ */
+MD uint32_t perm_b32(uint32_t hi, uint32_t lo, uint32_t sel)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+	return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+	uint64_t v = ((uint64_t) hi << 32) | lo;
+	uint32_t r = 0;
+	for (int k = 0; k < 4; k++)
+		r |= (uint32_t) ((v >> (8 * ((sel >> (8 * k)) & 7))) & 0xff) << (8 * k);
+	return r;
+#endif
+}
+
+struct P16 {
+	const u32_alias *w;
+	uint32_t prev, sel;
+};
+
+/* Opens the stream p[0..n) and returns how many pairs p16_next may deliver:
+ * n / 2 for an even start, (n - 1) / 2 for an odd one (whose last dword
+ * would straddle the end).  No byte outside p[0..n) is read, so no access
+ * leaves the array the stream lies in; the caller takes the remaining one
+ * to three samples one by one. */
+MD int p16_open(P16 &r, const int16_t *p, int n)
+{
+	int odd = (int) ((reinterpret_cast<uintptr_t>(p) >> 1) & 1);
+	r.w = reinterpret_cast<const u32_alias *>(p + odd);
+	r.prev = (odd && n > 0) ? (uint32_t) (uint16_t) p[0] << 16 : 0u;
+	r.sel = odd ? 0x05040302u : 0x07060504u;
+	int np = (n - odd) >> 1;
+	return np > 0 ? np : 0;
+}
+
+/* the next two samples: p[2k] in the low half, p[2k + 1] in the high half */
+MD uint32_t p16_next(P16 &r)
+{
+	uint32_t cur = *r.w++;
+	uint32_t v = perm_b32(cur, r.prev, r.sel);
+	r.prev = cur;
+	return v;
+}
+
+MD int16_t lo16(uint32_t v) { return (int16_t) (v & 0xffffu); }
+MD int16_t hi16(uint32_t v) { return (int16_t) (v >> 16); }
+
 /* ------------------------------------------------------------------ */
 /* vectors: melpe/mat_lib.c                                           */
 /* ------------------------------------------------------------------ */
 
+/* d[i] = f(s[i]), i ascending: samples read in pairs (P16), written as
+ * dwords after a one-sample head when d starts at an odd sample.  A
+ * destination overlapping the source from above (d in (s, s + n)) gets the
+ * plain loop: there the forward order is what the reference's smearing
+ * copy produces. */
+template <class F>
+MD void v_map(int16_t *d, const int16_t *s, int n, F f)
+{
+	if (d > s && d < s + n) {
+		for (int i = 0; i < n; i++)
+			d[i] = f(s[i]);
+		return;
+	}
+	int i = 0;
+	if (n > 0 && ((reinterpret_cast<uintptr_t>(d) >> 1) & 1)) {
+		d[0] = f(s[0]);
+		i = 1;
+	}
+	P16 r;
+	int np = p16_open(r, s + i, n - i);
+	u32_alias *dw = reinterpret_cast<u32_alias *>(d + i);
+	#pragma unroll 4
+	for (int k = 0; k < np; k++, i += 2) {
+		uint32_t x = p16_next(r);
+		uint32_t y0 = (uint16_t) f(lo16(x));	/* f may carry state: */
+		uint32_t y1 = (uint16_t) f(hi16(x));	/* sample order matters */
+		*dw++ = y0 | (y1 << 16);
+	}
+	for (; i < n; i++)
+		d[i] = f(s[i]);
+}
+
+#ifndef MELPE_VMAP_COPY
+#define MELPE_VMAP_COPY 0
+#endif
+#ifndef MELPE_VMAP_IIR
+#define MELPE_VMAP_IIR 0
+#endif
+
 MD void v_copy(int16_t *d, const int16_t *s, int n)	/* v_equ :136 */
 {
+#if MELPE_VMAP_COPY
+	v_map(d, s, n, [](int16_t x) { return x; });
+#else
 	for (int i = 0; i < n; i++)
 		d[i] = s[i];
+#endif
 }
 
 MD void v_copy32(int32_t *d, const int32_t *s, int n)	/* L_v_equ :237 */
@@ -58,14 +157,22 @@ MD void v_sub(int16_t *a, const int16_t *b, int n)	/* :520 */
 
 MD void v_equ_shr(int16_t *d, const int16_t *s, int16_t sc, int n)	/* :186 */
 {
+#if MELPE_VMAP_COPY
+	v_map(d, s, n, [sc](int16_t x) { return (int16_t) shr(x, sc); });
+#else
 	for (int i = 0; i < n; i++)
 		d[i] = shr(s[i], sc);
+#endif
 }
 
 MD void v_scale(int16_t *a, int16_t sc, int n)	/* :409 */
 {
+#if MELPE_VMAP_COPY
+	v_map(a, a, n, [sc](int16_t x) { return (int16_t) mult(x, sc); });
+#else
 	for (int i = 0; i < n; i++)
 		a[i] = mult(a[i], sc);
+#endif
 }
 
 MD void v_scale_shl(int16_t *a, int16_t sc, int n, int16_t sh)	/* :462 */
@@ -75,14 +182,24 @@ MD void v_scale_shl(int16_t *a, int16_t sc, int n, int16_t sh)	/* :462 */
 }
 
 /* L_v_inner :293 -- sum of products, then shift to the output Q.  The
- * unrolled body issues a batch of loads before the saturating (order
- * dependent, so strictly sequential) accumulation consumes them. */
+ * samples come in pairs (P16) and the unrolled body issues a batch of loads
+ * before the saturating (order dependent, so strictly sequential)
+ * accumulation consumes them. */
 MN Word32 L_v_inner(const int16_t *__restrict__ a, const int16_t *__restrict__ b, int n,
 		    int16_t qa, int16_t qb, int16_t qout)
 {
 	Word32 acc = 0;
+	P16 ra, rb;
+	int np = p16_open(ra, a, n), nb = p16_open(rb, b, n);
+	np = np < nb ? np : nb;
+	int i = 0;
 #pragma unroll 8
-	for (int i = 0; i < n; i++)
+	for (int k = 0; k < np; k++, i += 2) {
+		uint32_t x = p16_next(ra), y = p16_next(rb);
+		acc = L_mac(acc, lo16(x), lo16(y));
+		acc = L_mac(acc, hi16(x), hi16(y));
+	}
+	for (; i < n; i++)
 		acc = L_mac(acc, a[i], b[i]);
 	return L_shl(acc, sub(qout, add(add(qa, qb), 1)));
 }
@@ -91,8 +208,16 @@ MN Word32 L_v_inner(const int16_t *__restrict__ a, const int16_t *__restrict__ b
 MN Word32 L_v_magsq(const int16_t *__restrict__ a, int n, int16_t qa, int16_t qout)
 {
 	Word32 acc = 0;
+	P16 ra;
+	int np = p16_open(ra, a, n);
+	int i = 0;
 #pragma unroll 8
-	for (int i = 0; i < n; i++)
+	for (int k = 0; k < np; k++, i += 2) {
+		uint32_t x = p16_next(ra);
+		acc = L_mac(acc, lo16(x), lo16(x));
+		acc = L_mac(acc, hi16(x), hi16(x));
+	}
+	for (; i < n; i++)
 		acc = L_mac(acc, a[i], a[i]);
 	return L_shl(acc, sub(sub(qout, shl(qa, 1)), 1));
 }
@@ -710,7 +835,8 @@ MD Word16 biq_step(Biq &b, Word16 x)
  * din/dout[2s..2s+1]) run in place on x[0..n), sample by sample.  Section s
  * at sample i depends only on section s-1 at samples <= i and on its own
  * past, so this equals the reference's three sequential in-place calls.
- * Samples move in blocks of 4 (loads issued together, one wait per block).
+ * Samples move in blocks of 4 (loads issued together, one wait per block;
+ * MELPE_VMAP_IIR: in pairs through v_map, measured slower).
  * snap > 0 (a multiple of 4): the memories left behind are those after
  * sample snap-1 -- the reference's filter-then-save-then-restore around a
  * two-part call (melp_ana.c:324-346, pit_lib.c:604-622). */
@@ -730,6 +856,17 @@ MD void iir3_s(int16_t *x, const int16_t *den, const int16_t *num, int16_t *din,
 		b[s].o1 = dout[2 * s + 1];
 	}
 	Biq keep[3];
+#if MELPE_VMAP_IIR
+	auto filt = [&](int16_t v) -> int16_t { return biq_step(b[2], biq_step(b[1], biq_step(b[0], v))); };
+	if (snap > 0) {
+		v_map(x, x, snap, filt);
+		for (int s = 0; s < 3; s++)
+			keep[s] = b[s];
+		v_map(x + snap, x + snap, n - snap, filt);
+	} else {
+		v_map(x, x, n, filt);
+	}
+#else
 	int i = 0;
 	for (; i + 4 <= n; i += 4) {
 		if (i == snap)
@@ -750,6 +887,7 @@ MD void iir3_s(int16_t *x, const int16_t *den, const int16_t *num, int16_t *din,
 			keep[s] = b[s];
 	for (; i < n; i++)
 		x[i] = biq_step(b[2], biq_step(b[1], biq_step(b[0], x[i])));
+#endif
 	for (int s = 0; s < 3; s++) {
 		const Biq &o = snap > 0 ? keep[s] : b[s];
 		din[2 * s] = o.i0;
@@ -805,6 +943,11 @@ MD void iir3_d(const int16_t *in, int16_t *out, const int16_t *den, const int16_
 		b[s].l0 = dlo[2 * s];
 		b[s].l1 = dlo[2 * s + 1];
 	}
+#if MELPE_VMAP_IIR
+	v_map(out, in, n, [&](int16_t v) -> int16_t {
+		return biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], v)));
+	});
+#else
 	int i = 0;
 	for (; i + 4 <= n; i += 4) {
 		int16_t v0 = in[i], v1 = in[i + 1], v2 = in[i + 2], v3 = in[i + 3];
@@ -815,6 +958,7 @@ MD void iir3_d(const int16_t *in, int16_t *out, const int16_t *den, const int16_
 	}
 	for (; i < n; i++)
 		out[i] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], in[i])));
+#endif
 	for (int s = 0; s < 3; s++) {
 		din[2 * s] = b[s].i0;
 		din[2 * s + 1] = b[s].i1;
@@ -860,6 +1004,9 @@ MD void iir2_d(int16_t *x, const int16_t *den1, const int16_t *num1, int16_t *di
 	Biqd a, b;
 	biqd_load(a, den1, num1, din1, dhi1, dlo1);
 	biqd_load(b, den2, num2, din2, dhi2, dlo2);
+#if MELPE_VMAP_IIR
+	v_map(x, x, n, [&](int16_t v) -> int16_t { return biqd_step(b, biqd_step(a, v)); });
+#else
 	int i = 0;
 	for (; i + 4 <= n; i += 4) {
 		int16_t v0 = x[i], v1 = x[i + 1], v2 = x[i + 2], v3 = x[i + 3];
@@ -870,6 +1017,7 @@ MD void iir2_d(int16_t *x, const int16_t *den1, const int16_t *num1, int16_t *di
 	}
 	for (; i < n; i++)
 		x[i] = biqd_step(b, biqd_step(a, x[i]));
+#endif
 	biqd_store(a, din1, dhi1, dlo1);
 	biqd_store(b, din2, dhi2, dlo2);
 }
@@ -877,6 +1025,48 @@ MD void iir2_d(int16_t *x, const int16_t *den1, const int16_t *num1, int16_t *di
 /* ------------------------------------------------------------------ */
 /* LPC: melpe/lpc_lib.c                                               */
 /* ------------------------------------------------------------------ */
+
+#define LPC_ACOR_MAX 16
+
+/* The lag sums of lpc_acor in one pass over the samples: sample i adds
+ * w[i] * w[i - j] to lag j (j = 1..ORD), the last ORD samples held in
+ * registers.  Each lag's saturating chain still runs in ascending i, as the
+ * reference's per-lag loop (lpc_lib.c:146-152); the missing terms of the
+ * first ORD samples are L_mac(acc, x, 0), which leaves acc unchanged. */
+template <int ORD>
+MD void acor_lags(const int16_t *w, int n, Word32 *lags)
+{
+	Word32 acc[ORD];
+	int16_t h[ORD];	/* h[k] = w[i - 1 - k] */
+	#pragma unroll
+	for (int k = 0; k < ORD; k++) {
+		acc[k] = 0;
+		h[k] = 0;
+	}
+	auto step = [&](int16_t x) {
+		#pragma unroll
+		for (int k = 0; k < ORD; k++)
+			acc[k] = L_mac(acc[k], x, h[k]);
+		#pragma unroll
+		for (int k = ORD - 1; k > 0; k--)
+			h[k] = h[k - 1];
+		h[0] = x;
+	};
+	P16 r;
+	int np = p16_open(r, w, n);
+	int i = 0;
+	#pragma unroll 2
+	for (int k = 0; k < np; k++, i += 2) {
+		uint32_t x = p16_next(r);
+		step(lo16(x));
+		step(hi16(x));
+	}
+	for (; i < n; i++)
+		step(w[i]);
+	#pragma unroll
+	for (int k = 0; k < ORD; k++)
+		lags[k + 1] = acc[k];
+}
 
 /* lpc_acor :93 -- windowed, normalised autocorrelation with lag window */
 MN void lpc_acor(const int16_t *in, const int16_t *win, int16_t *r,
@@ -915,10 +1105,23 @@ MN void lpc_acor(const int16_t *in, const int16_t *win, int16_t *r,
 		r[0] = SW_MAX_;
 		sf = 0;
 	}
+	Word32 lags[LPC_ACOR_MAX + 1];
+#if defined(MELPE_OPCOUNT)
+	/* census build: the reference's per-lag loops */
 	for (int j = 1; j <= order; j++) {
 		Word32 acc = 0;
 		for (int i = j; i < n; i++)
 			acc = L_mac(acc, w[i], w[i - j]);
+		lags[j] = acc;
+	}
+#else
+	if (order == 16)
+		acor_lags<16>(w, n, lags);
+	else
+		acor_lags<10>(w, n, lags);
+#endif
+	for (int j = 1; j <= order; j++) {
+		Word32 acc = lags[j];
 		acc = L_shl(acc, nv);
 		acc = L_shl(L_mpy_ls(acc, sf), 1);
 		acc = L_mpy_ls(acc, lagw[j - 1]);

@@ -114,6 +114,18 @@ struct ProfScope {
  * NPP state image) move int16/int32/uint8 fields as dwords */
 typedef uint32_t __attribute__((__may_alias__)) u32_alias;
 
+/* the value of the first active lane (device), for waterfall loops over the
+ * distinct values a lane-varying operand takes; the host build runs one
+ * channel, whose value it is */
+MD int wave_first(int v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+	return __builtin_amdgcn_readfirstlane(v);
+#else
+	return v;
+#endif
+}
+
 typedef int16_t Word16;
 typedef int32_t Word32;
 typedef int64_t Word40;

@@ -94,26 +94,35 @@ MN void wvq1(const int16_t *tgt_in, const int16_t *wt_in, const int16_t *cb, int
 		dist[j] = LW_MAX_;
 	Word32 maxd = LW_MAX_;
 	int maxi = 0;
-	for (int i = 0; i < cbsize; i++) {
-		Word32 err = 0;
-		for (int j = 0; j < dim; j++)
-			if (wt[j] > 0) {
-				Word16 t = sub(tgt[j], cb[j]);
-				err = L_add(err, L_shr(L_mult(t, t), 2));
-				if (err >= maxd)
-					break;
-			}
-		if (err < maxd) {
-			index[maxi] = (int16_t) i;
-			dist[maxi] = err;
-			maxd = 0;
-			for (int j = 0; j < cand; j++)
-				if (dist[j] > maxd) {
-					maxd = dist[j];
-					maxi = j;
+	/* one scan per distinct (codebook, size) among the active lanes, both
+	 * wave-uniform inside: rows through the scalar cache (lspVQ_t) */
+	const int o_lane = (int) (cb - g_tab);
+	for (;;) {
+		const int uo = wave_first(o_lane), un = wave_first(cbsize);
+		if (o_lane != uo || cbsize != un)
+			continue;
+		const int16_t *ucb = g_tab + uo;
+		for (int i = 0; i < un; i++) {
+			Word32 err = 0;
+			for (int j = 0; j < dim; j++)
+				if (wt[j] > 0) {
+					Word16 t = sub(tgt[j], ucb[i * DIM + j]);
+					err = L_add(err, L_shr(L_mult(t, t), 2));
+					if (err >= maxd)
+						break;
 				}
+			if (err < maxd) {
+				index[maxi] = (int16_t) i;
+				dist[maxi] = err;
+				maxd = 0;
+				for (int j = 0; j < cand; j++)
+					if (dist[j] > maxd) {
+						maxd = dist[j];
+						maxi = j;
+					}
+			}
 		}
-		cb += dim;
+		break;
 	}
 }
 
@@ -378,22 +387,36 @@ MD void lspVQ_t(const int16_t *target, const int16_t *weight, int16_t *qout, con
 #pragma unroll
 			for (int i = 0; i < DIM; i++)
 				ct[i] = sub(target[i], cand[c1][i]);
-			for (int e = 0; e < cb_size[s1]; e++) {
-				Word16 d = WeightedMSE_t<DIM>(wr, cbp + off, ct, maxd);
-				if (d < maxd) {
-					int32_t nt = (c1 << 16) | e;
+			/* The codebook rows are the same for every lane that scans
+			 * this stage, so the scan runs once per distinct (codebook
+			 * offset, size) among the active lanes -- once, unless the
+			 * lanes took different branches of lsf_vq -- with both values
+			 * wave-uniform: the rows then come through the scalar cache
+			 * instead of per-lane vector loads. */
+			const int o_lane = (int) (cbp - g_tab), n_lane = cb_size[s1];
+			for (;;) {
+				const int uo = wave_first(o_lane), un = wave_first(n_lane);
+				if (o_lane != uo || n_lane != un)
+					continue;
+				const int16_t *ucb = g_tab + uo;
+				for (int e = 0; e < un; e++) {
+					Word16 d = WeightedMSE_t<DIM>(wr, ucb + e * DIM, ct, maxd);
+					if (d < maxd) {
+						int32_t nt = (c1 << 16) | e;
 #pragma unroll
-					for (int k = LSP_VQ_CAND - 1; k >= 0; k--) {
-						bool keep = dm[k] < d;
-						bool prev = k == 0 || dm[k > 0 ? k - 1 : 0] < d;
-						int16_t pd = k > 0 ? dm[k - 1] : d;
-						int32_t pt = k > 0 ? tag[k - 1] : nt;
-						dm[k] = keep ? dm[k] : (prev ? d : pd);
-						tag[k] = keep ? tag[k] : (prev ? nt : pt);
+						for (int k = LSP_VQ_CAND - 1; k >= 0; k--) {
+							bool keep = dm[k] < d;
+							bool prev = k == 0 || dm[k > 0 ? k - 1 : 0] < d;
+							int16_t pd = k > 0 ? dm[k - 1] : d;
+							int32_t pt = k > 0 ? tag[k - 1] : nt;
+							dm[k] = keep ? dm[k] : (prev ? d : pd);
+							tag[k] = keep ? tag[k] : (prev ? nt : pt);
+						}
+						maxd = dm[LSP_VQ_CAND - 1];
 					}
-					maxd = dm[LSP_VQ_CAND - 1];
+					off = add(off, (Word16) dim);
 				}
-				off = add(off, (Word16) dim);
+				break;
 			}
 		}
 		{
