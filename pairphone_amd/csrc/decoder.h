@@ -714,6 +714,21 @@ MD void derive_idft_cos(DerivedTables *d)
 			d->idft_cos[len][i] = idft_cos_entry((Word16) len, i);
 }
 
+/* Where realIDFT reads its cosine rows.  Lane-mode synthesis gathers one
+ * entry per lane per harmonic, each lane from the row of its own period
+ * length: through the vector memory path that is up to 64 cache lines per
+ * instruction (the texture addresser's rate, not HBM, bounds it).  k_dec.hip
+ * (MELPE_IDFT_LDS) stages the table packed in the block's LDS instead -- row
+ * len at (len - 1) * len / 2, 12,880 entries, 25.8 KB shared by the block's
+ * four waves -- where a gather costs bank cycles.  Elsewhere: g_der. */
+#define IDFT_LDS_WORDS (PITCHMAX * (PITCHMAX + 1) / 2)
+#if defined(MELPE_IDFT_LDS)
+extern __shared__ int16_t s_idft_cos[];
+#define IDFT_ROW(len) (s_idft_cos + (((len) - 1) * (len)) / 2)
+#else
+#define IDFT_ROW(len) (g_der.idft_cos[len])
+#endif
+
 /* realIDFT :63 -- direct real inverse DFT of one pitch period.  The
  * reference steps the cosine index k by adding phase[j], wrapping into
  * [0, len), then subtracting phase[j] and adding i, so before harmonic j
@@ -732,7 +747,7 @@ MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 		cbuf[i] = idft_cos_entry_w(w, i);
 	const int16_t *c = cbuf;
 #else
-	const int16_t *c = g_der.idft_cos[len];
+	const int16_t *c = IDFT_ROW(len);
 	int16_t phm[PITCHMAX / 2 + 1];	/* phase[j] mod len, in [0, len) */
 	for (int j = 1; j < len2; j++) {
 		int p = phase[j] % len;

@@ -2,9 +2,14 @@
  * k_dec.hip -- melpe_s (melpe/melpe.c:102-107): channel read, synthesis and
  * postfilter of one superframe per active channel, one lane per channel.
  */
+#define MELPE_IDFT_LDS	/* realIDFT's table from LDS (decoder.h) */
 #include "kern.h"
 
 MELPE_TU(dec)
+
+/* up to four waves per block share one LDS copy of the realIDFT table;
+ * kl_decode picks the widest block that still gives every CU four blocks */
+#define DEC_BLOCK 256
 
 struct DecLane {
 	uint8_t guard[FLAT_GUARD_BYTES];
@@ -12,10 +17,14 @@ struct DecLane {
 	int16_t out[BLOCK];
 };
 
-__global__ __launch_bounds__(WAVE, MELPE_DEC_WAVES) void k_decode(DecState *dec, int16_t *sp, const uint8_t *bits,
-						 const uint8_t *active, int n)
+__global__ __launch_bounds__(DEC_BLOCK, MELPE_DEC_WAVES) void k_decode(DecState *dec, int16_t *sp,
+						      const uint8_t *bits, const uint8_t *active, int n)
 {
-	int c = blockIdx.x * WAVE + threadIdx.x;
+	for (int len = 1; len <= PITCHMAX; len++)
+		for (int i = threadIdx.x; i < len; i += blockDim.x)
+			s_idft_cos[((len - 1) * len) / 2 + i] = g_der.idft_cos[len][i];
+	__syncthreads();
+	int c = blockIdx.x * blockDim.x + threadIdx.x;
 	if (c >= n || (active && !active[c]))
 		return;
 	DecLane L;
@@ -31,6 +40,9 @@ __global__ __launch_bounds__(WAVE, MELPE_DEC_WAVES) void k_decode(DecState *dec,
 extern "C" int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active,
 			 int n, hipStream_t s)
 {
-	k_decode<<<grid_for(n), WAVE, 0, s>>>(dec, sp, bits, active, n);
+	int b = DEC_BLOCK;
+	while (b > WAVE && (n + b - 1) / b < 1024)
+		b /= 2;
+	k_decode<<<(n + b - 1) / b, b, IDFT_LDS_WORDS * sizeof(int16_t), s>>>(dec, sp, bits, active, n);
 	return (int) hipGetLastError();
 }

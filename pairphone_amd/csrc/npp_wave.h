@@ -542,36 +542,45 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	PROF_SCOPE(37);
 	int gk0 = gk[lane], gk1 = gk[lane + 64], gk2 = gk[NPP_NB - 1];
 	int gs0 = gks[lane], gs1 = gks[lane + 64], gs2 = gks[NPP_NB - 1];
-	int acc = 0, sh2 = 0;		/* L, sh of the reference */
-	int mn = 0, ms = 0;		/* gmax, gmaxs */
-	for (int i = 0; i < NPP_NB; i++) {
-		int g = bin_at(gk0, gk1, gk2, i);
-		int e = bin_at(gs0, gs1, gs2, i);
-		if (i == 0) {
-			acc = g << 7;
-			sh2 = e - 1;
-			mn = g;
-			ms = e;
-			continue;
-		}
+	int acc, sh2;		/* L, sh of the reference */
+	int mn, ms;		/* gmax, gmaxs */
+	{
+		int g = __builtin_amdgcn_readlane(gk0, 0), e = __builtin_amdgcn_readlane(gs0, 0);
+		acc = g << 7;
+		sh2 = e - 1;
+		mn = g;
+		ms = e;
+	}
+	/* one bin: branch-free (selects), shift counts clamped to 31 where the
+	 * reference's saturating shift would give 0 (operands are >= 0) */
+	auto shc = [](int k) { return k < 0 ? 0 : (k > 31 ? 31 : k); };
+	auto step = [&](int g, int e, int ee) {
 		/* cmp_shift(gmax, gmaxs, g, e) < 0 for non-negative mantissas:
 		 * the value with the smaller exponent truncated to the larger */
 		int d = ms - e;
-		int a1 = d > 0 ? mn : (d <= -15 ? 0 : mn >> -d);
-		int b1 = d > 0 ? (d >= 15 ? 0 : g >> d) : g;
+		int a1 = d > 0 ? mn : mn >> shc(-d);
+		int b1 = d > 0 ? g >> shc(d) : g;
 		bool take = a1 < b1;
 		mn = take ? g : mn;
 		ms = take ? e : ms;
-		int ee = (i == NPP_NB - 1) ? e - 1 : e;
 		int t = sh2 - ee;
-		if (t > 0) {
-			int n = t - 7;	/* L_shr(gk, t - 7), no saturation for t >= 1 */
-			acc += n >= 0 ? (n >= 31 ? 0 : g >> n) : g << -n;
-		} else {
-			acc = (-t >= 31 ? 0 : acc >> -t) + (g << 7);
-			sh2 = ee;
-		}
+		int n = t - 7;	/* L_shr(gk, t - 7), no saturation for t >= 1 */
+		int term = n >= 0 ? g >> shc(n) : g << shc(-n);
+		int accb = (acc >> shc(-t)) + (g << 7);
+		acc = t > 0 ? acc + term : accb;
+		sh2 = t > 0 ? sh2 : ee;
+	};
+	#pragma unroll 2
+	for (int i = 1; i < 64; i++) {
+		int e = __builtin_amdgcn_readlane(gs0, i);
+		step(__builtin_amdgcn_readlane(gk0, i), e, e);
 	}
+	#pragma unroll 2
+	for (int i = 0; i < 64; i++) {
+		int e = __builtin_amdgcn_readlane(gs1, i);
+		step(__builtin_amdgcn_readlane(gk1, i), e, e);
+	}
+	step(gk2, gs2, gs2 - 1);
 	L = acc;
 	sh = (Word16) sh2;
 	if (L == 0)
