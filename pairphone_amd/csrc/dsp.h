@@ -97,13 +97,24 @@ MD void v_map(int16_t *d, const int16_t *s, int n, F f)
 	P16 r;
 	int np = p16_open(r, s + i, n - i);
 	u32_alias *dw = reinterpret_cast<u32_alias *>(d + i);
-	#pragma unroll 4
-	for (int k = 0; k < np; k++, i += 2) {
-		uint32_t x = p16_next(r);
+	auto put = [&](uint32_t x) {
 		uint32_t y0 = (uint16_t) f(lo16(x));	/* f may carry state: */
 		uint32_t y1 = (uint16_t) f(hi16(x));	/* sample order matters */
 		*dw++ = y0 | (y1 << 16);
+	};
+	/* four pairs loaded before any is stored: the stores may alias the
+	 * source (in place, or d below s), so the compiler could not hoist the
+	 * next loads over them; reading ahead is safe for both cases */
+	int k = 0;
+	for (; k + 4 <= np; k += 4, i += 8) {
+		uint32_t x0 = p16_next(r), x1 = p16_next(r), x2 = p16_next(r), x3 = p16_next(r);
+		put(x0);
+		put(x1);
+		put(x2);
+		put(x3);
 	}
+	for (; k < np; k++, i += 2)
+		put(p16_next(r));
 	for (; i < n; i++)
 		d[i] = f(s[i]);
 }

@@ -62,6 +62,31 @@ def main():
             for n, calls, tot, avg, pct in rows:
                 f.write("%-14s %6d %14.1f %12.1f %7.2f\n" % (short(n)[:14], calls, tot / 1e3,
                                                            avg / 1e3, pct))
+            # the bench's legs launch the same kernels at different sizes:
+            # per launch size (grid_x = threads = channels, or waves x 64 for
+            # the wave-per-channel kernels), so a leg's HIP-event average can
+            # be checked against the trace
+            f.write("\n# per launch size (grid_x threads); durations in ms\n")
+            f.write("%-14s %10s %6s %12s %10s\n" % ("kernel", "grid_x", "calls", "total_ms", "avg_ms"))
+            c = sqlite3.connect(kt[0])
+            for n, gx, calls, tot in c.execute(
+                    "select name, grid_x, count(*), sum(duration) from kernels "
+                    "where name like 'k_%' group by name, grid_x order by sum(duration) desc"):
+                if short(n).startswith("k_derive"):
+                    continue
+                f.write("%-14s %10d %6d %12.1f %10.3f\n" % (short(n)[:14], gx, calls, tot / 1e6,
+                                                           tot / 1e6 / calls))
+            # dispatch by dispatch for the short series (the bench's main
+            # loop: W warmup then K timed steps, whose mean is its kernel_ms)
+            f.write("\n# dispatches in order, series of <= 16 (ms)\n")
+            for n, gx in list(c.execute("select name, grid_x from kernels where name like 'k_%' "
+                                        "group by name, grid_x having count(*) <= 16")):
+                if short(n).startswith(("k_derive", "k_reset", "k_synth_seed", "k_vad_reset",
+                                        "k_modem_reset")):
+                    continue
+                d = [r[0] / 1e6 for r in c.execute("select duration from kernels where name = ? and "
+                                                   "grid_x = ? order by start", (n, gx))]
+                f.write("%-14s %10d %s\n" % (short(n)[:14], gx, " ".join("%.2f" % x for x in d)))
     pm = {}
     if len(sys.argv) <= 3:	# PMC summaries only with the channel count they were taken at
         return
