@@ -149,6 +149,28 @@ MD void q_bpvc_dec(int16_t *bpvc, Word16 idx, int16_t uv, int nb)
 /* melpe/pit_lib.c                                                    */
 /* ------------------------------------------------------------------ */
 
+/* f_pitch_scale's second half, given the window's exact energy (the sum of
+ * L_mult(x, x), in 64 bits): callers that produce the window can add its
+ * energy up while they write it (bpvc_ana) */
+MD Word16 f_pitch_scale_e(int16_t *out, const int16_t *in, int len, int64_t sum)
+{
+	Word16 sc = 0;
+	/* Every term L_mult(x, x) is >= 0, so the reference's running margin
+	 * test (:193-203) fails exactly when the running sum first exceeds
+	 * LW_MAX, i.e. iff the whole 64-bit sum does; without it L_add never
+	 * saturates and the sum is exact. */
+	Word32 corr = (Word32) sum;
+	if (sum > (int64_t) LW_MAX_) {
+		int16_t tb[PITCH_FR + 8];
+		sc = 5;
+		v_equ_shr(tb, in, sc, len);
+		corr = L_v_magsq(tb, len, 0, 1);
+	}
+	sc = sub(sc, shr(norm_l(corr), 1));
+	v_equ_shr(out, in, sc, len);
+	return sc;
+}
+
 /* f_pitch_scale :178 -- scale so the energy fits, returns the shift */
 MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 {
@@ -172,10 +194,7 @@ MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 		corr = sum;
 	}
 #else
-	/* Every term L_mult(x, x) is >= 0, so the reference's running margin
-	 * test (:193-203) fails exactly when the running sum first exceeds
-	 * LW_MAX, i.e. iff the whole 64-bit sum does; without it L_add never
-	 * saturates and the sum is exact.  One pass, no data-dependent exit. */
+	/* the energy in one pass, no data-dependent exit (f_pitch_scale_e) */
 	{
 		int64_t sum = 0;
 		P16 r;
@@ -189,8 +208,7 @@ MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 		}
 		for (; i < len; i++)
 			sum += L_mult(in[i], in[i]);
-		ovf = sum > (int64_t) LW_MAX_;
-		corr = (Word32) sum;
+		return f_pitch_scale_e(out, in, len, sum);
 	}
 #endif
 	if (ovf) {
@@ -571,6 +589,8 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 /* ------------------------------------------------------------------ */
 /* bpvc_ana, melpe/melp_sub.c:77 -- 5-band bandpass voicing           */
 /* ------------------------------------------------------------------ */
+#if defined(MELPE_OPCOUNT)
+/* census build: the reference's pass structure, op for op */
 MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
 		 Word16 *pitch)
 {
@@ -627,6 +647,87 @@ MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int1
 			bpvc[i] = pcorr;
 	}
 }
+
+#else
+
+/* One band's pitch window w[0..PITCH_FR) (w = &sb[BPF_ORD]): the band's
+ * filtered history bpfsp, then the new frame sp[0..FRAME) through the
+ * band's three biquads, the new history written back as it is produced --
+ * the reference's copy / iir / copy / f_pitch_scale-energy passes
+ * (melp_sub.c:95-110, pit_lib.c:186-203) as one pass over the samples.
+ * Returns the window's energy for f_pitch_scale_e. */
+MD int64_t bp_window(int16_t *hist, const int16_t *sp, int16_t *w, const int16_t *den,
+		     const int16_t *num, int16_t *din, int16_t *dout)
+{
+	const int H = PITCH_FR - FRAME;	/* 141 */
+	int64_t e = 0;
+	for (int k = 0; k < H; k++) {
+		int16_t v = hist[k];
+		w[k] = v;
+		e += L_mult(v, v);
+	}
+	iir3_s_io(sp, w + H, den, num, din, dout, FRAME, [&](int n, int16_t y) {
+		e += L_mult(y, y);
+		if (n >= FRAME - H)
+			hist[n - (FRAME - H)] = y;
+	});
+	return e;
+}
+
+/* bpvc_ana, melpe/melp_sub.c:77 */
+MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
+		 Word16 *pitch)
+{
+	PROF_SCOPE(4);
+	int16_t sb[BPF_ORD + PITCH_FR];
+	Word16 pcorr, t, sc;
+	const int16_t *bden = TB(bpf_den), *bnum = TB(bpf_num);
+	if (!E->bp_started) {
+		for (int i = 0; i < NUM_BANDS; i++) {
+			v_zero(E->bpfsp[i], PITCH_FR - FRAME);
+			v_zero(E->bpfdelin[i], BPF_ORD);
+			v_zero(E->bpfdelout[i], BPF_ORD);
+			v_zero(E->envdel[i], ENV_ORD);
+		}
+		v_zero(E->envdel2, NUM_BANDS);
+		E->bp_started = 1;
+	}
+	const int16_t *sp = &speech[PITCH_FR - FRAME - PITCHMAX];
+	int16_t *w = &sb[BPF_ORD];
+	int64_t e = bp_window(E->bpfsp[0], sp, w, bden, bnum, E->bpfdelin[0], E->bpfdelout[0]);
+	f_pitch_scale_e(w, w, PITCH_FR, e);
+	*pitch = frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[0], fpitch[0], 5, PITCHMIN, PITCHMAX,
+			  PITCHMIN_Q7, PITCHMAX_Q7, 160);
+	for (int i = 1; i < 2; i++) {	/* NUM_PITCHES */
+		t = frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, fpitch[i], 5, PITCHMIN, PITCHMAX,
+			     PITCHMIN_Q7, PITCHMAX_Q7, 160);
+		if (pcorr > bpvc[0]) {
+			*pitch = t;
+			bpvc[0] = pcorr;
+		}
+	}
+	for (int i = 1; i < NUM_BANDS; i++) {
+		int fi = i * (BPF_ORD / 2) * 3;
+		e = bp_window(E->bpfsp[i], sp, w, bden + fi, bnum + fi, E->bpfdelin[i], E->bpfdelout[i]);
+		sc = f_pitch_scale_e(w, w, PITCH_FR, e);
+		frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[i], *pitch, 0, PITCHMIN, PITCHMAX,
+			 PITCHMIN_Q7, PITCHMAX_Q7, 160);
+		/* envelope: the history samples are re-scaled to this frame's scale */
+		t = shr(E->envdel2[i], sc);
+		E->envdel2[i] = shr(sb[BPF_ORD + FRAME - 1], (Word16) -sc);
+		v_equ_shr(&sb[BPF_ORD - ENV_ORD], E->envdel[i], sc, ENV_ORD);
+		e = envelope_e(w, t, w, PITCH_FR);
+		v_equ_shr(E->envdel[i], &sb[BPF_ORD + FRAME - ENV_ORD], (Word16) -sc, ENV_ORD);
+		f_pitch_scale_e(w, w, PITCH_FR, e);
+		frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, *pitch, 0, PITCHMIN, PITCHMAX,
+			 PITCHMIN_Q7, PITCHMAX_Q7, 160);
+		pcorr = sub(pcorr, 1638);
+		if (pcorr > bpvc[i])
+			bpvc[i] = pcorr;
+	}
+}
+
+#endif
 
 /* ------------------------------------------------------------------ */
 /* melpe/pitch.c -- 8-candidate pitch tracker                          */
@@ -688,17 +789,37 @@ MN void ivfilt(int16_t *iv, const int16_t *lp, int len)
 	int16_t rc[3];
 	Word16 pc1, pc2;
 	v_copy(iv, &iv[len], PIT_COR_LEN - len);
-	Word40 acc = 0;
-	for (int i = 0; i < PIT_COR_LEN; i++)
-		acc = L40_mac(acc, lp[i], lp[i]);
-	Word16 sh = norm32(acc);
-	rc[0] = r_ound((Word32) L40_shl(acc, sh));
-	for (int i = 1; i < 3; i++) {
-		acc = 0;
-		for (int j = i; j < PIT_COR_LEN; j++)
-			acc = L40_mac(acc, lp[j], lp[j - i]);
-		rc[i] = r_ound((Word32) L40_shl(acc, sh));
+	/* the reference's three autocorrelation sums (lags 0, 1, 2) in one pass
+	 * over lp, the samples in pairs (P16); each sum keeps its own chain in
+	 * index order and the same terms */
+	Word40 a0 = L40_mac(0, lp[0], lp[0]);
+	Word40 a1 = L40_mac(0, lp[1], lp[0]);
+	a0 = L40_mac(a0, lp[1], lp[1]);
+	Word40 a2 = 0;
+	{
+		int16_t h1 = lp[1], h2 = lp[0];	/* lp[j - 1], lp[j - 2] */
+		auto step = [&](int16_t x) {
+			a0 = L40_mac(a0, x, x);
+			a1 = L40_mac(a1, x, h1);
+			a2 = L40_mac(a2, x, h2);
+			h2 = h1;
+			h1 = x;
+		};
+		P16 r;
+		int np = p16_open(r, lp + 2, PIT_COR_LEN - 2);
+		int j = 2;
+		for (int k = 0; k < np; k++, j += 2) {
+			uint32_t x = p16_next(r);
+			step(lo16(x));
+			step(hi16(x));
+		}
+		for (; j < PIT_COR_LEN; j++)
+			step(lp[j]);
 	}
+	Word16 sh = norm32(a0);
+	rc[0] = r_ound((Word32) L40_shl(a0, sh));
+	rc[1] = r_ound((Word32) L40_shl(a1, sh));
+	rc[2] = r_ound((Word32) L40_shl(a2, sh));
 	if (rc[0] == 0) {
 		pc1 = pc2 = 0;
 	} else {

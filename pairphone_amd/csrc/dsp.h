@@ -440,6 +440,27 @@ MN void envelope(const int16_t *in, int16_t prev_in, int16_t *out, int n)
 	}
 }
 
+/* envelope, returning the exact energy (sum of L_mult(y, y)) of what it
+ * wrote, for f_pitch_scale_e (bpvc_ana) */
+MD int64_t envelope_e(const int16_t *in, int16_t prev_in, int16_t *out, int n)
+{
+	Word16 pa = abs_s(prev_in), y1 = out[-1], y2 = out[-2];
+	int64_t e = 0;
+	for (int i = 0; i < n; i++) {
+		Word16 ca = abs_s(in[i]);
+		Word32 acc = L_shr(L_deposit_h(sub(ca, pa)), 5);
+		acc = L_mac(acc, 31565, y1);
+		acc = L_mac(acc, -15415, y2);
+		Word16 y = r_ound(L_shl(acc, 1));
+		out[i] = y;
+		e += L_mult(y, y);
+		y2 = y1;
+		y1 = y;
+		pa = ca;
+	}
+	return e;
+}
+
 /* interp_array :113 */
 MD void interp_array(const int16_t *prev, const int16_t *curr, int16_t *out,
 		     int16_t f, int n)
@@ -905,6 +926,47 @@ MD void iir3_s(int16_t *x, const int16_t *den, const int16_t *num, int16_t *din,
 		din[2 * s + 1] = o.i1;
 		dout[2 * s] = o.o0;
 		dout[2 * s + 1] = o.o1;
+	}
+}
+
+/* iir3_s from in[] to out[] (no snapshot), handing each output to
+ * f(i, y) as it is produced (bpvc_ana's fused window pass) */
+template <class F>
+MD void iir3_s_io(const int16_t *in, int16_t *out, const int16_t *den, const int16_t *num,
+		  int16_t *din, int16_t *dout, int n, F f)
+{
+	Biq b[3];
+	for (int s = 0; s < 3; s++) {
+		b[s].n0 = num[3 * s];
+		b[s].n1 = num[3 * s + 1];
+		b[s].n2 = num[3 * s + 2];
+		b[s].d1 = den[3 * s + 1];
+		b[s].d2 = den[3 * s + 2];
+		b[s].i0 = din[2 * s];
+		b[s].i1 = din[2 * s + 1];
+		b[s].o0 = dout[2 * s];
+		b[s].o1 = dout[2 * s + 1];
+	}
+	int i = 0;
+	for (; i + 4 <= n; i += 4) {
+		int16_t v[4] = {in[i], in[i + 1], in[i + 2], in[i + 3]};
+		#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			int16_t y = biq_step(b[2], biq_step(b[1], biq_step(b[0], v[q])));
+			out[i + q] = y;
+			f(i + q, y);
+		}
+	}
+	for (; i < n; i++) {
+		int16_t y = biq_step(b[2], biq_step(b[1], biq_step(b[0], in[i])));
+		out[i] = y;
+		f(i, y);
+	}
+	for (int s = 0; s < 3; s++) {
+		din[2 * s] = b[s].i0;
+		din[2 * s + 1] = b[s].i1;
+		dout[2 * s] = b[s].o0;
+		dout[2 * s + 1] = b[s].o1;
 	}
 }
 
