@@ -268,6 +268,56 @@ MD void fp_corr8(const int16_t *pa, const int16_t *pb, int len, Word32 *out)
 		out[k] = acc[k];
 }
 
+/* fp_corr8 for a block of K lags (K even or odd): lag n0 + k reads
+ * pa[j + (k + 1) / 2] * pb[j + (k + 1) / 2 - k + BMAX], BMAX = (K - 1) - K / 2,
+ * from the bases a = cb_n0 and b = cb_(n0+K-1) + i_(n0+K-1).  find_pitch's
+ * +-5 lag searches are 11 lags or fewer: one pass of K = 12 covers them all
+ * (the reads of the unused lags stay inside the window the real lags span). */
+template <int K>
+MD void fp_corrK(const int16_t *pa, const int16_t *pb, int len, Word32 *out)
+{
+	constexpr int NA = K / 2 + 1, BMAX = (K - 1) - K / 2;
+	Word32 acc[K];
+	int16_t A[NA], B[BMAX + 1];
+	#pragma unroll
+	for (int k = 0; k < K; k++)
+		acc[k] = 0;
+	#pragma unroll
+	for (int q = 0; q < NA - 1; q++)
+		A[q] = pa[q];
+	#pragma unroll
+	for (int q = 0; q < BMAX; q++)
+		B[q] = pb[q];
+	auto step = [&](int16_t an, int16_t bn) {
+		A[NA - 1] = an;
+		B[BMAX] = bn;
+		#pragma unroll
+		for (int k = 0; k < K; k++)
+			acc[k] = L_mac(acc[k], A[(k + 1) / 2], B[(k + 1) / 2 - k + BMAX]);
+		#pragma unroll
+		for (int q = 0; q < NA - 1; q++)
+			A[q] = A[q + 1];
+		#pragma unroll
+		for (int q = 0; q < BMAX; q++)
+			B[q] = B[q + 1];
+	};
+	P16 ra, rb;
+	int np = p16_open(ra, pa + NA - 1, len), nb = p16_open(rb, pb + BMAX, len);
+	np = np < nb ? np : nb;
+	int j = 0;
+	#pragma unroll 2
+	for (int k = 0; k < np; k++, j += 2) {
+		uint32_t x = p16_next(ra), y = p16_next(rb);
+		step(lo16(x), lo16(y));
+		step(hi16(x), hi16(y));
+	}
+	for (; j < len; j++)
+		step(pa[j + NA - 1], pb[j + BMAX]);
+	#pragma unroll
+	for (int k = 0; k < K; k++)
+		out[k] = acc[k];
+}
+
 /* find_pitch :240 -- normalised autocorrelation lag search, lags upper..lower */
 MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upper, Word16 len)
 {
@@ -281,16 +331,29 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 	Word32 cTT = L_v_magsq(&sig[cb + upper], len, 0, 1);
 	Word32 blk[8];
 	int nlags = upper - lower + 1;
+#if !defined(MELPE_OPCOUNT)
+	/* up to 12 lags (every +-5 search): all of them in one pass */
+	Word32 blk12[12];
+	const bool one = nlags <= 12;
+	if (one)
+		fp_corrK<12>(&sig[cb0], &sig[cb0 + 6 + upper - 11], len, blk12);
+#else
+	const bool one = false;
+	Word32 *blk12 = blk;
+#endif
 	for (Word16 i = upper; i >= lower; i--) {
 		int n = upper - i;
 		Word32 corr;
-		if ((n & 7) == 0 && n + 8 <= nlags) {
+		if (one) {
+			corr = blk12[n];
+		} else if ((n & 7) == 0 && n + 8 <= nlags) {
 			/* the block's bases: a at cb_n0, b at cb_(n0+7) + i_(n0+7) */
 			int c_n0 = cb0 + (n + 1) / 2;
 			int b0 = cb0 + (n + 8) / 2 + upper - n - 7;
 			fp_corr8(&sig[c_n0], &sig[b0], len, blk);
 		}
-		if (n < (nlags & ~7)) {
+		if (one) {
+		} else if (n < (nlags & ~7)) {
 			corr = blk[n & 7];
 			/* census: the reference's L_v_inner tail per lag */
 			OPC_ADD(OP_add, 2);
@@ -930,12 +993,21 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 	 * blocks of 8 (lag 146 - n for n = n0..n0+7, n0 even; window start
 	 * lo = 1 + n/2) sharing the sample loads of one pass. */
 	const int NL = MAXPITCH - MINPITCH;	/* 127 lags 146..20 */
+	/* The last block (lags 26..19) takes the 7 remaining lags and one
+	 * unused lag 19, whose reads stay inside pb (lo + PW + 19 < 219): one
+	 * paired pass instead of seven scalar ones.  The census build keeps the
+	 * reference's per-lag tail. */
+#if defined(MELPE_OPCOUNT)
+	const int NL_BLK = NL & ~7;
+#else
+	const int NL_BLK = (NL + 7) & ~7;
+#endif
 	int64_t blk[8];
 	{
 	PROF_SCOPE(39);
 	for (int i = MAXPITCH - 1; i >= MINPITCH; i--) {
 		int n = MAXPITCH - 1 - i;
-		if ((n & 7) == 0 && n + 8 <= NL) {
+		if ((n & 7) == 0 && n + 8 <= NL_BLK) {
 			const int16_t *pa = &pb[1 + n / 2];
 			const int16_t *pq = &pb[143 - n / 2];
 			int64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -987,7 +1059,7 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 			rk = L40_msu(rk, pb[hi + PW], pb[hi + PW]);
 			norm40(&rk, &rks, &Lrk);
 		}
-		if (n < (NL & ~7)) {
+		if (n < NL_BLK) {
 			A = blk[n & 7];
 			OPC_ADD(OP_L40_mac, PW);	/* census: the reference's per-lag sum */
 		} else {
