@@ -48,7 +48,15 @@ MN void remove_dc(const int16_t *in, int16_t *out, int16_t len)
 	sum = L_shr(sum, up);
 	Word16 off = mult(extract_l(sum), divide_s(pdown, len));
 	off = shl(off, 1);
-	for (int i = 0; i < len; i++)
+	np = p16_open(r, in, len);
+	i = 0;
+	#pragma unroll 4
+	for (int k = 0; k < np; k++, i += 2) {
+		uint32_t x = p16_next(r);
+		out[i] = sub(lo16(x), off);
+		out[i + 1] = sub(hi16(x), off);
+	}
+	for (; i < len; i++)
 		out[i] = sub(in[i], off);
 }
 
@@ -620,10 +628,27 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 		v_zero(E->lpres_delout, LPF_ORD);
 		E->pana_started = 1;
 	}
+#if defined(MELPE_OPCOUNT)
 	v_copy(&sb[2], &resid[-PITCHMAX], PITCH_FR);
 	iir3_s(&sb[2], TB(lpf_den), TB(lpf_num), E->lpres_delin, E->lpres_delout, PITCH_FR,
 	       FRAME);
 	f_pitch_scale(&sb[2], &sb[2], PITCH_FR);
+#else
+	/* copy, lowpass (memories kept after FRAME samples) and the
+	 * f_pitch_scale energy in one pass, as bpvc_ana's windows */
+	{
+		int64_t e = 0;
+		auto acc = [&](int, int16_t y) { e += L_mult(y, y); };
+		iir3_s_io(&resid[-PITCHMAX], &sb[2], TB(lpf_den), TB(lpf_num), E->lpres_delin,
+			  E->lpres_delout, FRAME, acc);
+		int16_t tin[2 * 3], tout[2 * 3];
+		v_copy(tin, E->lpres_delin, 6);
+		v_copy(tout, E->lpres_delout, 6);
+		iir3_s_io(&resid[-PITCHMAX + FRAME], &sb[2 + FRAME], TB(lpf_den), TB(lpf_num), tin, tout,
+			  PITCH_FR - FRAME, acc);
+		f_pitch_scale_e(&sb[2], &sb[2], PITCH_FR, e);
+	}
+#endif
 	t = frac_pch(&sb[2 + PITCH_FR / 2], &pcorr, pest, 5, PITCHMIN, PITCHMAX,
 		     PITCHMIN_Q7, PITCHMAX_Q7, 160);
 	if (pcorr < 9831) {
@@ -966,11 +991,24 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 	Word40 r0 = 0, rk = 0, A = 0;
 	Word16 r0s, rks;
 	Word32 Lr0, Lrk;
-	for (int i = 0; i < PW; i++) {	/* three opening sums, one pass */
-		int16_t u = pb[i], v = pb[i + MAXPITCH];
-		r0 = L40_mac(r0, u, u);
-		rk = L40_mac(rk, v, v);
-		A = L40_mac(A, u, v);
+	{	/* three opening sums, one paired pass */
+		auto step = [&](int16_t u, int16_t v) {
+			r0 = L40_mac(r0, u, u);
+			rk = L40_mac(rk, v, v);
+			A = L40_mac(A, u, v);
+		};
+		P16 ru, rv;
+		int np = p16_open(ru, pb, PW), nv = p16_open(rv, pb + MAXPITCH, PW);
+		np = np < nv ? np : nv;
+		int i = 0;
+		#pragma unroll 2
+		for (int k = 0; k < np; k++, i += 2) {
+			uint32_t x = p16_next(ru), y = p16_next(rv);
+			step(lo16(x), lo16(y));
+			step(hi16(x), hi16(y));
+		}
+		for (; i < PW; i++)
+			step(pb[i], pb[i + MAXPITCH]);
 	}
 	norm40(&r0, &r0s, &Lr0);
 	norm40(&rk, &rks, &Lrk);
@@ -1318,11 +1356,24 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 	Word16 win = sub(PIT_COR_LEN, hp);
 	/* the reference's three opening sums (:520-530) in one pass: each keeps
 	 * its own chain in index order */
-	for (int i = 0; i < win; i++) {
-		int16_t u = in[i], v = in[i + hp];
-		r0 = L40_mac(r0, u, u);
-		rk = L40_mac(rk, v, v);
-		A = L40_mac(A, u, v);
+	{
+		auto step = [&](int16_t u, int16_t v) {
+			r0 = L40_mac(r0, u, u);
+			rk = L40_mac(rk, v, v);
+			A = L40_mac(A, u, v);
+		};
+		P16 ru, rv;
+		int np = p16_open(ru, in, win), nv = p16_open(rv, in + hp, win);
+		np = np < nv ? np : nv;
+		int i = 0;
+		#pragma unroll 2
+		for (int k = 0; k < np; k++, i += 2) {
+			uint32_t x = p16_next(ru), y = p16_next(rv);
+			step(lo16(x), lo16(y));
+			step(hi16(x), hi16(y));
+		}
+		for (; i < win; i++)
+			step(in[i], in[i + hp]);
 	}
 	norm40(&r0, &r0s, &Lr0);
 	norm40(&rk, &rks, &Lrk);
