@@ -10,12 +10,20 @@
 
 MELPE_TU(npp)
 
+/* waves per SIMD the NPP kernels are compiled for: the LDS image
+ * (NppWave, 9,980 B) lets 16 waves share a CU, and 4 per SIMD caps the
+ * registers at 128 */
+#ifndef NPP_WAVES_PER_EU
+#define NPP_WAVES_PER_EU 4
+#endif
+#define NPP_WPE __attribute__((amdgpu_waves_per_eu(NPP_WAVES_PER_EU)))
+
 using namespace mlp::wv;
 
 /* melpe_n on `frames` frames per channel; channel c's samples at
  * sp[c*stride ...]; the first call of a channel reads 256 samples (or what
  * the row holds, zero-extended) */
-__global__ __launch_bounds__(WAVE) void k_npp(EncState *enc, int16_t *sp, int frames, int stride,
+__global__ __launch_bounds__(WAVE) NPP_WPE void k_npp(EncState *enc, int16_t *sp, int frames, int stride,
 					      const uint8_t *active, int n, int rate1200)
 {
 	int c = blockIdx.x;
@@ -34,7 +42,7 @@ __global__ __launch_bounds__(WAVE) void k_npp(EncState *enc, int16_t *sp, int fr
 
 /* the NPP part of melpe_a: frames 0..2 of every active channel's 540-sample
  * superframe, in place */
-__global__ __launch_bounds__(WAVE) void k_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active,
+__global__ __launch_bounds__(WAVE) NPP_WPE void k_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active,
 						  int n)
 {
 	int c = blockIdx.x;

@@ -62,14 +62,14 @@ static_assert(NPP_HOT_BYTES % 4 == 0, "NppState hot part copied by dwords");
 static_assert(sizeof(NppState) % 4 == 0, "NppState copied by dwords");
 
 /* per-frame scratch that the reference keeps in file statics but rewrites
- * before every read (YY, vk, noisespect2, var_rel, alpha_var, ybuf, temp_yy) */
+ * before every read (YY, vk, noisespect2, var_rel, alpha_var, ybuf; its
+ * temp_yy is a local of the functions using it) */
 struct NppScratch {
 	int16_t YY[NPP_NB], YY_shift[NPP_NB];
 	int16_t vk[NPP_NB], vk_shift[NPP_NB];
 	int16_t noisespect2[NPP_NB], noise2_shift[NPP_NB];
 	int16_t var_rel[NPP_NB], alpha_var[NPP_NB];
 	int16_t ybuf[2 * NPP_WIN + 2];
-	int32_t temp_yy[NPP_WIN + 2];
 };
 
 MD void npp_reset(NppState *s)
@@ -537,8 +537,8 @@ MD Word16 npp_bias_scalars(NppState *s, const NppScratch *w, Word32 vsum, Word16
 }
 
 /* second per-bin pass: the bias-compensated spectra for the minimum search */
-MD void npp_bias2_bin(const NppState *s, const NppScratch *w, int16_t *bsp, int16_t *bsh,
-		      int16_t *bsub, int16_t *bsubsh, Word16 vsq, Word16 f1, Word16 f2, int i)
+MD void npp_bias2_bin(const NppState *s, const NppScratch *w, int16_t &bsp, int16_t &bsh,
+		      int16_t &bsub, int16_t &bsubsh, Word16 vsq, Word16 f1, Word16 f2, int i)
 {
 	Word32 L3 = L_mult(vsq, s->smoothedspect[i]);
 	Word16 vr = w->var_rel[i];
@@ -550,8 +550,8 @@ MD void npp_bias2_bin(const NppState *s, const NppScratch *w, int16_t *bsp, int1
 	if (L < 1)
 		L = 1;
 	Word16 s1 = norm_l(L);
-	bsp[i] = extract_h(L_shl(L, s1));
-	bsh[i] = add(s->sm_shift[i], sub(8, s1));
+	bsp = extract_h(L_shl(L, s1));
+	bsh = add(s->sm_shift[i], sub(8, s1));
 	t = add(13968, shr(vr, 2));
 	t = add(11909, shr(mult(vr, t), 1));
 	L = L_mpy_ls(L_mpy_ls(L4, f2), t);
@@ -559,8 +559,8 @@ MD void npp_bias2_bin(const NppState *s, const NppScratch *w, int16_t *bsp, int1
 	if (L < 1)
 		L = 1;
 	s1 = norm_l(L);
-	bsub[i] = extract_h(L_shl(L, s1));
-	bsubsh[i] = add(s->sm_shift[i], sub(6, s1));
+	bsub = extract_h(L_shl(L, s1));
+	bsubsh = add(s->sm_shift[i], sub(6, s1));
 }
 
 MN void npp_bias_compensation(NppState *s, NppScratch *w, int16_t *bsp, int16_t *bsh,
@@ -574,7 +574,7 @@ MN void npp_bias_compensation(NppState *s, NppScratch *w, int16_t *bsp, int16_t 
 	Word16 f1, f2;
 	Word16 vsq = npp_bias_scalars(s, w, vsum, &f1, &f2);
 	for (int i = 0; i < NPP_NB; i++)
-		npp_bias2_bin(s, w, bsp, bsh, bsub, bsubsh, vsq, f1, f2, i);
+		npp_bias2_bin(s, w, bsp[i], bsh[i], bsub[i], bsubsh[i], vsq, f1, f2, i);
 }
 
 /* noise_slope :843 */
@@ -594,15 +594,15 @@ MD Word16 npp_noise_slope(const NppState *s)
 /* min_search :889 -- minimum tracking over 8 windows of 9 frames.  Every
  * loop of the reference touches bin i only, so the per-bin part runs each
  * bin through the whole branch; the counters advance afterwards. */
-MD void npp_min_search_bin(NppState *s, NppState *m, const int16_t *bsp, const int16_t *bsh,
-			   const int16_t *bsub, const int16_t *bsubsh, Word16 slope, int i)
+MD void npp_min_search_bin(NppState *s, NppState *m, int16_t bsp, int16_t bsh, int16_t bsub,
+			   int16_t bsubsh, Word16 slope, int i)
 {
 	if (s->minspec_counter == 0) {
-		if (cmp_shift(bsp[i], bsh[i], s->act_min[i], s->act_min_shift[i]) < 0) {
-			s->act_min[i] = bsp[i];
-			s->act_min_shift[i] = bsh[i];
-			m->act_min_sub[i] = bsub[i];
-			m->act_min_sub_shift[i] = bsubsh[i];
+		if (cmp_shift(bsp, bsh, s->act_min[i], s->act_min_shift[i]) < 0) {
+			s->act_min[i] = bsp;
+			s->act_min_shift[i] = bsh;
+			m->act_min_sub[i] = bsub;
+			m->act_min_sub_shift[i] = bsubsh;
 			m->localflag[i] = 0;
 		}
 		m->circb[s->circb_index][i] = s->act_min[i];
@@ -630,16 +630,16 @@ MD void npp_min_search_bin(NppState *s, NppState *m, const int16_t *bsp, const i
 		}
 		m->localflag[i] = 0;
 	} else if (s->minspec_counter == 1) {
-		s->act_min[i] = bsp[i];
-		s->act_min_shift[i] = bsh[i];
-		m->act_min_sub[i] = bsub[i];
-		m->act_min_sub_shift[i] = bsubsh[i];
+		s->act_min[i] = bsp;
+		s->act_min_shift[i] = bsh;
+		m->act_min_sub[i] = bsub;
+		m->act_min_sub_shift[i] = bsubsh;
 	} else {
-		if (cmp_shift(bsp[i], bsh[i], s->act_min[i], s->act_min_shift[i]) < 0) {
-			s->act_min[i] = bsp[i];
-			s->act_min_shift[i] = bsh[i];
-			m->act_min_sub[i] = bsub[i];
-			m->act_min_sub_shift[i] = bsubsh[i];
+		if (cmp_shift(bsp, bsh, s->act_min[i], s->act_min_shift[i]) < 0) {
+			s->act_min[i] = bsp;
+			s->act_min_shift[i] = bsh;
+			m->act_min_sub[i] = bsub;
+			m->act_min_sub_shift[i] = bsubsh;
 			m->localflag[i] = 1;
 		}
 		if (cmp_shift(m->act_min_sub[i], m->act_min_sub_shift[i],
@@ -677,7 +677,7 @@ MN void npp_min_search(NppState *s, const int16_t *bsp, const int16_t *bsh,
 {
 	Word16 slope = npp_noise_slope(s);
 	for (int i = 0; i < NPP_NB; i++)
-		npp_min_search_bin(s, s, bsp, bsh, bsub, bsubsh, slope, i);
+		npp_min_search_bin(s, s, bsp[i], bsh[i], bsub[i], bsubsh[i], slope, i);
 	npp_min_search_post(s);
 }
 
@@ -712,7 +712,7 @@ MN void npp_minstat_init(NppState *s)
 MN void npp_enh_init(NppState *s, NppScratch *w, int16_t *noise)
 {
 	int16_t *yb = w->ybuf;
-	int32_t *ty = w->temp_yy;
+	int32_t ty[NPP_WIN + 2];
 	window(noise, TB(sqrt_tukey_256_180), noise, NPP_WIN);
 	Word16 mx = 1;
 	for (int i = 0; i < NPP_WIN; i++) {
@@ -834,7 +834,7 @@ MD void npp_ksi_bin(NppState *s, const int16_t *gk, const int16_t *gks, int i)
 MN void npp_process_frame(NppState *s, NppScratch *w, const int16_t *in, int16_t *out)
 {
 	int16_t *yb = w->ybuf;
-	int32_t *ty = w->temp_yy;
+	int32_t ty[NPP_WIN + 2];
 	int16_t Ymag[NPP_NB], Ymag_shift[NPP_NB], GainD[NPP_NB];
 	int16_t gk[NPP_NB], gks[NPP_NB];
 	int16_t bsp[NPP_NB], bsub[NPP_NB], bsh[NPP_NB], bsubsh[NPP_NB];

@@ -35,6 +35,10 @@ namespace wv {
 
 #define WV 64
 #define LANE_LOOP(i, n) for (int i = lane; i < (n); i += WV)
+/* the lane's bins i = lane + 64 t, t = 0..2, unrolled: per-bin values that
+ * only the owning lane reads back can live in registers indexed by t */
+#define BIN_LOOP(t, i) \
+	_Pragma("unroll") for (int t = 0, i = lane; t < 3; t++, i += WV) if (i < NPP_NB)
 
 __device__ __forceinline__ void wsync()
 {
@@ -85,15 +89,20 @@ __device__ __forceinline__ int bin_at(int r0, int r1, int r2, int i)
 
 /* LDS image of one channel's NPP */
 struct NppWave {
-	NppScratch w;	/* YY.., ybuf, temp_yy (int32 first: alignment) */
+	union {
+		NppScratch w;	/* YY.., ybuf */
+		/* wv_enh_init's temp_yy (the scratch is dead there); may_alias
+		 * dwords, like the record copies */
+		u32_alias ty_init[NPP_WIN + 2];
+	};
 	/* the channel's NppState up to its min-statistics memory (NPP_HOT_BYTES);
 	 * that memory stays in the HBM record (the `m` view below) */
 	u32_alias s_hot[NPP_HOT_BYTES / 4];	/* an NppState image, read as fields */
-	int16_t Ymag[NPP_NB], Ymag_shift[NPP_NB], GainD[NPP_NB];
+	int16_t GainD[NPP_NB];
 	int16_t gk[NPP_NB], gks[NPP_NB];
-	int16_t bsp[NPP_NB], bsub[NPP_NB], bsh[NPP_NB], bsubsh[NPP_NB];
-	int16_t buf[NPP_WIN];	/* analysis frame / initial noise frame */
-	int16_t out[NPP_WIN];	/* synthesis frame */
+	/* analysis frame / initial noise frame, then the synthesis frame (the
+	 * analysis frame is dead once the forward FFT's input is built) */
+	int16_t buf[NPP_WIN];
 };
 
 /* per-lane constants of the FFT and the analysis window, loaded once per
@@ -315,7 +324,7 @@ MD void wv_enh_init(NppWave *W, int16_t *noise, const WvConst *kc, int lane, Npp
 {
 	NppState *s = wv_S(W);
 	int16_t *yb = W->w.ybuf;
-	int32_t *ty = W->w.temp_yy;
+	u32_alias *ty = W->ty_init;
 	int mx = 0;
 #pragma unroll
 	LANE_LOOP(i, NPP_WIN) {
@@ -339,7 +348,7 @@ MD void wv_enh_init(NppWave *W, int16_t *noise, const WvConst *kc, int lane, Npp
 			v = L_shr(L_mult(yb[i], yb[i]), 1);
 		else
 			v = L_shr(L_add(L_mult(yb[i], yb[i]), L_mult(yb[i + 1], yb[i + 1])), 1);
-		ty[i] = v;
+		ty[i] = (uint32_t) v;
 		ty[i + 1] = 0;
 		Lm = max(Lm, (int) v);
 		if (p != NPP_NB - 1)
@@ -349,7 +358,7 @@ MD void wv_enh_init(NppWave *W, int16_t *noise, const WvConst *kc, int lane, Npp
 	wsync();
 	sh = norm_l(L);
 	LANE_LOOP(i, NPP_WIN + 1)
-		yb[i] = extract_h(L_shl(ty[i], sh));
+		yb[i] = extract_h(L_shl((Word32) ty[i], sh));
 	sh = sub(shl(add(ash, g), 1), add(sh, 7));
 	wsync();
 	wv_mirror(yb, lane);
@@ -416,7 +425,6 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	NppState *s = wv_S(W);
 	NppScratch *w = &W->w;
 	int16_t *yb = w->ybuf;
-	int32_t *ty = w->temp_yy;
 	int16_t *GainD = W->GainD, *gk = W->gk, *gks = W->gks;
 	Word16 sh, t, t1, t2, t3, t4;
 	Word32 L;
@@ -477,14 +485,17 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	}
 	maxs = wmax(maxs);
 	int part = 0;
-	LANE_LOOP(i, NPP_NB) {
+	/* |Y| of the lane's bins lane + 64 t: read back only by the same lane,
+	 * so it stays in registers (BIN_LOOP) */
+	int16_t ymag[3] = {0, 0, 0}, ymag_sh[3] = {0, 0, 0};
+	BIN_LOOP(t, i) {
 		Word16 y = w->YY[i], ys = w->YY_shift[i];
 		if (ys & 1) {
 			y = shr(y, 1);
 			ys = add(ys, 1);
 		}
-		W->Ymag[i] = sqrt_Q15(y);
-		W->Ymag_shift[i] = shr(ys, 1);
+		ymag[t] = sqrt_Q15(y);
+		ymag_sh[t] = shr(ys, 1);
 		w->YY_shift[i] = sub(w->YY_shift[i], 8);
 		/* maxs is taken before the -8 (npp.c:1300-1330) */
 		part += npp_spec_term(w->YY, w->YY_shift, (Word16) maxs, i);
@@ -521,8 +532,9 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	Word16 vsq = npp_bias_scalars(s, w, vsum, &f1, &f2);
 	Word16 slope = npp_noise_slope(s);
 	LANE_LOOP(i, NPP_NB) {
-		npp_bias2_bin(s, w, W->bsp, W->bsh, W->bsub, W->bsubsh, vsq, f1, f2, i);
-		npp_min_search_bin(s, m, W->bsp, W->bsh, W->bsub, W->bsubsh, slope, i);
+		int16_t bsp, bsh, bsub, bsubsh;	/* bin i's, this lane's only */
+		npp_bias2_bin(s, w, bsp, bsh, bsub, bsubsh, vsq, f1, f2, i);
+		npp_min_search_bin(s, m, bsp, bsh, bsub, bsubsh, slope, i);
 		gk[i] = divide_s(shr(w->YY[i], 1), s->lambdaD[i]);
 		gks[i] = sub(add(w->YY_shift[i], 1), s->lambdaD_shift[i]);
 	}
@@ -603,11 +615,11 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	{
 	PROF_SCOPE(38);
 	if (s->enh_i == 1) {
-		LANE_LOOP(i, NPP_NB) {
-			Word32 v = L_mult(W->Ymag[i], GM_MIN);
+		BIN_LOOP(t, i) {
+			Word32 v = L_mult(ymag[t], GM_MIN);
 			Word16 n = norm_l(v);
 			s->agal[i] = extract_h(L_shl(v, n));
-			s->agal_shift[i] = sub(W->Ymag_shift[i], n);
+			s->agal_shift[i] = sub(ymag_sh[t], n);
 		}
 	} else {
 		LANE_LOOP(i, NPP_NB)
@@ -680,28 +692,38 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 			}
 			s->qk_started = 1;
 		}
-		LANE_LOOP(i, NPP_NB) {
+		BIN_LOOP(t, i) {
 			npp_gain_log_mmse_bin(s, w, s->qk, s->Gain, gk, gks, i);
 			GainD[i] = s->Gain[i];
 			npp_gain_mod_bin(s, w, s->qk, GainD, i);
-			Word32 v = L_mult(GainD[i], W->Ymag[i]);
+			Word32 v = L_mult(GainD[i], ymag[t]);
 			Word16 n = norm_l(v);
 			s->agal[i] = extract_h(L_shl(v, n));
-			s->agal_shift[i] = sub(W->Ymag_shift[i], n);
+			s->agal_shift[i] = sub(ymag_sh[t], n);
 		}
 	}
 	}
 	wsync();
 	int lm = 0;
-	LANE_LOOP(i, NPP_WIN + 2) {
-		Word32 v = L_mult(yb[i], GainD[i / 2]);
-		ty[i] = v;
-		lm = max(lm, (int) L_abs(v));
+	Word32 tyr[5];	/* temp_yy of samples lane + 64 t, in registers */
+#pragma unroll
+	for (int t = 0; t < 5; t++) {
+		int i = lane + WV * t;
+		tyr[t] = 0;
+		if (i < NPP_WIN + 2) {
+			Word32 v = L_mult(yb[i], GainD[i / 2]);
+			tyr[t] = v;
+			lm = max(lm, (int) L_abs(v));
+		}
 	}
 	Word32 Lmax = wmax(lm);
 	sh = norm_l(Lmax);
-	LANE_LOOP(i, NPP_WIN + 2)
-		yb[i] = extract_h(L_shl(ty[i], sh));
+#pragma unroll
+	for (int t = 0; t < 5; t++) {
+		int i = lane + WV * t;
+		if (i < NPP_WIN + 2)
+			yb[i] = extract_h(L_shl(tyr[t], sh));
+	}
 	sh = sub(Ysh, sh);
 	wsync();
 	wv_mirror(yb, lane);
@@ -760,15 +782,15 @@ MD void wv_npp_frame(NppWave *W, NppState *m, int16_t *x, int avail, bool rate12
 	LANE_LOOP(i, NPP_HOP)
 		s->speech_in[NPP_OVL + i] = x[i];
 	wsync();
-	wv_process_frame(W, m, s->speech_in, W->out, kc, lane);
+	wv_process_frame(W, m, s->speech_in, W->buf, kc, lane);
 	LANE_LOOP(i, NPP_OVL) {
-		Word16 o = add(W->out[i], s->overlap[i]);
-		s->overlap[i] = W->out[NPP_HOP + i];
-		W->out[i] = o;
+		Word16 o = add(W->buf[i], s->overlap[i]);
+		s->overlap[i] = W->buf[NPP_HOP + i];
+		W->buf[i] = o;
 	}
 	wsync();
 	LANE_LOOP(i, NPP_HOP)
-		x[i] = W->out[i];
+		x[i] = W->buf[i];
 	wsync();
 }
 
