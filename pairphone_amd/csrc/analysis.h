@@ -157,10 +157,71 @@ MD void q_bpvc_dec(int16_t *bpvc, Word16 idx, int16_t uv, int nb)
 /* melpe/pit_lib.c                                                    */
 /* ------------------------------------------------------------------ */
 
+/* Exact-path bookkeeping for the host build's tests: MELPE_NO_EXACT turns the
+ * exact correlators off (every chain runs sequentially), MELPE_EXACT_STATS
+ * counts the frac_pch / find_pitch calls that took each path. */
+#if defined(MELPE_EXACT_STATS) && !defined(__HIP__)
+extern "C" long melpe_exact_stats[4];
+#define EXACT_STAT(i) (melpe_exact_stats[i]++)
+#else
+#define EXACT_STAT(i) ((void) 0)
+#endif
+
+/* p[i] = shr(p[i], sc) in place, returning sum y^2 saturated to 32 bits
+ * (exact below 2^31 - 1, which is all the bound needs): dword pairs in
+ * chunks of four, the next chunk loaded before this one is stored */
+MD int32_t shr_energy_inplace(int16_t *p, int n, Word16 sc)
+{
+	int32_t e = 0;
+	int i = 0;
+	if (n > 0 && ((reinterpret_cast<uintptr_t>(p) >> 1) & 1)) {
+		int16_t y = shr(p[0], sc);
+		p[0] = y;
+		e = (int32_t) y * y;
+		i = 1;
+	}
+	u32_alias *w = reinterpret_cast<u32_alias *>(p + i);
+	const int nd = (n - i) >> 1, G = nd >> 2;
+	auto sh2 = [&](uint32_t v) {
+		return (uint32_t) (uint16_t) shr(lo16(v), sc) | ((uint32_t) (uint16_t) shr(hi16(v), sc) << 16);
+	};
+	uint32_t cur[4];
+	if (G > 0)
+		for (int k = 0; k < 4; k++)
+			cur[k] = w[k];
+	for (int g = 0; g < G; g++) {
+		int gn = g + 1 < G ? g + 1 : g;
+		uint32_t nxt[4];
+		#pragma unroll
+		for (int k = 0; k < 4; k++)
+			nxt[k] = w[4 * gn + k];
+		#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			uint32_t y = sh2(cur[k]);
+			w[4 * g + k] = y;
+			e = sdot2_sat(y, y, e);
+			cur[k] = nxt[k];
+		}
+	}
+	for (int d = 4 * G; d < nd; d++) {
+		uint32_t y = sh2(w[d]);
+		w[d] = y;
+		e = sdot2_sat(y, y, e);
+	}
+	for (int k = i + 2 * nd; k < n; k++) {
+		int16_t y = shr(p[k], sc);
+		p[k] = y;
+		int64_t t = (int64_t) e + (int32_t) y * y;
+		e = t > LW_MAX_ ? LW_MAX_ : (int32_t) t;
+	}
+	return e;
+}
+
 /* f_pitch_scale's second half, given the window's exact energy (the sum of
  * L_mult(x, x), in 64 bits): callers that produce the window can add its
  * energy up while they write it (bpvc_ana) */
-MD Word16 f_pitch_scale_e(int16_t *out, const int16_t *in, int len, int64_t sum)
+MD Word16 f_pitch_scale_e(int16_t *out, const int16_t *in, int len, int64_t sum,
+			     bool *exact = nullptr, int64_t extra = 0)
 {
 	Word16 sc = 0;
 	/* Every term L_mult(x, x) is >= 0, so the reference's running margin
@@ -175,12 +236,34 @@ MD Word16 f_pitch_scale_e(int16_t *out, const int16_t *in, int len, int64_t sum)
 		corr = L_v_magsq(tb, len, 0, 1);
 	}
 	sc = sub(sc, shr(norm_l(corr), 1));
-	v_equ_shr(out, in, sc, len);
+	if (!exact) {
+		v_equ_shr(out, in, sc, len);
+		return sc;
+	}
+	/* the output's own energy, sum of 2 y^2 without saturation: when it
+	 * fits 32 bits no L_mac chain over these samples can clamp
+	 * (sum |2ab| <= sum a^2 + b^2), which the exact correlators rely on */
+	int64_t e2 = extra;
+	if (out == in) {
+		e2 += 2 * (int64_t) shr_energy_inplace(out, len, sc);
+	} else {
+		for (int i = 0; i < len; i++) {
+			int16_t y = shr(in[i], sc);
+			out[i] = y;
+			e2 += 2 * (int64_t) ((int32_t) y * y);
+		}
+	}
+#if defined(MELPE_NO_EXACT)
+	*exact = false;
+#else
+	*exact = e2 <= (int64_t) LW_MAX_;
+#endif
 	return sc;
 }
 
 /* f_pitch_scale :178 -- scale so the energy fits, returns the shift */
-MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
+MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len, bool *exact = nullptr,
+			int64_t extra = 0)
 {
 	Word16 sc = 0;
 	Word32 corr;
@@ -216,7 +299,7 @@ MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 		}
 		for (; i < len; i++)
 			sum += L_mult(in[i], in[i]);
-		return f_pitch_scale_e(out, in, len, sum);
+		return f_pitch_scale_e(out, in, len, sum, exact, extra);
 	}
 #endif
 	if (ovf) {
@@ -227,6 +310,9 @@ MN Word16 f_pitch_scale(int16_t *out, const int16_t *in, int len)
 	}
 	sc = sub(sc, shr(norm_l(corr), 1));
 	v_equ_shr(out, in, sc, len);
+	if (exact)
+		*exact = false;
+	(void) extra;
 	return sc;
 }
 
@@ -326,25 +412,119 @@ MD void fp_corrK(const int16_t *pa, const int16_t *pb, int len, Word32 *out)
 		out[k] = acc[k];
 }
 
+/* frac_pch's nine sums as exact plain sums (the caller's bound), on packed
+ * pairs: a_j = pa[j], b_j = pb[j], j < len; in q[]: a.a, b.b, a.b, a.b+1,
+ * a.b+2, b+1.b+2, b+1.b+1, b+2.b+2, b.b+1.  Reads pa[0 .. len), pb[0 .. len + 2). */
+MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q)
+{
+	constexpr int PD = MELPE_XC_PD;
+	int32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+	const int T = len >> 1;
+	int jt = 0;
+	if (T >= 4) {
+		PairStream sa, sb;
+		ps_open(sa, pa, len);
+		ps_open(sb, pb, len + 2);
+		/* steps 4g .. 4g + 3: a pairs xa[st]; b pairs wb[st] (b_j),
+		 * their mids (b_j+1) and wb[st + 1] (b_j+2) */
+		uint32_t wb[5];
+		ps_head<1>(sb, wb);
+		auto group = [&](const uint32_t *xa, int nst) {
+			#pragma unroll
+			for (int st = 0; st < 4; st++) {
+				uint32_t A = xa[st], b0 = wb[st], b2 = wb[st + 1];
+				uint32_t b1 = pair_mid(b2, b0);
+				int32_t d[9] = {sdot2(A, A, acc[0]), sdot2(b0, b0, acc[1]),
+						 sdot2(A, b0, acc[2]), sdot2(A, b1, acc[3]),
+						 sdot2(A, b2, acc[4]), sdot2(b1, b2, acc[5]),
+						 sdot2(b1, b1, acc[6]), sdot2(b2, b2, acc[7]),
+						 sdot2(b0, b1, acc[8])};
+				#pragma unroll
+				for (int k = 0; k < 9; k++)
+					acc[k] = st < nst ? d[k] : acc[k];
+			}
+			wb[0] = wb[4];
+		};
+		int G = T >> 2, ga = ps_full_groups(sa, 0), gb = ps_full_groups(sb, 1);
+		G = G < ga ? G : ga;
+		G = G < gb ? G : gb;
+		if (G > 0) {
+			P16C<PD> ca, cb;
+			p16c_open(ca, sa, 0, G);
+			p16c_open(cb, sb, 1, G);
+			for (int g = 0; g < G; g++) {
+				uint32_t xa[4];
+				p16c_next4(ca, xa);
+				p16c_next4(cb, &wb[1]);
+				group(xa, 4);
+			}
+		}
+		for (int t = 4 * G; t < T; t += 4) {
+			uint32_t xa[4];
+			ps_pairs4(sa, t, xa);
+			ps_pairs4(sb, 1 + t, &wb[1]);
+			group(xa, T - t);
+		}
+		jt = 2 * T;
+	}
+	for (int j = jt; j < len; j++) {
+		int a = pa[j], x0 = pb[j], x1 = pb[j + 1], x2 = pb[j + 2];
+		acc[0] += a * a;
+		acc[1] += x0 * x0;
+		acc[2] += a * x0;
+		acc[3] += a * x1;
+		acc[4] += a * x2;
+		acc[5] += x1 * x2;
+		acc[6] += x1 * x1;
+		acc[7] += x2 * x2;
+		acc[8] += x0 * x1;
+	}
+	for (int k = 0; k < 9; k++)
+		q[k] = acc[k];
+}
+
 /* find_pitch :240 -- normalised autocorrelation lag search, lags upper..lower */
-MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upper, Word16 len)
+MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upper, Word16 len,
+		     bool exact = false)
 {
 	PROF_SCOPE(2);
+#if defined(MELPE_OPCOUNT)
+	exact = false;
+#endif
+	EXACT_STAT(exact ? 1 : 0);
 	Word16 ip = lower;
 	Word32 max_num = 0, max_den = 1;
 	bool even = true;
 	Word16 cb = negate(shr(add(len, upper), 1));
 	const Word16 cb0 = cb;
-	Word32 c00 = L_v_magsq(&sig[cb], len, 0, 1);
-	Word32 cTT = L_v_magsq(&sig[cb + upper], len, 0, 1);
+	/* exact: the caller's bound holds over sig[cb0 .. cb0 + upper + len),
+	 * which every lag block below reads inside (also the unused lags of a
+	 * last partial block), so each L_mac chain is the plain sum */
+	Word32 c00, cTT;
+	if (exact) {
+		c00 = 2 * magsq_pairs(&sig[cb], len);
+		cTT = 2 * magsq_pairs(&sig[cb + upper], len);
+		OPC_ADD(OP_L_mac, 0);
+	} else {
+		c00 = L_v_magsq(&sig[cb], len, 0, 1);
+		cTT = L_v_magsq(&sig[cb + upper], len, 0, 1);
+	}
 	Word32 blk[8];
 	int nlags = upper - lower + 1;
 #if !defined(MELPE_OPCOUNT)
 	/* up to 12 lags (every +-5 search): all of them in one pass */
 	Word32 blk12[12];
 	const bool one = nlags <= 12;
-	if (one)
-		fp_corrK<12>(&sig[cb0], &sig[cb0 + 6 + upper - 11], len, blk12);
+	if (one) {
+		if (exact) {
+			int32_t raw[12];
+			xcorr_pairs<12, FpLags<12>, false>(&sig[cb0], &sig[cb0 + 6 + upper - 11], len, raw);
+			for (int k = 0; k < 12; k++)
+				blk12[k] = 2 * raw[k];
+		} else {
+			fp_corrK<12>(&sig[cb0], &sig[cb0 + 6 + upper - 11], len, blk12);
+		}
+	}
 #else
 	const bool one = false;
 	Word32 *blk12 = blk;
@@ -354,14 +534,21 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 		Word32 corr;
 		if (one) {
 			corr = blk12[n];
-		} else if ((n & 7) == 0 && n + 8 <= nlags) {
+		} else if ((n & 7) == 0 && (exact || n + 8 <= nlags)) {
 			/* the block's bases: a at cb_n0, b at cb_(n0+7) + i_(n0+7) */
 			int c_n0 = cb0 + (n + 1) / 2;
 			int b0 = cb0 + (n + 8) / 2 + upper - n - 7;
-			fp_corr8(&sig[c_n0], &sig[b0], len, blk);
+			if (exact) {
+				int32_t raw[8];
+				xcorr_pairs<8, FpLags<8>, false>(&sig[c_n0], &sig[b0], len, raw);
+				for (int k = 0; k < 8; k++)
+					blk[k] = 2 * raw[k];
+			} else {
+				fp_corr8(&sig[c_n0], &sig[b0], len, blk);
+			}
 		}
 		if (one) {
-		} else if (n < (nlags & ~7)) {
+		} else if (exact || n < (nlags & ~7)) {
 			corr = blk[n & 7];
 			/* census: the reference's L_v_inner tail per lag */
 			OPC_ADD(OP_add, 2);
@@ -409,9 +596,14 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 
 /* frac_pch :340 -- fractional pitch refinement and its correlation */
 MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 range,
-		   Word16 pmin, Word16 pmax, Word16 pmin_q7, Word16 pmax_q7, Word16 lmin)
+		   Word16 pmin, Word16 pmax, Word16 pmin_q7, Word16 pmax_q7, Word16 lmin,
+		   bool exact = false)
 {
 	PROF_SCOPE(3);
+#if defined(MELPE_OPCOUNT)
+	exact = false;
+#endif
+	EXACT_STAT(exact ? 3 : 2);
 	Word16 len, cb, ip, corr;
 	if (range > 0) {
 		ip = shift_r(fpitch, -7);
@@ -426,7 +618,7 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 		len = ip;
 		if (len < lmin)
 			len = lmin;
-		fpitch = shl(find_pitch(sig, &corr, lo, hi, len), 7);
+		fpitch = shl(find_pitch(sig, &corr, lo, hi, len, exact), 7);
 	}
 	ip = shift_r(fpitch, -7);
 	if (ip >= pmax)
@@ -442,7 +634,19 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 	 * the ip-1 test are formed (cTT of one outcome is cT1T1 of the other, and
 	 * cTT of the ip-1 outcome is the len-prefix of the (len+2)-term magsq). */
 	Word32 msq = 0, m2 = 0, cm1 = 0, c0 = 0, c1 = 0, tt1 = 0, tt = 0, t1t1 = 0, tt1m = 0;
-	{
+	if (exact) {
+		int32_t q[9];
+		fp_sums9(&sig[cb], &sig[cb + ip - 1], len, q);
+		msq = 2 * q[0];
+		m2 = 2 * q[1];
+		cm1 = 2 * q[2];
+		c0 = 2 * q[3];
+		c1 = 2 * q[4];
+		tt1 = 2 * q[5];
+		tt = 2 * q[6];
+		t1t1 = 2 * q[7];
+		tt1m = 2 * q[8];
+	} else {
 		const int16_t *pa = &sig[cb], *pb = &sig[cb + ip - 1];
 		int16_t b0 = pb[0], b1 = pb[1];
 		auto step = [&](int16_t a, int16_t b2) {
@@ -552,7 +756,7 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 
 /* double_ver :151 */
 MN void double_ver(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pmin, Word16 pmax,
-		   Word16 pmin_q7, Word16 pmax_q7, Word16 lmin)
+		   Word16 pmin_q7, Word16 pmax_q7, Word16 lmin, bool exact)
 {
 	Word16 m = 1;
 	while (extract_l(L_shr(L_mult(pitch, m), 1)) < 3840)
@@ -560,7 +764,7 @@ MN void double_ver(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pmin,
 	if (m > 1) {
 		Word16 tp = extract_l(L_shr(L_mult(pitch, m), 1));
 		Word16 c;
-		frac_pch(sig, &c, tp, 0, pmin, pmax, pmin_q7, pmax_q7, lmin);
+		frac_pch(sig, &c, tp, 0, pmin, pmax, pmin_q7, pmax_q7, lmin, exact);
 		if (c < *pcorr)
 			*pcorr = c;
 	}
@@ -568,9 +772,10 @@ MN void double_ver(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pmin,
 
 /* double_chk :84 -- pitch-halving check over multiples 8..2 */
 MN Word16 double_chk(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pdouble,
-		     Word16 pmin, Word16 pmax, Word16 pmin_q7, Word16 pmax_q7, Word16 lmin)
+		     Word16 pmin, Word16 pmax, Word16 pmin_q7, Word16 pmax_q7, Word16 lmin,
+		     bool exact)
 {
-	pitch = frac_pch(sig, pcorr, pitch, 0, pmin, pmax, pmin_q7, pmax_q7, lmin);
+	pitch = frac_pch(sig, pcorr, pitch, 0, pmin, pmax, pmin_q7, pmax_q7, lmin, exact);
 	Word16 thresh = extract_l(L_shr(L_mult(*pcorr, pdouble), 8));
 	for (Word16 m = 8; m >= 2; m--) {
 		Word16 t1 = 0;
@@ -585,15 +790,16 @@ MN Word16 double_chk(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pdo
 		tp = shr(t2, t1);
 		if (tp >= pmin_q7) {
 			Word16 c;
-			tp = frac_pch(sig, &c, tp, 0, pmin, pmax, pmin_q7, pmax_q7, lmin);
-			double_ver(sig, &c, tp, pmin, pmax, pmin_q7, pmax_q7, lmin);
+			tp = frac_pch(sig, &c, tp, 0, pmin, pmax, pmin_q7, pmax_q7, lmin, exact);
+			double_ver(sig, &c, tp, pmin, pmax, pmin_q7, pmax_q7, lmin, exact);
 			if (c > thresh) {
-				pitch = frac_pch(sig, pcorr, tp, 0, pmin, pmax, pmin_q7, pmax_q7, lmin);
+				pitch = frac_pch(sig, pcorr, tp, 0, pmin, pmax, pmin_q7, pmax_q7, lmin,
+						 exact);
 				break;
 			}
 		}
 	}
-	double_ver(sig, pcorr, pitch, pmin, pmax, pmin_q7, pmax_q7, lmin);
+	double_ver(sig, pcorr, pitch, pmin, pmax, pmin_q7, pmax_q7, lmin, exact);
 	return pitch;
 }
 
@@ -623,6 +829,7 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 	PROF_SCOPE(7);
 	int16_t *sb = E->pa_sigbuf;
 	Word16 pcorr, pitch, t, t2;
+	bool ex = false;
 	if (!E->pana_started) {
 		v_zero(E->lpres_delin, LPF_ORD);
 		v_zero(E->lpres_delout, LPF_ORD);
@@ -632,7 +839,7 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 	v_copy(&sb[2], &resid[-PITCHMAX], PITCH_FR);
 	iir3_s(&sb[2], TB(lpf_den), TB(lpf_num), E->lpres_delin, E->lpres_delout, PITCH_FR,
 	       FRAME);
-	f_pitch_scale(&sb[2], &sb[2], PITCH_FR);
+	f_pitch_scale(&sb[2], &sb[2], PITCH_FR, &ex);
 #else
 	/* copy, lowpass (memories kept after FRAME samples) and the
 	 * f_pitch_scale energy in one pass, as bpvc_ana's windows */
@@ -646,27 +853,38 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 		v_copy(tout, E->lpres_delout, 6);
 		iir3_s_io(&resid[-PITCHMAX + FRAME], &sb[2 + FRAME], TB(lpf_den), TB(lpf_num), tin, tout,
 			  PITCH_FR - FRAME, acc);
-		f_pitch_scale_e(&sb[2], &sb[2], PITCH_FR, e);
+		/* double_chk below reads up to sb[LPF_ORD + PITCH_FR), past the
+		 * scaled window: the persistent tail joins the bound */
+		int64_t tail = 0;
+		for (int i = 2 + PITCH_FR; i < LPF_ORD + PITCH_FR; i++)
+			tail += 2 * (int64_t) ((int32_t) sb[i] * sb[i]);
+		f_pitch_scale_e(&sb[2], &sb[2], PITCH_FR, e, &ex, tail);
 	}
 #endif
 	t = frac_pch(&sb[2 + PITCH_FR / 2], &pcorr, pest, 5, PITCHMIN, PITCHMAX,
-		     PITCHMIN_Q7, PITCHMAX_Q7, 160);
+		     PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
 	if (pcorr < 9831) {
 		v_copy(&sb[LPF_ORD], &speech[-PITCHMAX], PITCH_FR);
-		f_pitch_scale(&sb[2], &sb[2], PITCH_FR);
+		/* the frac_pch calls below read up to sb[LPF_ORD + PITCH_FR): past
+		 * the scaled sb[2 .. 2 + PITCH_FR), four unscaled speech samples
+		 * join the bound */
+		int64_t tail = 0;
+		for (int i = 2 + PITCH_FR; i < LPF_ORD + PITCH_FR; i++)
+			tail += 2 * (int64_t) ((int32_t) sb[i] * sb[i]);
+		f_pitch_scale(&sb[2], &sb[2], PITCH_FR, &ex, tail);
 		t = frac_pch(&sb[LPF_ORD + PITCH_FR / 2], &pcorr, pest, 0, PITCHMIN, PITCHMAX,
-			     PITCHMIN_Q7, PITCHMAX_Q7, 160);
+			     PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
 		if (pcorr < 9012) {
 			pitch = pavg;
 		} else {
 			t2 = (t > 12800) ? 89 : 115;
 			pitch = double_chk(&sb[LPF_ORD + PITCH_FR / 2], &pcorr, t, t2, PITCHMIN,
-					   PITCHMAX, PITCHMIN_Q7, PITCHMAX_Q7, 160);
+					   PITCHMAX, PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
 		}
 	} else {
 		t2 = (t > 12800) ? 64 : 96;
 		pitch = double_chk(&sb[LPF_ORD + PITCH_FR / 2], &pcorr, t, t2, PITCHMIN, PITCHMAX,
-				   PITCHMIN_Q7, PITCHMAX_Q7, 160);
+				   PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
 	}
 	if (pcorr < 9012)
 		pitch = pavg;
@@ -783,12 +1001,13 @@ MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int1
 	const int16_t *sp = &speech[PITCH_FR - FRAME - PITCHMAX];
 	int16_t *w = &sb[BPF_ORD];
 	int64_t e = bp_window(E->bpfsp[0], sp, w, bden, bnum, E->bpfdelin[0], E->bpfdelout[0]);
-	f_pitch_scale_e(w, w, PITCH_FR, e);
+	bool ex;
+	f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
 	*pitch = frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[0], fpitch[0], 5, PITCHMIN, PITCHMAX,
-			  PITCHMIN_Q7, PITCHMAX_Q7, 160);
+			  PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
 	for (int i = 1; i < 2; i++) {	/* NUM_PITCHES */
 		t = frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, fpitch[i], 5, PITCHMIN, PITCHMAX,
-			     PITCHMIN_Q7, PITCHMAX_Q7, 160);
+			     PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
 		if (pcorr > bpvc[0]) {
 			*pitch = t;
 			bpvc[0] = pcorr;
@@ -797,18 +1016,18 @@ MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int1
 	for (int i = 1; i < NUM_BANDS; i++) {
 		int fi = i * (BPF_ORD / 2) * 3;
 		e = bp_window(E->bpfsp[i], sp, w, bden + fi, bnum + fi, E->bpfdelin[i], E->bpfdelout[i]);
-		sc = f_pitch_scale_e(w, w, PITCH_FR, e);
+		sc = f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
 		frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[i], *pitch, 0, PITCHMIN, PITCHMAX,
-			 PITCHMIN_Q7, PITCHMAX_Q7, 160);
+			 PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
 		/* envelope: the history samples are re-scaled to this frame's scale */
 		t = shr(E->envdel2[i], sc);
 		E->envdel2[i] = shr(sb[BPF_ORD + FRAME - 1], (Word16) -sc);
 		v_equ_shr(&sb[BPF_ORD - ENV_ORD], E->envdel[i], sc, ENV_ORD);
 		e = envelope_e(w, t, w, PITCH_FR);
 		v_equ_shr(E->envdel[i], &sb[BPF_ORD + FRAME - ENV_ORD], (Word16) -sc, ENV_ORD);
-		f_pitch_scale_e(w, w, PITCH_FR, e);
+		f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
 		frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, *pitch, 0, PITCHMIN, PITCHMAX,
-			 PITCHMIN_Q7, PITCHMAX_Q7, 160);
+			 PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
 		pcorr = sub(pcorr, 1638);
 		if (pcorr > bpvc[i])
 			bpvc[i] = pcorr;
@@ -981,6 +1200,13 @@ MD void peak_insert(int16_t *tv, int16_t *tj, int16_t v, int16_t j)
 	}
 }
 
+/* corPeak's lag block: acc[k] = sum_t pa[t + k / 2] * pq[t + 4 - (k + 1) / 2] */
+struct CpLags {
+	static constexpr int NA = 4, NB = 5;
+	static constexpr int oa(int k) { return k / 2; }
+	static constexpr int ob(int k) { return 4 - (k + 1) / 2; }
+};
+
 /* corPeak :216 */
 MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 {
@@ -1048,6 +1274,14 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 		if ((n & 7) == 0 && n + 8 <= NL_BLK) {
 			const int16_t *pa = &pb[1 + n / 2];
 			const int16_t *pq = &pb[143 - n / 2];
+#if !defined(MELPE_OPCOUNT)
+			/* exact on packed pairs: the a samples split as 256 hi8 + lo8
+			 * keep both halves' 73-term sums within 32 bits */
+			int32_t hl[16];
+			xcorr_pairs<8, CpLags, true>(pa, pq, PW, hl);
+			for (int k = 0; k < 8; k++)
+				blk[k] = 2 * (256 * (int64_t) hl[k] + hl[8 + k]);
+#else
 			int64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 			int a0 = pa[0], a1 = pa[1], a2 = pa[2];
 			int q0 = pq[0], q1 = pq[1], q2 = pq[2], q3 = pq[3];
@@ -1083,6 +1317,7 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 				step(pa[t + 3], pq[t + 4]);
 			for (int k = 0; k < 8; k++)
 				blk[k] = 2 * acc[k];
+#endif
 		}
 		if (i % 2 == 0) {
 			r0 = L40_shr((Word40) Lr0, r0s);
@@ -1298,10 +1533,28 @@ MN Word16 bandEn(const int16_t *ac, int band)
  * The sums are 2*x*y over at most 200 terms, |sum| < 2^39: the 40-bit
  * clamp of L40_mac never acts, so int64 sums are the reference's values. */
 template <int ODD>
+struct FcLags {
+	static constexpr int NA = 6, NB = 6;
+	static constexpr int lon(int n) { return ODD ? n / 2 + 1 : (n + 1) / 2; }
+	static constexpr int oa(int n) { return lon(n) - (ODD ? 1 : 0); }
+	static constexpr int ob(int n) { return lon(n) - n + 4; }
+};
+
+template <int ODD>
 MD void fc_corr10(const int16_t *in, int hp, int win, Word40 *A)
 {
 	constexpr int lo0 = ODD ? 1 : 0, lo9 = 5;
 	const int16_t *pa = &in[lo0], *pb = &in[lo9 + hp - 10];
+#if !defined(MELPE_OPCOUNT)
+	/* exact on packed pairs, a split as 256 hi8 + lo8 (win <= 200 terms) */
+	{
+		int32_t hl[20];
+		xcorr_pairs<10, FcLags<ODD>, true>(pa, pb, win, hl);
+		for (int n = 0; n < 10; n++)
+			A[n] = 2 * (256 * (int64_t) hl[n] + hl[10 + n]);
+		return;
+	}
+#endif
 	int64_t acc[10];
 	int av[6], bv[6];
 	for (int k = 0; k < 10; k++)

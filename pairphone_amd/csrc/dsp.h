@@ -72,6 +72,355 @@ MD uint32_t p16_next(P16 &r)
 MD int16_t lo16(uint32_t v) { return (int16_t) (v & 0xffffu); }
 MD int16_t hi16(uint32_t v) { return (int16_t) (v >> 16); }
 
+/*
+ * Exact correlation sums on packed pairs.  Where a caller has proved that a
+ * saturating L_mac chain cannot clamp (every partial sum of |2ab|, in any
+ * order, stays within 32 bits), the chain equals the plain integer sum, which
+ * may then be formed in any order: two products per v_dot2_i32_i16 instead
+ * of a mul and two clamped adds per product.
+ */
+MD int32_t sdot2(uint32_t a, uint32_t b, int32_t c)	/* c + a.lo*b.lo + a.hi*b.hi */
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+	typedef short v2s __attribute__((ext_vector_type(2)));
+	return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s, a), __builtin_bit_cast(v2s, b), c,
+				      false);
+#else
+	return (int32_t) ((uint32_t) c + (uint32_t) ((int32_t) lo16(a) * lo16(b)) +
+			  (uint32_t) ((int32_t) hi16(a) * hi16(b)));
+#endif
+}
+
+/* c + a.lo*b.lo + a.hi*b.hi, saturated to 32 bits (the clamp bit) */
+MD int32_t sdot2_sat(uint32_t a, uint32_t b, int32_t c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+	typedef short v2s __attribute__((ext_vector_type(2)));
+	return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s, a), __builtin_bit_cast(v2s, b), c,
+				      true);
+#else
+	int64_t v = (int64_t) c + (int64_t) lo16(a) * lo16(b) + (int64_t) hi16(a) * hi16(b);
+	return v > LW_MAX_ ? LW_MAX_ : (v < LW_MIN_ ? LW_MIN_ : (int32_t) v);
+#endif
+}
+
+/* the pair one sample later: (lo's high half, hi's low half) */
+MD uint32_t pair_mid(uint32_t hi, uint32_t lo)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+	return __builtin_amdgcn_alignbit(hi, lo, 16);
+#else
+	return (lo >> 16) | (hi << 16);
+#endif
+}
+
+/* x = 256 * hi8(x) + lo8(x) per half: hi8 signed (arithmetic >> 8), lo8 in
+ * [0, 255] -- products with an int16 then fit 23 bits, so up to 256 of them
+ * sum exactly in 32 */
+MD uint32_t pk_hi8(uint32_t x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+	typedef short v2s __attribute__((ext_vector_type(2)));
+	return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2s, x) >> (v2s) {8, 8});
+#else
+	return (uint32_t) (uint16_t) (lo16(x) >> 8) | ((uint32_t) (uint16_t) (hi16(x) >> 8) << 16);
+#endif
+}
+MD uint32_t pk_lo8(uint32_t x) { return x & 0x00ff00ffu; }
+
+/*
+ * Pair streams for the exact correlators.  PairStream p[0..n) yields the
+ * pairs (p[2m], p[2m+1]), m < ceil(n/2), p[n] taken as 0 when n is odd.
+ * Raw dword d of the stream is the d-th aligned dword from p (p + 1 for an
+ * odd start); those wholly inside p[0..n) are "full", the one holding the
+ * last sample alone is the "partial" one, read as a 16-bit load.  Pair m is
+ * raw dword m (even start) or the perm of raw m and m - 1 (odd start, raw
+ * -1 being p[0] << 16).  Nothing outside p[0..n) is read.
+ */
+struct PairStream {
+	const u32_alias *w;
+	uint32_t sel, prev0, partial;
+	int nfull;
+};
+MD void ps_open(PairStream &s, const int16_t *p, int n)
+{
+	int odd = (int) ((reinterpret_cast<uintptr_t>(p) >> 1) & 1);
+	s.w = reinterpret_cast<const u32_alias *>(p + odd);
+	s.sel = odd ? 0x05040302u : 0x07060504u;
+	s.prev0 = odd ? (uint32_t) (uint16_t) p[0] << 16 : 0u;
+	s.nfull = odd ? (n - 1) >> 1 : n >> 1;
+	s.partial = (odd ^ (n & 1)) ? (uint32_t) (uint16_t) p[n - 1] : 0u;
+}
+/* raw dword d >= 0, any d: full ones loaded (index clamped, so the load is
+ * always inside), the partial one and anything past it selected */
+MD uint32_t ps_raw(const PairStream &s, int d)
+{
+	int c = d < s.nfull ? d : s.nfull - 1;
+	uint32_t v = s.w[c > 0 ? c : 0];
+	v = d < s.nfull ? v : (d == s.nfull ? s.partial : 0u);
+	return d < 0 ? s.prev0 : v;
+}
+/* four consecutive pairs m0 .. m0 + 3 (m0 >= 1), loads issued together */
+MD void ps_pairs4(const PairStream &s, int m0, uint32_t *out)
+{
+	uint32_t r[5];
+	#pragma unroll
+	for (int i = 0; i < 5; i++)
+		r[i] = ps_raw(s, m0 - 1 + i);
+	#pragma unroll
+	for (int i = 0; i < 4; i++)
+		out[i] = perm_b32(r[i + 1], r[i], s.sel);
+}
+/* pairs 0 .. N-1 (N small), loads issued together */
+template <int N>
+MD void ps_head(const PairStream &s, uint32_t *out)
+{
+	uint32_t r[N > 0 ? N : 1];
+	#pragma unroll
+	for (int i = 0; i < N; i++)
+		r[i] = ps_raw(s, i);
+	#pragma unroll
+	for (int i = 0; i < N; i++)
+		out[i] = perm_b32(r[i], i ? r[i - 1] : s.prev0, s.sel);
+}
+/* full four-dword groups available from pair m0 on */
+MD int ps_full_groups(const PairStream &s, int m0)
+{
+	int g = (s.nfull - m0) >> 2;
+	return g > 0 ? g : 0;
+}
+
+/* Chunks of four full raw dwords (pairs m0 + 4c .. m0 + 4c + 3), PD chunks
+ * in flight: next4() returns chunk c and issues the load of chunk c + PD
+ * (past the last chunk the last one is re-read, never a dword outside). */
+template <int PD>
+struct P16C {
+	const u32_alias *w;
+	uint32_t prev, sel;
+	uint32_t buf[PD][4];
+	int next, last;
+};
+template <int PD>
+MD void p16c_load(P16C<PD> &s, uint32_t *d)
+{
+	int c = s.next < s.last ? s.next : s.last;
+	const u32_alias *q = s.w + 4 * c;
+	d[0] = q[0];
+	d[1] = q[1];
+	d[2] = q[2];
+	d[3] = q[3];
+	s.next++;
+}
+template <int PD>
+MD void p16c_open(P16C<PD> &s, const PairStream &ps, int m0, int nchunks)
+{
+	s.w = ps.w + m0;
+	s.prev = m0 > 0 ? ps.w[m0 - 1] : ps.prev0;
+	s.sel = ps.sel;
+	s.next = 0;
+	s.last = nchunks - 1;
+	if (nchunks > 0)
+		#pragma unroll
+		for (int d = 0; d < PD; d++)
+			p16c_load(s, s.buf[d]);
+}
+template <int PD>
+MD void p16c_next4(P16C<PD> &s, uint32_t *out)
+{
+	uint32_t raw[4];
+	#pragma unroll
+	for (int i = 0; i < 4; i++)
+		raw[i] = s.buf[0][i];
+	#pragma unroll
+	for (int d = 0; d + 1 < PD; d++)
+		#pragma unroll
+		for (int i = 0; i < 4; i++)
+			s.buf[d][i] = s.buf[d + 1][i];
+	p16c_load(s, s.buf[PD - 1]);
+	#pragma unroll
+	for (int i = 0; i < 4; i++)
+		out[i] = perm_b32(raw[i], i ? raw[i - 1] : s.prev, s.sel);
+	s.prev = raw[3];
+}
+
+#ifndef MELPE_XC_PD
+#define MELPE_XC_PD 2
+#endif
+
+/*
+ * K lag sums of one block, exactly: out[k] = sum_{j<len} pa[j + S::oa(k)] *
+ * pb[j + S::ob(k)], 0 <= oa < S::NA, 0 <= ob < S::NB.  Reads pa[0 .. len +
+ * NA - 1) and pb[0 .. len + NB - 1) only.  The sums must fit 32 bits (the
+ * caller's bound); with SPLIT the a samples are split as 256 * hi8 + lo8 and
+ * the two 32-bit halves returned separately (hi in out[k], lo in out[K + k]),
+ * for sums that only fit 40 bits.
+ *
+ * Steps t take j = 2t, 2t + 1 from windows of pairs: a pair at an even
+ * offset o is window entry o / 2, one at an odd offset the pair_mid of two
+ * neighbours.  Steps go four at a time, each group refilling the windows
+ * with four pairs per stream: full chunks prefetched ahead (P16C), the last
+ * groups through clamped loads with the steps past the end masked off.  Only
+ * an odd len leaves one j, summed sample by sample.
+ */
+template <int K, class S, bool SPLIT>
+MD void xcorr_pairs(const int16_t *pa, const int16_t *pb, int len, int32_t *out)
+{
+	constexpr int NA = S::NA, NB = S::NB;
+	constexpr int MA = NA / 2 + 1, MB = NB / 2 + 1;	/* pairs a step reads */
+	constexpr int NH = SPLIT ? 2 : 1;
+	constexpr int PD = MELPE_XC_PD;
+	int32_t acc[NH * K];
+	#pragma unroll
+	for (int k = 0; k < NH * K; k++)
+		acc[k] = 0;
+	const int T = len >> 1;
+	int jt = 0;	/* first j of the sample-by-sample tail */
+	if (T >= 4) {
+		PairStream sa, sb;
+		ps_open(sa, pa, len + NA - 1);
+		ps_open(sb, pb, len + NB - 1);
+		/* windows of steps 4g .. 4g + 3: pairs (and mids) */
+		uint32_t wa[NH][MA + 3], ma[NH][MA + 3], wb[MB + 3], mb[MB + 3];
+		auto put_a = [&](int m, uint32_t x) {
+			wa[0][m] = SPLIT ? pk_hi8(x) : x;
+			if (SPLIT)
+				wa[NH - 1][m] = pk_lo8(x);
+		};
+		{
+			uint32_t ha[MA], hb[MB];
+			ps_head<MA - 1>(sa, ha);
+			ps_head<MB - 1>(sb, hb);
+			#pragma unroll
+			for (int m = 0; m < MA - 1; m++)
+				put_a(m, ha[m]);
+			#pragma unroll
+			for (int m = 0; m < MB - 1; m++)
+				wb[m] = hb[m];
+		}
+		#pragma unroll
+		for (int m = 0; m + 1 < MA - 1; m++)
+			#pragma unroll
+			for (int h = 0; h < NH; h++)
+				ma[h][m] = pair_mid(wa[h][m + 1], wa[h][m]);
+		#pragma unroll
+		for (int m = 0; m + 1 < MB - 1; m++)
+			mb[m] = pair_mid(wb[m + 1], wb[m]);
+		/* one group: the four new pairs xa/xb, steps st < nst */
+		auto group = [&](const uint32_t *xa, const uint32_t *xb, int nst) {
+			#pragma unroll
+			for (int i = 0; i < 4; i++) {
+				put_a(MA - 1 + i, xa[i]);
+				wb[MB - 1 + i] = xb[i];
+			}
+			#pragma unroll
+			for (int m = MA - 2; m < MA + 2; m++)
+				#pragma unroll
+				for (int h = 0; h < NH; h++)
+					if (m >= 0)
+						ma[h][m] = pair_mid(wa[h][m + 1], wa[h][m]);
+			#pragma unroll
+			for (int m = MB - 2; m < MB + 2; m++)
+				if (m >= 0)
+					mb[m] = pair_mid(wb[m + 1], wb[m]);
+			#pragma unroll
+			for (int st = 0; st < 4; st++)
+				#pragma unroll
+				for (int k = 0; k < K; k++) {
+					const int oa = S::oa(k), ob = S::ob(k);
+					const int ia = st + (oa >> 1), ib = st + (ob >> 1);
+					uint32_t y = (ob & 1) ? mb[ib] : wb[ib];
+					#pragma unroll
+					for (int h = 0; h < NH; h++) {
+						uint32_t x = (oa & 1) ? ma[h][ia] : wa[h][ia];
+						int32_t v = sdot2(x, y, acc[h * K + k]);
+						acc[h * K + k] = st < nst ? v : acc[h * K + k];
+					}
+				}
+			#pragma unroll
+			for (int m = 0; m < MA - 1; m++)
+				#pragma unroll
+				for (int h = 0; h < NH; h++) {
+					wa[h][m] = wa[h][m + 4];
+					if (m < MA - 2)
+						ma[h][m] = ma[h][m + 4];
+				}
+			#pragma unroll
+			for (int m = 0; m < MB - 1; m++) {
+				wb[m] = wb[m + 4];
+				if (m < MB - 2)
+					mb[m] = mb[m + 4];
+			}
+		};
+		int G = T >> 2, ga = ps_full_groups(sa, MA - 1), gb = ps_full_groups(sb, MB - 1);
+		G = G < ga ? G : ga;
+		G = G < gb ? G : gb;
+		if (G > 0) {
+			P16C<PD> ca, cb;
+			p16c_open(ca, sa, MA - 1, G);
+			p16c_open(cb, sb, MB - 1, G);
+			for (int g = 0; g < G; g++) {
+				uint32_t xa[4], xb[4];
+				p16c_next4(ca, xa);
+				p16c_next4(cb, xb);
+				group(xa, xb, 4);
+			}
+		}
+		for (int t = 4 * G; t < T; t += 4) {
+			uint32_t xa[4], xb[4];
+			ps_pairs4(sa, MA - 1 + t, xa);
+			ps_pairs4(sb, MB - 1 + t, xb);
+			group(xa, xb, T - t);
+		}
+		jt = 2 * T;
+	}
+	/* an odd len's last j (or a short len's every j), sample by sample */
+	for (int j = jt; j < len; j++) {
+		#pragma unroll
+		for (int k = 0; k < K; k++) {
+			int x = pa[j + S::oa(k)], y = pb[j + S::ob(k)];
+			if (SPLIT) {
+				acc[k] += (x >> 8) * y;
+				acc[K + k] += (x & 0xff) * y;
+			} else {
+				acc[k] += x * y;
+			}
+		}
+	}
+	#pragma unroll
+	for (int k = 0; k < NH * K; k++)
+		out[k] = acc[k];
+}
+
+/* find_pitch's lag blocks (fp_corrK below): lag n0 + k reads
+ * pa[j + (k + 1) / 2] * pb[j + (k + 1) / 2 - k + BMAX], BMAX = (K - 1) - K / 2 */
+template <int K>
+struct FpLags {
+	static constexpr int BMAX = (K - 1) - K / 2;
+	static constexpr int NA = K / 2 + 1, NB = BMAX + 1;
+	static constexpr int oa(int k) { return (k + 1) / 2; }
+	static constexpr int ob(int k) { return (k + 1) / 2 - k + BMAX; }
+};
+
+/* sum of squares, exactly (caller's bound) */
+MD int32_t magsq_pairs(const int16_t *p, int n)
+{
+	int32_t acc0 = 0, acc1 = 0;
+	P16 r;
+	int np = p16_open(r, p, n);
+	int i = 0;
+	#pragma unroll 4
+	for (int k = 0; k < np; k++, i += 2) {
+		uint32_t x = p16_next(r);
+		if (k & 1)
+			acc1 = sdot2(x, x, acc1);
+		else
+			acc0 = sdot2(x, x, acc0);
+	}
+	for (; i < n; i++)
+		acc0 += (int32_t) p[i] * p[i];
+	return acc0 + acc1;
+}
+
 /* ------------------------------------------------------------------ */
 /* vectors: melpe/mat_lib.c                                           */
 /* ------------------------------------------------------------------ */

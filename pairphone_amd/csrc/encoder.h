@@ -38,9 +38,10 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 	v_copy(&sb[LPF_ORD], &speech[PITCH_BEG], PITCH_FR);
 	iir3_s(&sb[LPF_ORD], TB(lpf_den), TB(lpf_num), E->lpfsp_delin, E->lpfsp_delout,
 	       PITCH_FR, FRAME);
-	f_pitch_scale(&sb[LPF_ORD], &sb[LPF_ORD], PITCH_FR);
+	bool ex;
+	f_pitch_scale(&sb[LPF_ORD], &sb[LPF_ORD], PITCH_FR, &ex);
 	E->fpitch[1] = find_pitch(&sb[LPF_ORD + PITCH_FR / 2], &dontcare, 2 * PITCHMIN,
-				  PITCHMAX, PITCHMAX);
+				  PITCHMAX, PITCHMAX, ex);
 	E->fpitch[1] = shl(E->fpitch[1], 7);
 	bpvc_ana(E, &speech[FRAME_END], E->fpitch, par->bpvc, &sub_pitch);
 	par->jitter = (par->bpvc[0] < VJIT_Q14) ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;

@@ -10,7 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["MELPE_AMD_LIB"] = os.path.join(ROOT, "pairphone_amd", "libmelpe_amd_prof.so")
+os.environ.setdefault("MELPE_AMD_LIB", os.path.join(ROOT, "pairphone_amd", "libmelpe_amd_prof.so"))
 
 import numpy as np  # noqa: E402
 
