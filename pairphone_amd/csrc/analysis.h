@@ -161,7 +161,7 @@ MD void q_bpvc_dec(int16_t *bpvc, Word16 idx, int16_t uv, int nb)
  * exact correlators off (every chain runs sequentially), MELPE_EXACT_STATS
  * counts the frac_pch / find_pitch calls that took each path. */
 #if defined(MELPE_EXACT_STATS) && !defined(__HIP__)
-extern "C" long melpe_exact_stats[4];
+extern "C" long melpe_exact_stats[6];
 #define EXACT_STAT(i) (melpe_exact_stats[i]++)
 #else
 #define EXACT_STAT(i) ((void) 0)
@@ -189,6 +189,7 @@ MD int32_t shr_energy_inplace(int16_t *p, int n, Word16 sc)
 	if (G > 0)
 		for (int k = 0; k < 4; k++)
 			cur[k] = w[k];
+	#pragma unroll 1
 	for (int g = 0; g < G; g++) {
 		int gn = g + 1 < G ? g + 1 : g;
 		uint32_t nxt[4];
@@ -452,6 +453,7 @@ MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q)
 			P16C<PD> ca, cb;
 			p16c_open(ca, sa, 0, G);
 			p16c_open(cb, sb, 1, G);
+			#pragma unroll 1
 			for (int g = 0; g < G; g++) {
 				uint32_t xa[4];
 				p16c_next4(ca, xa);
@@ -459,6 +461,7 @@ MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q)
 				group(xa, 4);
 			}
 		}
+		#pragma unroll 1
 		for (int t = 4 * G; t < T; t += 4) {
 			uint32_t xa[4];
 			ps_pairs4(sa, t, xa);
@@ -529,9 +532,24 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 	const bool one = false;
 	Word32 *blk12 = blk;
 #endif
+	/* the energy updates' samples, loaded eight lags ahead: the c00 update
+	 * of lag n0 + 2k reads sig[cb0 + n0/2 + k] (and + len), the cTT update
+	 * of lag n0 + 2k + 1 sig[cb0 + upper - 1 - n0/2 - k] (and + len); each
+	 * register queue moves up by one per update */
+	int16_t qa[4], qal[4], qb[4], qbl[4];
 	for (Word16 i = upper; i >= lower; i--) {
 		int n = upper - i;
 		Word32 corr;
+		if ((n & 7) == 0) {
+			const int16_t *pa = &sig[cb0 + n / 2], *pb = &sig[cb0 + upper - 1 - n / 2];
+			#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				qa[k] = pa[k];
+				qal[k] = pa[k + len];
+				qb[k] = pb[-k];
+				qbl[k] = pb[len - k];
+			}
+		}
 		if (one) {
 			corr = blk12[n];
 		} else if ((n & 7) == 0 && (exact || n + 8 <= nlags)) {
@@ -581,15 +599,27 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 		}
 		if (even) {
 			even = false;
-			c00 = L_msu(c00, sig[cb], sig[cb]);
-			c00 = L_mac(c00, sig[cb + len], sig[cb + len]);
+			c00 = L_msu(c00, qa[0], qa[0]);	/* sig[cb], sig[cb + len] */
+			c00 = L_mac(c00, qal[0], qal[0]);
 			cb = add(cb, 1);
+			#pragma unroll
+			for (int k = 0; k < 3; k++) {
+				qa[k] = qa[k + 1];
+				qal[k] = qal[k + 1];
+			}
 		} else {
 			even = true;
-			cTT = L_msu(cTT, sig[cb + i - 1 + len], sig[cb + i - 1 + len]);
-			cTT = L_mac(cTT, sig[cb + i - 1], sig[cb + i - 1]);
+			/* sig[cb + i - 1 + len], sig[cb + i - 1] */
+			cTT = L_msu(cTT, qbl[0], qbl[0]);
+			cTT = L_mac(cTT, qb[0], qb[0]);
+			#pragma unroll
+			for (int k = 0; k < 3; k++) {
+				qb[k] = qb[k + 1];
+				qbl[k] = qbl[k + 1];
+			}
 		}
 	}
+	(void) cb;
 	*pcorr = shr(sqrt_fxp(divide_s(extract_l(max_num), extract_l(max_den)), 15), 1);
 	return ip;
 }
@@ -965,9 +995,23 @@ MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int1
 MD int64_t bp_window(int16_t *hist, const int16_t *sp, int16_t *w, const int16_t *den,
 		     const int16_t *num, int16_t *din, int16_t *dout)
 {
+	PROF_SCOPE(47);
 	const int H = PITCH_FR - FRAME;	/* 141 */
 	int64_t e = 0;
-	for (int k = 0; k < H; k++) {
+	int k = 0;
+	#pragma unroll 1
+	for (; k + 8 <= H; k += 8) {	/* eight loads issued together */
+		int16_t v[8];
+		#pragma unroll
+		for (int q = 0; q < 8; q++)
+			v[q] = hist[k + q];
+		#pragma unroll
+		for (int q = 0; q < 8; q++) {
+			w[k + q] = v[q];
+			e += L_mult(v[q], v[q]);
+		}
+	}
+	for (; k < H; k++) {
 		int16_t v = hist[k];
 		w[k] = v;
 		e += L_mult(v, v);
@@ -1267,10 +1311,23 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 	const int NL_BLK = (NL + 7) & ~7;
 #endif
 	int64_t blk[8];
+	/* the r0 / rk updates' samples, loaded eight lags ahead (pb[lo + k],
+	 * pb[lo + k + PW]; pb[hi - 1 - k], pb[hi - 1 - k + PW]), each register
+	 * queue moving up by one per update */
+	int16_t qa[4], qal[4], qb[4], qbl[4];
 	{
 	PROF_SCOPE(39);
 	for (int i = MAXPITCH - 1; i >= MINPITCH; i--) {
 		int n = MAXPITCH - 1 - i;
+		if ((n & 7) == 0) {
+			#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				qa[k] = pb[lo + k];
+				qal[k] = pb[lo + k + PW];
+				qb[k] = pb[hi - 1 - k];
+				qbl[k] = pb[hi - 1 - k + PW];
+			}
+		}
 		if ((n & 7) == 0 && n + 8 <= NL_BLK) {
 			const int16_t *pa = &pb[1 + n / 2];
 			const int16_t *pq = &pb[143 - n / 2];
@@ -1321,16 +1378,26 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 		}
 		if (i % 2 == 0) {
 			r0 = L40_shr((Word40) Lr0, r0s);
-			r0 = L40_msu(r0, pb[lo], pb[lo]);
-			r0 = L40_mac(r0, pb[lo + PW], pb[lo + PW]);
+			r0 = L40_msu(r0, qa[0], qa[0]);	/* pb[lo], pb[lo + PW] */
+			r0 = L40_mac(r0, qal[0], qal[0]);
 			norm40(&r0, &r0s, &Lr0);
 			lo++;
+			#pragma unroll
+			for (int k = 0; k < 3; k++) {
+				qa[k] = qa[k + 1];
+				qal[k] = qal[k + 1];
+			}
 		} else {
 			hi--;
 			rk = L40_shr((Word40) Lrk, rks);
-			rk = L40_mac(rk, pb[hi], pb[hi]);
-			rk = L40_msu(rk, pb[hi + PW], pb[hi + PW]);
+			rk = L40_mac(rk, qb[0], qb[0]);	/* pb[hi], pb[hi + PW] */
+			rk = L40_msu(rk, qbl[0], qbl[0]);
 			norm40(&rk, &rks, &Lrk);
+			#pragma unroll
+			for (int k = 0; k < 3; k++) {
+				qb[k] = qb[k + 1];
+				qbl[k] = qbl[k + 1];
+			}
 		}
 		if (n < NL_BLK) {
 			A = blk[n & 7];
@@ -1598,6 +1665,7 @@ MD void fc_corr10(const int16_t *in, int hp, int win, Word40 *A)
 /* frac_cor :504 -- best normalised correlation within +-5 of pitch */
 MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 {
+	PROF_SCOPE(46);
 	Word16 lp = sub(pitch, 5), hp = add(pitch, 5);
 	if (lp < MINPITCH)
 		lp = MINPITCH;
@@ -1706,6 +1774,7 @@ MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *
 	 * with the four two-sample histories in registers; what is left in
 	 * bpfdel afterwards is the same last-two-samples of each stage. */
 	{
+		PROF_SCOPE(45);
 		const int16_t *pn = TB(bpf_num), *pd = TB(bpf_den);
 		Biq bq[3];
 		for (int k = 0; k < 3; k++) {

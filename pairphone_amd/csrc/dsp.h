@@ -358,6 +358,7 @@ MD void xcorr_pairs(const int16_t *pa, const int16_t *pb, int len, int32_t *out)
 			P16C<PD> ca, cb;
 			p16c_open(ca, sa, MA - 1, G);
 			p16c_open(cb, sb, MB - 1, G);
+			#pragma unroll 1
 			for (int g = 0; g < G; g++) {
 				uint32_t xa[4], xb[4];
 				p16c_next4(ca, xa);
@@ -365,6 +366,7 @@ MD void xcorr_pairs(const int16_t *pa, const int16_t *pb, int len, int32_t *out)
 				group(xa, xb, 4);
 			}
 		}
+		#pragma unroll 1
 		for (int t = 4 * G; t < T; t += 4) {
 			uint32_t xa[4], xb[4];
 			ps_pairs4(sa, MA - 1 + t, xa);
@@ -793,6 +795,7 @@ MN void envelope(const int16_t *in, int16_t prev_in, int16_t *out, int n)
  * wrote, for f_pitch_scale_e (bpvc_ana) */
 MD int64_t envelope_e(const int16_t *in, int16_t prev_in, int16_t *out, int n)
 {
+	PROF_SCOPE(48);
 	Word16 pa = abs_s(prev_in), y1 = out[-1], y2 = out[-2];
 	int64_t e = 0;
 	for (int i = 0; i < n; i++) {
@@ -1296,15 +1299,31 @@ MD void iir3_s_io(const int16_t *in, int16_t *out, const int16_t *den, const int
 		b[s].o0 = dout[2 * s];
 		b[s].o1 = dout[2 * s + 1];
 	}
+	/* in place or disjoint: inputs are read one group of four ahead of the
+	 * outputs written */
 	int i = 0;
-	for (; i + 4 <= n; i += 4) {
-		int16_t v[4] = {in[i], in[i + 1], in[i + 2], in[i + 3]};
+	if (n >= 4) {
+		int16_t v[4] = {in[0], in[1], in[2], in[3]};
+		#pragma unroll 1
+		for (; i + 8 <= n; i += 4) {
+			int16_t nv[4] = {in[i + 4], in[i + 5], in[i + 6], in[i + 7]};
+			#pragma unroll
+			for (int q = 0; q < 4; q++) {
+				int16_t y = biq_step(b[2], biq_step(b[1], biq_step(b[0], v[q])));
+				out[i + q] = y;
+				f(i + q, y);
+			}
+			#pragma unroll
+			for (int q = 0; q < 4; q++)
+				v[q] = nv[q];
+		}
 		#pragma unroll
 		for (int q = 0; q < 4; q++) {
 			int16_t y = biq_step(b[2], biq_step(b[1], biq_step(b[0], v[q])));
 			out[i + q] = y;
 			f(i + q, y);
 		}
+		i += 4;
 	}
 	for (; i < n; i++) {
 		int16_t y = biq_step(b[2], biq_step(b[1], biq_step(b[0], in[i])));
@@ -2092,21 +2111,38 @@ MN Word16 cfft_pk(uint32_t *x, int nn, Word16 mx, Word16 *omx)
 	PROF_SCOPE(30);
 	const int16_t *wrt = g_der.wr, *wit = g_der.wi;
 	Word16 g = 0;
-	/* bit reversal (the reference's j recurrence on 1-based short indices) */
+	/* bit reversal: the reference's j recurrence on 1-based short indices
+	 * swaps sample i with r = bitrev(i) whenever r > i.  The swaps are
+	 * disjoint, so they go eight samples at a time, every load of a batch
+	 * issued before its stores. */
 	{
-		int n = 2 * nn, j = 1;
-		for (int i = 1; i < n; i += 2) {
-			if (j > i) {
-				uint32_t t = x[(j - 1) >> 1];
-				x[(j - 1) >> 1] = x[(i - 1) >> 1];
-				x[(i - 1) >> 1] = t;
+		const int lg = 31 - __builtin_clz(nn);
+		auto rev = [lg](int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+			return (int) (__builtin_bitreverse32((uint32_t) i) >> (32 - lg));
+#else
+			int r = 0;
+			for (int b = 0; b < lg; b++)
+				r |= ((i >> b) & 1) << (lg - 1 - b);
+			return r;
+#endif
+		};
+		#pragma unroll 1
+		for (int i0 = 0; i0 < nn; i0 += 8) {
+			uint32_t xi[8], xr[8];
+			int r[8];
+			#pragma unroll
+			for (int k = 0; k < 8; k++) {
+				r[k] = rev(i0 + k);
+				xi[k] = x[i0 + k];
+				xr[k] = x[r[k]];
 			}
-			int m = nn;
-			while (m >= 2 && j > m) {
-				j -= m;
-				m >>= 1;
-			}
-			j += m;
+			#pragma unroll
+			for (int k = 0; k < 8; k++)
+				if (r[k] > i0 + k) {
+					x[i0 + k] = xr[k];
+					x[r[k]] = xi[k];
+				}
 		}
 	}
 	Word16 s = 0;
@@ -2147,7 +2183,12 @@ MN Word16 cfft_pk(uint32_t *x, int nn, Word16 mx, Word16 *omx)
 		x[k + 3] = b1;
 		mx = pk_amax(b1, pk_amax(a1, pk_amax(b0, pk_amax(a0, mx))));
 	}
-	/* radix-2 stages; half = the reference's mmax / 2 in complex samples */
+	/* radix-2 stages; half = the reference's mmax / 2 in complex samples.
+	 * A stage's butterflies are independent (and the guard max is order
+	 * free), so they go four at a time -- twiddles m0 .. m0 + 3 of one group,
+	 * two contiguous quads of samples -- with the next quad pair loaded before
+	 * this one is stored.  Twiddle m is the reference's running table index
+	 * m * istep, m = 0 taking (SW_MAX, 0). */
 	int istep_idx = nn >> 1;
 	for (int half = 4; half < nn; half <<= 1) {
 		s = 0;
@@ -2159,14 +2200,35 @@ MN Word16 cfft_pk(uint32_t *x, int nn, Word16 mx, Word16 *omx)
 			s = 1;
 		}
 		istep_idx >>= 1;
-		int idx = 0;
-		Word16 wr = SW_MAX_, wi = 0;
 		Word16 nmx = 0;
-		for (int m = 0; m < half; m++) {
-			for (int ci = m; ci < nn; ci += 2 * half) {
-				int cj = ci + half;
-				uint32_t P = pk_shr(x[ci], s), Q = pk_shr(x[cj], s);
-				Word16 pr = pk_re(P), pi = pk_im(P), qr = pk_re(Q), qi = pk_im(Q);
+		const int nb = nn >> 3;	/* quads of butterflies */
+		auto base = [half](int b) { int q = 4 * b; return (q / half) * 2 * half + q % half; };
+		uint32_t P[4], Q[4];
+		{
+			const int c0 = base(0);
+			#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				P[k] = x[c0 + k];
+				Q[k] = x[c0 + half + k];
+			}
+		}
+		#pragma unroll 1
+		for (int b = 0; b < nb; b++) {
+			const int ci = base(b), cn = base(b + 1 < nb ? b + 1 : b);
+			uint32_t NP[4], NQ[4];
+			#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				NP[k] = x[cn + k];
+				NQ[k] = x[cn + half + k];
+			}
+			const int m0 = ci & (half - 1);
+			#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				const int m = m0 + k;
+				Word16 wr = m ? wrt[m * istep_idx] : (Word16) SW_MAX_;
+				Word16 wi = m ? wit[m * istep_idx] : (Word16) 0;
+				uint32_t Pk = pk_shr(P[k], s), Qk = pk_shr(Q[k], s);
+				Word16 pr = pk_re(Pk), pi = pk_im(Pk), qr = pk_re(Qk), qi = pk_im(Qk);
 				Word32 tr = L_add(L_mult(wr, qr), L_mult(wi, qi));
 				tr = L_add(tr, 0x8000);
 				tr = L_shl(L_shr(tr, 16), 16);
@@ -2175,15 +2237,17 @@ MN Word16 cfft_pk(uint32_t *x, int nn, Word16 mx, Word16 *omx)
 				ti = L_shl(L_shr(ti, 16), 16);
 				uint32_t a = pk(extract_h(L_add(L_deposit_h(pr), tr)),
 						extract_h(L_sub(L_deposit_h(pi), ti)));
-				uint32_t b = pk(extract_h(L_sub(L_deposit_h(pr), tr)),
-						extract_h(L_add(L_deposit_h(pi), ti)));
-				x[ci] = a;
-				x[cj] = b;
-				nmx = pk_amax(b, pk_amax(a, nmx));
+				uint32_t bb = pk(extract_h(L_sub(L_deposit_h(pr), tr)),
+						 extract_h(L_add(L_deposit_h(pi), ti)));
+				x[ci + k] = a;
+				x[ci + half + k] = bb;
+				nmx = pk_amax(bb, pk_amax(a, nmx));
 			}
-			idx += istep_idx;
-			wr = wrt[idx];
-			wi = wit[idx];
+			#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				P[k] = NP[k];
+				Q[k] = NQ[k];
+			}
 		}
 		mx = nmx;
 	}
@@ -2201,8 +2265,12 @@ MN void rfft_pk(uint32_t *x, int n, Word16 mx)
 	const int n2 = n >> 1;		/* complex points of the inner FFT */
 	cfft_pk(x, n2, mx, &mx);
 	Word16 s = mx > 16383 ? 1 : 0;
-	for (int k = 1; k < n2 / 2; k++) {
-		uint32_t A = pk_shr(x[k], s), B = pk_shr(x[n2 - k], s);
+	/* the k-th step reads x[k], x[n2 - k] and writes x[k], x[n2 - k],
+	 * x[n - k], x[n2 + k]: disjoint across k (k < n2 / 2), so four steps
+	 * share one batch of loads */
+	auto split_step = [&](int k, uint32_t A, uint32_t B) {
+		A = pk_shr(A, s);
+		B = pk_shr(B, s);
 		Word16 ar = pk_re(A), ai = pk_im(A), br = pk_re(B), bi = pk_im(B);
 		Word16 r1 = add_shr(ar, br);
 		Word32 a = L_shl(L_sub(ai, bi), 16);
@@ -2215,16 +2283,31 @@ MN void rfft_pk(uint32_t *x, int n, Word16 mx)
 		a = L_negate(a);
 		x[n - k] = pk(ah, bh);
 		x[n2 + k] = pk(extract_h(L_shr(a, 1)), extract_h(L_shr(b, 1)));
+	};
+	int k1 = 1;
+	#pragma unroll 1
+	for (; k1 + 4 <= n2 / 2; k1 += 4) {
+		uint32_t A[4], B[4];
+		#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			A[q] = x[k1 + q];
+			B[q] = x[n2 - k1 - q];
+		}
+		#pragma unroll
+		for (int q = 0; q < 4; q++)
+			split_step(k1 + q, A[q], B[q]);
 	}
+	for (; k1 < n2 / 2; k1++)
+		split_step(k1, x[k1], x[n2 - k1]);
 	x[n2 + n2 / 2] = 0;
 	x[n2 / 2] = pk_shr(x[n2 / 2], s);
 	uint32_t z = pk_shr(x[0], s);
 	x[0] = pk(add(pk_re(z), pk_im(z)), 0);
 	x[n2] = pk(sub(pk_re(z), pk_im(z)), 0);
-	int idx = 1;
-	Word16 wr = wrt[idx], wi = wit[idx];
-	for (int k = 1; k < n2; k++) {
-		uint32_t A = x[k], B = x[n - k];
+	/* step k reads and writes x[k], x[n - k] with twiddle k (the
+	 * reference's running index): disjoint across k < n2, four per batch */
+	auto twid_step = [&](int k, uint32_t A, uint32_t B) {
+		Word16 wr = wrt[k], wi = wit[k];
 		Word16 a1 = pk_re(A), a2 = pk_im(A), b1 = pk_re(B), b2 = pk_im(B);
 		Word32 t = L_deposit_h(a1);
 		t = L_add(t, L_mult(a2, wr));
@@ -2240,10 +2323,22 @@ MN void rfft_pk(uint32_t *x, int n, Word16 mx)
 		u = L_add(u, 0x8000);
 		x[k] = pk(extract_h(t), extract_h(u));
 		x[n - k] = pk(extract_h(t), extract_h(L_negate(u)));
-		idx += 1;
-		wr = wrt[idx];
-		wi = wit[idx];
+	};
+	int k2 = 1;
+	#pragma unroll 1
+	for (; k2 + 4 <= n2; k2 += 4) {
+		uint32_t A[4], B[4];
+		#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			A[q] = x[k2 + q];
+			B[q] = x[n - k2 - q];
+		}
+		#pragma unroll
+		for (int q = 0; q < 4; q++)
+			twid_step(k2 + q, A[q], B[q]);
 	}
+	for (; k2 < n2; k2++)
+		twid_step(k2, x[k2], x[n - k2]);
 }
 
 }  // namespace mlp

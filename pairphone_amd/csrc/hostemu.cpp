@@ -30,7 +30,7 @@ struct emu_engine {
 static NppScratch g_npp_scratch;
 
 #if defined(MELPE_EXACT_STATS)
-extern "C" { long melpe_exact_stats[4] = {0, 0, 0, 0}; }
+extern "C" { long melpe_exact_stats[6] = {0, 0, 0, 0, 0, 0}; }
 #endif
 
 #if defined(MELPE_OPCOUNT)

@@ -349,6 +349,7 @@ template <int DIM>
 MD void lspVQ_t(const int16_t *target, const int16_t *weight, int16_t *qout, const int16_t *cb,
 		int tos, const int16_t *cb_size, int16_t *cb_index, bool flag)
 {
+	PROF_SCOPE(42);
 	const int dim = DIM;
 	int16_t index[LSP_VQ_CAND][LSP_VQ_STAGES], nextIndex[LSP_VQ_CAND][LSP_VQ_STAGES];
 	int16_t cand[LSP_VQ_CAND][2 * LPC_ORD], dMin[LSP_VQ_CAND];
@@ -538,9 +539,12 @@ MN void lsf_vq(EncState *E, MelpParam *par)
 		}
 		E->lsf_started = 1;
 	}
+	{
+	PROF_SCOPE(44);
 	for (int i = 0; i < NF; i++) {
 		lpc_lsp2pred(lsp(i), lpc, LPC_ORD);
 		vq_lspw(wgt[i], lsp(i), lpc, LPC_ORD);
+	}
 	}
 	Word16 uvc = 0;
 	for (int i = 0; i < NF; i++) {
@@ -577,6 +581,73 @@ MN void lsf_vq(EncState *E, MelpParam *par)
 		int cand = 0;
 		int16_t inp = 0;
 		const int16_t *ic = TB(inpCoef);
+		{
+		PROF_SCOPE(43);
+#if !defined(MELPE_OPCOUNT)
+		/* Every error term lsf_werr() is >= 0 when the weights are (they
+		 * are: |A(e^jw)|^-0.3 scaled by 6554 at most), so each candidate's
+		 * saturating L_add chain is min(LW_MAX, exact sum), whatever the
+		 * term order.  That lets the search run j outer, the 16
+		 * interpolation patterns inner: each j's six operands are loaded
+		 * once per candidate instead of once per pattern, the frame-2 term
+		 * (pattern-free) is added once, and the interpolated vectors are
+		 * rebuilt only for the winner.  Candidates and patterns are still
+		 * compared in the reference's order with strict '<'. */
+		bool wpos = true;
+		for (int f = 0; f < NF; f++)
+			for (int j = 0; j < LPC_ORD; j++)
+				wpos &= wgt[f][j] >= 0;
+		EXACT_STAT(wpos ? 5 : 4);
+		if (wpos) {
+			for (int k = 0; k < LSP_INP_CAND; k++) {
+				Word32 e3 = 0;
+				for (int j = 0; j < LPC_ORD; j++) {
+					Word32 acc = L_shl(L_deposit_l(lsp(2)[j]), 15);
+					acc = L_sub(acc, L_shl(L_deposit_l(lcand[k][j]), 15));
+					e3 = L_add(e3, lsf_werr(acc, wgt[2][j]));
+				}
+				/* four patterns at a time: their chains in registers */
+				#pragma unroll 1
+				for (int i0 = 0; i0 < 16; i0 += 4) {
+					Word32 errs[4] = {e3, e3, e3, e3};
+					#pragma unroll 1
+					for (int j = 0; j < LPC_ORD; j++) {
+						const Word16 qp = E->qplsp[j], lc = lcand[k][j];
+						const Word32 l0 = L_shl(L_deposit_l(lsp(0)[j]), 15);
+						const Word32 l1 = L_shl(L_deposit_l(lsp(1)[j]), 15);
+						const Word16 w0 = wgt[0][j], w1 = wgt[1][j];
+						#pragma unroll
+						for (int q = 0; q < 4; q++) {
+							const int i = i0 + q;
+							Word16 f = ic[i * 20 + j];
+							Word32 acc = L_mac(L_mult(f, qp), sub(16384, f), lc);
+							acc = L_sub(acc, l0);
+							f = ic[i * 20 + j + LPC_ORD];
+							Word32 bcc = L_mac(L_mult(f, qp), sub(16384, f), lc);
+							bcc = L_sub(bcc, l1);
+							errs[q] = L_add(errs[q], lsf_werr(acc, w0));
+							errs[q] = L_add(errs[q], lsf_werr(bcc, w1));
+						}
+					}
+					#pragma unroll
+					for (int q = 0; q < 4; q++)
+						if (errs[q] < minErr) {
+							minErr = errs[q];
+							cand = k;
+							inp = (int16_t) (i0 + q);
+						}
+				}
+			}
+			for (int j = 0; j < LPC_ORD; j++) {
+				Word16 f = ic[inp * 20 + j];
+				Word32 acc = L_mac(L_mult(f, E->qplsp[j]), sub(16384, f), lcand[cand][j]);
+				best0[j] = extract_h(L_shl(acc, 1));
+				f = ic[inp * 20 + j + LPC_ORD];
+				acc = L_mac(L_mult(f, E->qplsp[j]), sub(16384, f), lcand[cand][j]);
+				best1[j] = extract_h(L_shl(acc, 1));
+			}
+		} else
+#endif
 		for (int k = 0; k < LSP_INP_CAND; k++)
 			for (int i = 0; i < 16; i++) {
 				Word32 err = 0;
@@ -605,6 +676,7 @@ MN void lsf_vq(EncState *E, MelpParam *par)
 					v_copy(best1, il1, LPC_ORD);
 				}
 			}
+		}
 		v_copy(lsp(2), lcand[cand], LPC_ORD);
 		v_copy(q->lsf_index[0], &lidx[cand * tos], tos);
 		q->lsf_index[1][0] = inp;
