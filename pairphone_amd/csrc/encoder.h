@@ -19,6 +19,11 @@ namespace mlp {
  * 441, 460): LPC autocorrelation to order 10, LSFs of the unexpanded LPC
  * (kept as top_lpc), no pitch tracking / classification, the 2400 gain
  * window, and no voicing decision here (q_bpvc makes it) */
+/* Timing knockouts (diagnostics only, never in a product build): compiled
+ * with -DMELPE_KO_<stage>, the stage is skipped, so an A/B of kernel times
+ * prices it in the product code itself, free of profiler perturbation.
+ * The output of such a build is wrong by construction. */
+
 template <bool R24>
 MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 {
@@ -43,7 +48,12 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 	E->fpitch[1] = find_pitch(&sb[LPF_ORD + PITCH_FR / 2], &dontcare, 2 * PITCHMIN,
 				  PITCHMAX, PITCHMAX, ex);
 	E->fpitch[1] = shl(E->fpitch[1], 7);
+#if !defined(MELPE_KO_BPVC)
 	bpvc_ana(E, &speech[FRAME_END], E->fpitch, par->bpvc, &sub_pitch);
+#else
+	sub_pitch = E->fpitch[0];
+	v_set(par->bpvc, 0, NUM_BANDS);
+#endif
 	par->jitter = (par->bpvc[0] < VJIT_Q14) ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;
 	lpc_acor(&speech[FRAME_END - LPC_FRAME / 2], TB(win_cof), ac, 4, R24 ? LPC_ORD : 16,
 		 LPC_FRAME);
@@ -68,14 +78,23 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 	if (!R24) {
 		int ct = CUR_TRACK + subnum * PIT_SUBNUM;
 		for (int i = 0; i < PIT_SUBNUM; i++) {
+#if !defined(MELPE_KO_PAUTO)
 			pitchAuto(E, &speech[FRAME_END + i * PIT_SUBFRAME + PIT_COR_LEN / 2],
 				  &E->pitTrack[ct + i + 1], &E->classStat[ct + i + 1]);
+#endif
+#if !defined(MELPE_KO_CLASSIFY)
 			classify(E, &speech[FRAME_END + i * PIT_SUBFRAME + PIT_SUBFRAME / 2],
 				 &E->classStat[ct + i + 1], ac);
+#endif
 		}
 	}
+#if !defined(MELPE_KO_PITCHANA)
 	par->pitch = pitch_ana(E, &speech[FRAME_END], &sb[LPF_ORD + PITCHMAX], sub_pitch,
 			       E->pitch_avg, &pcorr);
+#else
+	par->pitch = sub_pitch;
+	pcorr = 0;
+#endif
 	for (int i = 0; i < NUM_GAINFR; i++) {
 		if (par->bpvc[0] > BPTHRESH_Q14)
 			par->gain[i] = gain_ana(&speech[FRAME_BEG + (i + 1) * 90], sub_pitch, 120, 320);
@@ -359,7 +378,9 @@ MN void analysis_tail(EncState *E)
 	int16_t lpc[LPC_ORD + 1];
 	sc_ana(E, par);
 	lpc[0] = 4096;
+#if !defined(MELPE_KO_LSFVQ)
 	lsf_vq(E, par);
+#endif
 	pitch_vq(E, par);
 	gain_vq(E, par);
 	for (int i = 0; i < NF; i++)
@@ -374,7 +395,9 @@ MN void analysis_tail(EncState *E)
 			zerflt(&E->hpspeech[i * FRAME + FRAME_END - LPC_FRAME / 2], lpc, E->sigbuf,
 			       LPC_ORD, LPC_FRAME);
 			window(E->sigbuf, TB(win_cof), E->sigbuf, LPC_FRAME);
+#if !defined(MELPE_KO_HARM)
 			find_harm(E->sigbuf, par[i].fs_mag, par[i].pitch, NUM_HARM, LPC_FRAME);
+#endif
 		}
 	}
 	quant_fsmag(E, par);
@@ -387,6 +410,9 @@ MN void analysis_tail(EncState *E)
 MN void analysis(EncState *E, const int16_t *sp_in)
 {
 	PROF_SCOPE(15);
+#if defined(MELPE_KO_ANALYSIS)
+	return;
+#endif
 	for (int i = 0; i < NF; i++)
 		analysis_frame(E, sp_in, i);
 	analysis_tail(E);
