@@ -64,9 +64,11 @@ int kl_npp(EncState *enc, int16_t *sp, int frames, int stride, const uint8_t *ac
 	   int rate1200, hipStream_t s);
 int kl_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active, int n, hipStream_t s);
 int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
+	       const int *perm, const int *nlive,
 	       hipStream_t s);
 int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto, hipStream_t s);
 int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
+	      const int *perm, const int *nlive,
 	      hipStream_t s);
 int kl_enc24(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
 	     hipStream_t s);
@@ -375,6 +377,131 @@ static int stage_get(int dev, size_t bytes, void **out)
 	return 0;
 }
 
+/*
+ * Lane order by pitch class (MELPE_BIN, default on).
+ *
+ * k_enc_ana and k_decode run one channel per lane, and their loops follow
+ * each channel's own pitch period and voicing: a synthesis period costs
+ * O(L^2) in realIDFT and a frame holds 180/L of them, the analysis windows
+ * and harmonic counts follow the pitch, and unvoiced frames take other
+ * branches.  A wave pays the slowest of its 64 channels in every such loop.
+ * So before each launch the live channels are counting-sorted into 64
+ * classes -- voiced frames of the channel's last superframe (0..3) x its last
+ * pitch in 5-sample steps -- and lane g of the kernel runs channel perm[g];
+ * lanes at or past the live count exit at once, so a ragged mask also packs
+ * the live channels into the fewest waves.  Each channel's arithmetic is
+ * untouched (the order only decides which channels share a wave), so the
+ * output is the same bit for bit; the order within a class follows the
+ * atomics and is not reproducible, which nothing depends on.
+ */
+#define NBIN 64
+struct BinBuf {
+	int *perm = nullptr;	/* [C] lane -> channel */
+	uint8_t *key = nullptr;	/* [C] class of each channel (0xff: not live) */
+	unsigned *ctl = nullptr;	/* [0,64) counts, [64,128) next slot, [128] live count */
+};
+
+static hipError_t bin_alloc(BinBuf *b, int channels)
+{
+	size_t pb = sizeof(int) * (size_t) channels, cb = sizeof(unsigned) * (2 * NBIN + 1);
+	char *p = nullptr;
+	hipError_t er = hipMalloc(&p, pb + cb + (size_t) channels);
+	if (er != hipSuccess)
+		return er;
+	b->perm = (int *) p;
+	b->ctl = (unsigned *) (p + pb);
+	b->key = (uint8_t *) (p + pb + cb);
+	return hipSuccess;
+}
+
+/* the class of one record: voiced frames of the last superframe
+ * (quant_par uv_flag, 0 = voiced) and the last frame's pitch (Q7) */
+__device__ __forceinline__ int bin_class(const char *rec, int off_pitch, int off_uv)
+{
+	const int16_t *uv = (const int16_t *) (rec + off_uv);
+	int nv = (uv[0] == 0) + (uv[1] == 0) + (uv[2] == 0);
+	int b = ((*(const int16_t *) (rec + off_pitch) >> 7) - 20) / 5;
+	b = b < 0 ? 0 : (b > 15 ? 15 : b);
+	return nv * 16 + b;
+}
+
+__global__ __launch_bounds__(256) void k_bin_count(const char *rec, size_t stride, int off_pitch,
+						   int off_uv, const uint8_t *active, int n, BinBuf b)
+{
+	__shared__ unsigned cnt[NBIN];
+	if (threadIdx.x < NBIN)
+		cnt[threadIdx.x] = 0;
+	__syncthreads();
+	int c = blockIdx.x * blockDim.x + threadIdx.x;
+	if (c < n) {
+		int k = 0xff;
+		if (!active || active[c]) {
+			k = bin_class(rec + (size_t) c * stride, off_pitch, off_uv);
+			atomicAdd(&cnt[k], 1u);
+		}
+		b.key[c] = (uint8_t) k;
+	}
+	__syncthreads();
+	if (threadIdx.x < NBIN && cnt[threadIdx.x])
+		atomicAdd(&b.ctl[threadIdx.x], cnt[threadIdx.x]);
+}
+
+__global__ void k_bin_scan(BinBuf b)
+{
+	if (threadIdx.x == 0) {
+		unsigned acc = 0;
+		for (int k = 0; k < NBIN; k++) {
+			b.ctl[NBIN + k] = acc;
+			acc += b.ctl[k];
+		}
+		b.ctl[2 * NBIN] = acc;
+	}
+}
+
+__global__ __launch_bounds__(256) void k_bin_scatter(int n, BinBuf b)
+{
+	__shared__ unsigned cnt[NBIN], base[NBIN];
+	if (threadIdx.x < NBIN)
+		cnt[threadIdx.x] = 0;
+	__syncthreads();
+	int c = blockIdx.x * blockDim.x + threadIdx.x;
+	int k = c < n ? b.key[c] : 0xff;
+	unsigned r = 0;
+	if (k != 0xff)
+		r = atomicAdd(&cnt[k], 1u);
+	__syncthreads();
+	if (threadIdx.x < NBIN && cnt[threadIdx.x])
+		base[threadIdx.x] = atomicAdd(&b.ctl[NBIN + threadIdx.x], cnt[threadIdx.x]);
+	__syncthreads();
+	if (k != 0xff)
+		b.perm[base[k] + r] = c;
+}
+
+static bool bin_enabled(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *s = getenv("MELPE_BIN");
+		v = !(s && s[0] == '0');
+	}
+	return v != 0;
+}
+
+/* sorts the live channels of `rec` (records of `stride` bytes) into b.perm on
+ * stream s; false when the order is off (identity lanes + mask) */
+static bool bin_launch(BinBuf &b, const void *rec, size_t stride, int off_pitch, int off_uv,
+		       const uint8_t *active, int n, hipStream_t s)
+{
+	if (!bin_enabled())
+		return false;
+	unsigned g = (unsigned) ((n + 255) / 256);
+	hipMemsetAsync(b.ctl, 0, sizeof(unsigned) * NBIN, s);
+	k_bin_count<<<g, 256, 0, s>>>((const char *) rec, stride, off_pitch, off_uv, active, n, b);
+	k_bin_scan<<<1, WAVE, 0, s>>>(b);
+	k_bin_scatter<<<g, 256, 0, s>>>(n, b);
+	return true;
+}
+
 struct melpe_engine {
 	int device = 0;
 	int channels = 0;
@@ -387,9 +514,34 @@ struct melpe_engine {
 	unsigned char *d_bits = nullptr;
 	uint8_t *d_mask = nullptr;
 	int16_t *d_npp = nullptr;	/* staging of melpe_npp_host, grown on demand */
+	BinBuf bin_enc, bin_dec;	/* pitch-class lane order of k_enc_ana / k_decode */
 	size_t npp_bytes = 0;
 	float last_ms = 0.f;
 };
+
+static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, const uint8_t *d_act,
+		      hipStream_t s)
+{
+	BinBuf &b = e->bin_enc;
+	bool on = bin_launch(b, e->d_enc, sizeof(EncState),
+			     (int) (offsetof(EncState, par) + (NF - 1) * sizeof(MelpParam)),
+			     (int) (offsetof(EncState, qpar) + offsetof(QuantParam, uv_flag)), d_act,
+			     e->channels, s);
+	return kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, on ? b.perm : nullptr,
+			  on ? (const int *) (b.ctl + 2 * NBIN) : nullptr, s);
+}
+
+static int dec_launch(melpe_engine *e, int16_t *d_sp, const uint8_t *d_bits, const uint8_t *d_act,
+		      hipStream_t s)
+{
+	BinBuf &b = e->bin_dec;
+	bool on = bin_launch(b, e->d_dec, sizeof(DecState),
+			     (int) (offsetof(DecState, par) + (NF - 1) * sizeof(MelpParam)),
+			     (int) (offsetof(DecState, qpar) + offsetof(QuantParam, uv_flag)), d_act,
+			     e->channels, s);
+	return kl_decode(e->d_dec, d_sp, d_bits, d_act, e->channels, on ? b.perm : nullptr,
+			 on ? (const int *) (b.ctl + 2 * NBIN) : nullptr, s);
+}
 
 static std::mutex g_dev_mu;
 static bool g_dev_ready[64];
@@ -465,6 +617,8 @@ int melpe_engine_create(melpe_engine **out, int device, int channels)
 	CREATE_STEP(hipMalloc(&e->d_pcm, sizeof(int16_t) * MELPE_SF_SAMPLES * (size_t) channels));
 	CREATE_STEP(hipMalloc(&e->d_bits, (size_t) MELPE_SF_BYTES * channels));
 	CREATE_STEP(hipMalloc(&e->d_mask, (size_t) channels));
+	CREATE_STEP(bin_alloc(&e->bin_enc, channels));
+	CREATE_STEP(bin_alloc(&e->bin_dec, channels));
 #undef CREATE_STEP
 	if (er != hipSuccess) {
 		int r = fail(what, er);
@@ -496,6 +650,8 @@ int melpe_engine_destroy(melpe_engine *e)
 	hipFree(e->d_pcm);
 	hipFree(e->d_bits);
 	hipFree(e->d_mask);
+	hipFree(e->bin_enc.perm);
+	hipFree(e->bin_dec.perm);
 	if (e->ev0)
 		hipEventDestroy(e->ev0);
 	if (e->ev1)
@@ -611,7 +767,7 @@ static int encode_launch(melpe_engine *e, unsigned char *d_bits, int16_t *d_sp,
 	DEVGUARD(e->device);
 	ev_begin(e, s);
 	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, d_sp, d_act, e->channels, s));
-	HIPCHK((hipError_t) kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, s));
+	HIPCHK((hipError_t) ana_launch(e, d_sp, d_bits, d_act, s));
 	ev_end(e, s, sync);
 	return 0;
 }
@@ -641,9 +797,8 @@ int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const 
 	if (!e || !d_bits || !d_sp)
 		return fail_msg("melpe_encode_ana_dev: null argument");
 	DEVGUARD(e->device);
-	HIPCHK((hipError_t) kl_enc_ana(e->d_enc, (const int16_t *) d_sp, (uint8_t *) d_bits,
-				       (const uint8_t *) d_active, e->channels,
-				       (hipStream_t) hip_stream));
+	HIPCHK((hipError_t) ana_launch(e, (const int16_t *) d_sp, (uint8_t *) d_bits,
+				       (const uint8_t *) d_active, (hipStream_t) hip_stream));
 	return 0;
 }
 
@@ -676,7 +831,7 @@ static int decode_launch(melpe_engine *e, int16_t *d_sp, const unsigned char *d_
 {
 	DEVGUARD(e->device);
 	ev_begin(e, s);
-	HIPCHK((hipError_t) kl_decode(e->d_dec, d_sp, d_bits, d_act, e->channels, s));
+	HIPCHK((hipError_t) dec_launch(e, d_sp, d_bits, d_act, s));
 	ev_end(e, s, sync);
 	return 0;
 }

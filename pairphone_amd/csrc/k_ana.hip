@@ -16,11 +16,19 @@ struct AnaLane {
 };
 
 __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits,
-						  const uint8_t *active, int n)
+						  const uint8_t *active, int n, const int *perm,
+						  const int *nlive)
 {
+	/* lane g runs channel perm[g] when the engine ordered the live channels
+	 * by pitch class (engine.hip, MELPE_BIN), else channel g under the mask */
 	int c = blockIdx.x * WAVE + threadIdx.x;
-	if (c >= n || (active && !active[c]))
+	if (perm) {
+		if (c >= *nlive)
+			return;
+		c = perm[c];
+	} else if (c >= n || (active && !active[c])) {
 		return;
+	}
 	AnaLane L;
 	PIN_FRAME(L);
 	lane_copy((char *) &L.S + ENC_ANA_OFF, (const char *) &enc[c] + ENC_ANA_OFF, ENC_ANA_BYTES);
@@ -58,9 +66,9 @@ static unsigned ana_lds_bytes(void)
 }
 
 extern "C" int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
-			  int n, hipStream_t s)
+			  int n, const int *perm, const int *nlive, hipStream_t s)
 {
-	k_enc_ana<<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n);
+	k_enc_ana<<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive);
 	return (int) hipGetLastError();
 }
 

@@ -18,15 +18,23 @@ struct DecLane {
 };
 
 __global__ __launch_bounds__(DEC_BLOCK, MELPE_DEC_WAVES) void k_decode(DecState *dec, int16_t *sp,
-						      const uint8_t *bits, const uint8_t *active, int n)
+						      const uint8_t *bits, const uint8_t *active, int n,
+						      const int *perm, const int *nlive)
 {
 	for (int len = 1; len <= PITCHMAX; len++)
 		for (int i = threadIdx.x; i < len; i += blockDim.x)
 			s_idft_cos[((len - 1) * len) / 2 + i] = g_der.idft_cos[len][i];
 	__syncthreads();
+	/* lane g decodes channel perm[g] when the engine ordered the live
+	 * channels by pitch class (engine.hip, MELPE_BIN) */
 	int c = blockIdx.x * blockDim.x + threadIdx.x;
-	if (c >= n || (active && !active[c]))
+	if (perm) {
+		if (c >= *nlive)
+			return;
+		c = perm[c];
+	} else if (c >= n || (active && !active[c])) {
 		return;
+	}
 	DecLane L;
 	PIN_FRAME(L);
 	lane_copy(&L.S, &dec[c], sizeof(DecState));
@@ -38,11 +46,11 @@ __global__ __launch_bounds__(DEC_BLOCK, MELPE_DEC_WAVES) void k_decode(DecState 
 }
 
 extern "C" int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active,
-			 int n, hipStream_t s)
+			 int n, const int *perm, const int *nlive, hipStream_t s)
 {
 	int b = DEC_BLOCK;
 	while (b > WAVE && (n + b - 1) / b < 1024)
 		b /= 2;
-	k_decode<<<(n + b - 1) / b, b, IDFT_LDS_WORDS * sizeof(int16_t), s>>>(dec, sp, bits, active, n);
+	k_decode<<<(n + b - 1) / b, b, IDFT_LDS_WORDS * sizeof(int16_t), s>>>(dec, sp, bits, active, n, perm, nlive);
 	return (int) hipGetLastError();
 }
