@@ -63,9 +63,11 @@ TUS = ("engine", "k_npp", "k_ana", "k_dec", "k_r24")
 HOT_TUS = ("k_npp", "k_ana", "k_dec", "k_r24")
 
 
-def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=HOT_TUS):
+def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=HOT_TUS, only=None):
     """hipcc build of the product library (prof=True: the stage-timer
-    diagnostics variant libmelpe_amd_prof.so, -DMELPE_PROF)"""
+    diagnostics variant libmelpe_amd_prof.so, -DMELPE_PROF); only=(tu, ...)
+    recompiles just those TUs and relinks with the other TUs' objects from
+    the previous build (a development shortcut; the default rebuilds all)"""
     out = out or (PROF_LIB if prof else LIB)
     deps = _sources()
     if not force and not _newer(out, deps):
@@ -82,6 +84,8 @@ def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=
     for tu in TUS:
         o = os.path.join(objdir, tu + ".o")
         objs.append(o)
+        if only is not None and tu not in only and os.path.exists(o):
+            continue
         extra = ["-DMELPE_INLINE_ALL"] if tu in hot else []
         if tus_defs and tu in tus_defs:
             extra += ["-D" + d for d in tus_defs[tu]]

@@ -385,16 +385,16 @@ static int stage_get(int dev, size_t bytes, void **out)
  * O(L^2) in realIDFT and a frame holds 180/L of them, the analysis windows
  * and harmonic counts follow the pitch, and unvoiced frames take other
  * branches.  A wave pays the slowest of its 64 channels in every such loop.
- * So before each launch the live channels are counting-sorted into 64
+ * So before each launch the live channels are counting-sorted into 128
  * classes -- voiced frames of the channel's last superframe (0..3) x its last
- * pitch in 5-sample steps -- and lane g of the kernel runs channel perm[g];
+ * pitch in 3-sample steps -- and lane g of the kernel runs channel perm[g];
  * lanes at or past the live count exit at once, so a ragged mask also packs
  * the live channels into the fewest waves.  Each channel's arithmetic is
  * untouched (the order only decides which channels share a wave), so the
  * output is the same bit for bit; the order within a class follows the
  * atomics and is not reproducible, which nothing depends on.
  */
-#define NBIN 64
+#define NBIN 128
 struct BinBuf {
 	int *perm = nullptr;	/* [C] lane -> channel */
 	uint8_t *key = nullptr;	/* [C] class of each channel (0xff: not live) */
@@ -414,36 +414,56 @@ static hipError_t bin_alloc(BinBuf *b, int channels)
 	return hipSuccess;
 }
 
-/* the class of one record: voiced frames of the last superframe
- * (quant_par uv_flag, 0 = voiced) and the last frame's pitch (Q7) */
-__device__ __forceinline__ int bin_class(const char *rec, int off_pitch, int off_uv)
+/* the class of one record, from its last superframe: the voiced frames
+ * (quant_par uv_flag, 0 = voiced) and the pitch (Q7) of its frames.
+ * Default: voiced count x last pitch in 3-sample steps (128 classes).
+ * MELPE_BIN_KEY (diagnostics) 1 = mean pitch in 2-sample steps, 2 = voiced
+ * count x last pitch in 5-sample steps; on MI355X at 262,144 channels the
+ * default was best for both kernels (k_enc_ana 39.8 / 41.5 / 39.9 ms,
+ * k_decode 19.0 / 19.2 / 19.2 ms, profiles/r02_binkey_{vp3,mean2,vp5}_*). */
+__device__ __forceinline__ int bin_class(const char *rec, int off_par, int off_uv, int mode)
 {
 	const int16_t *uv = (const int16_t *) (rec + off_uv);
 	int nv = (uv[0] == 0) + (uv[1] == 0) + (uv[2] == 0);
-	int b = ((*(const int16_t *) (rec + off_pitch) >> 7) - 20) / 5;
-	b = b < 0 ? 0 : (b > 15 ? 15 : b);
-	return nv * 16 + b;
+	int p[NF];
+	for (int k = 0; k < NF; k++)
+		p[k] = *(const int16_t *) (rec + off_par + k * sizeof(MelpParam)) >> 7;
+	int b;
+	if (mode == 1) {
+		b = ((p[0] + p[1] + p[2]) / 3 - 20) / 2;
+		return b < 0 ? 0 : (b > NBIN - 1 ? NBIN - 1 : b);
+	}
+	if (mode == 2) {
+		b = (p[NF - 1] - 20) / 5;
+		b = b < 0 ? 0 : (b > 15 ? 15 : b);
+		return nv * 16 + b;
+	}
+	b = (p[NF - 1] - 20) / 3;
+	b = b < 0 ? 0 : (b > 31 ? 31 : b);
+	return nv * 32 + b;
 }
 
-__global__ __launch_bounds__(256) void k_bin_count(const char *rec, size_t stride, int off_pitch,
-						   int off_uv, const uint8_t *active, int n, BinBuf b)
+__global__ __launch_bounds__(256) void k_bin_count(const char *rec, size_t stride, int off_par,
+						   int off_uv, const uint8_t *active, int n, BinBuf b,
+						   int mode)
 {
 	__shared__ unsigned cnt[NBIN];
-	if (threadIdx.x < NBIN)
-		cnt[threadIdx.x] = 0;
+	for (int k = threadIdx.x; k < NBIN; k += blockDim.x)
+		cnt[k] = 0;
 	__syncthreads();
 	int c = blockIdx.x * blockDim.x + threadIdx.x;
 	if (c < n) {
 		int k = 0xff;
 		if (!active || active[c]) {
-			k = bin_class(rec + (size_t) c * stride, off_pitch, off_uv);
+			k = bin_class(rec + (size_t) c * stride, off_par, off_uv, mode);
 			atomicAdd(&cnt[k], 1u);
 		}
 		b.key[c] = (uint8_t) k;
 	}
 	__syncthreads();
-	if (threadIdx.x < NBIN && cnt[threadIdx.x])
-		atomicAdd(&b.ctl[threadIdx.x], cnt[threadIdx.x]);
+	for (int k = threadIdx.x; k < NBIN; k += blockDim.x)
+		if (cnt[k])
+			atomicAdd(&b.ctl[k], cnt[k]);
 }
 
 __global__ void k_bin_scan(BinBuf b)
@@ -461,8 +481,8 @@ __global__ void k_bin_scan(BinBuf b)
 __global__ __launch_bounds__(256) void k_bin_scatter(int n, BinBuf b)
 {
 	__shared__ unsigned cnt[NBIN], base[NBIN];
-	if (threadIdx.x < NBIN)
-		cnt[threadIdx.x] = 0;
+	for (int k = threadIdx.x; k < NBIN; k += blockDim.x)
+		cnt[k] = 0;
 	__syncthreads();
 	int c = blockIdx.x * blockDim.x + threadIdx.x;
 	int k = c < n ? b.key[c] : 0xff;
@@ -470,8 +490,9 @@ __global__ __launch_bounds__(256) void k_bin_scatter(int n, BinBuf b)
 	if (k != 0xff)
 		r = atomicAdd(&cnt[k], 1u);
 	__syncthreads();
-	if (threadIdx.x < NBIN && cnt[threadIdx.x])
-		base[threadIdx.x] = atomicAdd(&b.ctl[NBIN + threadIdx.x], cnt[threadIdx.x]);
+	for (int j = threadIdx.x; j < NBIN; j += blockDim.x)
+		if (cnt[j])
+			base[j] = atomicAdd(&b.ctl[NBIN + j], cnt[j]);
 	__syncthreads();
 	if (k != 0xff)
 		b.perm[base[k] + r] = c;
@@ -489,14 +510,25 @@ static bool bin_enabled(void)
 
 /* sorts the live channels of `rec` (records of `stride` bytes) into b.perm on
  * stream s; false when the order is off (identity lanes + mask) */
-static bool bin_launch(BinBuf &b, const void *rec, size_t stride, int off_pitch, int off_uv,
+static int bin_key_mode(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *s = getenv("MELPE_BIN_KEY");
+		v = s ? atoi(s) : 0;
+	}
+	return v;
+}
+
+static bool bin_launch(BinBuf &b, const void *rec, size_t stride, int off_par, int off_uv,
 		       const uint8_t *active, int n, hipStream_t s)
 {
 	if (!bin_enabled())
 		return false;
 	unsigned g = (unsigned) ((n + 255) / 256);
 	hipMemsetAsync(b.ctl, 0, sizeof(unsigned) * NBIN, s);
-	k_bin_count<<<g, 256, 0, s>>>((const char *) rec, stride, off_pitch, off_uv, active, n, b);
+	k_bin_count<<<g, 256, 0, s>>>((const char *) rec, stride, off_par, off_uv, active, n, b,
+				      bin_key_mode());
 	k_bin_scan<<<1, WAVE, 0, s>>>(b);
 	k_bin_scatter<<<g, 256, 0, s>>>(n, b);
 	return true;
@@ -524,7 +556,7 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 {
 	BinBuf &b = e->bin_enc;
 	bool on = bin_launch(b, e->d_enc, sizeof(EncState),
-			     (int) (offsetof(EncState, par) + (NF - 1) * sizeof(MelpParam)),
+			     (int) offsetof(EncState, par),
 			     (int) (offsetof(EncState, qpar) + offsetof(QuantParam, uv_flag)), d_act,
 			     e->channels, s);
 	return kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, on ? b.perm : nullptr,
@@ -536,7 +568,7 @@ static int dec_launch(melpe_engine *e, int16_t *d_sp, const uint8_t *d_bits, con
 {
 	BinBuf &b = e->bin_dec;
 	bool on = bin_launch(b, e->d_dec, sizeof(DecState),
-			     (int) (offsetof(DecState, par) + (NF - 1) * sizeof(MelpParam)),
+			     (int) offsetof(DecState, par),
 			     (int) (offsetof(DecState, qpar) + offsetof(QuantParam, uv_flag)), d_act,
 			     e->channels, s);
 	return kl_decode(e->d_dec, d_sp, d_bits, d_act, e->channels, on ? b.perm : nullptr,
