@@ -61,6 +61,14 @@ int melpe_engine_reset(melpe_engine *e, const uint8_t *mask_host, int which);
 /* the same, enqueued on `hip_stream` (d_mask: device C-byte mask or NULL) */
 int melpe_engine_reset_dev(melpe_engine *e, const void *d_mask, int which, void *hip_stream);
 
+/* Lane order of the lane-per-channel kernels (analysis, synthesis): on (1,
+ * the default unless MELPE_BIN=0 is set in the environment), the live
+ * channels are sorted by pitch class before each launch so that channels
+ * with similar pitch and voicing share a wave; off (0), lane g runs channel g.
+ * Either way every channel's bits and PCM are the same; only the speed
+ * differs. */
+int melpe_engine_set_lane_order(melpe_engine *e, int on);
+
 /* Per-channel state records, for checkpoint / resume and for moving channels
  * between engines or GPUs (e.g. re-balancing ragged streams).  which: 1 =
  * encoder (EncState), 2 = decoder (DecState).  melpe_engine_state_bytes gives

@@ -38,6 +38,7 @@ def load_library(path=None):
         "melpe_engine_channels": (i32, [vp]),
         "melpe_engine_reset": (i32, [vp, vp, i32]),
         "melpe_engine_reset_dev": (i32, [vp, vp, i32, vp]),
+        "melpe_engine_set_lane_order": (i32, [vp, i32]),
         "melpe_engine_state_bytes": (ctypes.c_long, [i32]),
         "melpe_engine_export": (i32, [vp, i32, i32, i32, vp]),
         "melpe_engine_import": (i32, [vp, i32, i32, i32, vp]),
@@ -212,6 +213,11 @@ class MelpeEngine:
     def reset(self, mask=None, which=3):
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
         _check(self.lib.melpe_engine_reset(self.h, _ptr(m), which))
+
+    def set_lane_order(self, on):
+        """pitch-class lane order of the analysis / synthesis kernels on or
+        off (results are the same either way)"""
+        _check(self.lib.melpe_engine_set_lane_order(self.h, 1 if on else 0))
 
     def reset_dev(self, d_mask=None, which=3, stream=None):
         """reset enqueued on `stream` (ordered with the *_dev calls on it)"""

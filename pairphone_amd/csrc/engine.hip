@@ -520,10 +520,10 @@ static int bin_key_mode(void)
 	return v;
 }
 
-static bool bin_launch(BinBuf &b, const void *rec, size_t stride, int off_par, int off_uv,
-		       const uint8_t *active, int n, hipStream_t s)
+static bool bin_launch(int order, BinBuf &b, const void *rec, size_t stride, int off_par,
+		       int off_uv, const uint8_t *active, int n, hipStream_t s)
 {
-	if (!bin_enabled())
+	if (order == 0 || (order < 0 && !bin_enabled()))
 		return false;
 	unsigned g = (unsigned) ((n + 255) / 256);
 	hipMemsetAsync(b.ctl, 0, sizeof(unsigned) * NBIN, s);
@@ -547,6 +547,7 @@ struct melpe_engine {
 	uint8_t *d_mask = nullptr;
 	int16_t *d_npp = nullptr;	/* staging of melpe_npp_host, grown on demand */
 	BinBuf bin_enc, bin_dec;	/* pitch-class lane order of k_enc_ana / k_decode */
+	int lane_order = -1;	/* 1 on, 0 off, -1 the MELPE_BIN default */
 	size_t npp_bytes = 0;
 	float last_ms = 0.f;
 };
@@ -555,7 +556,7 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 		      hipStream_t s)
 {
 	BinBuf &b = e->bin_enc;
-	bool on = bin_launch(b, e->d_enc, sizeof(EncState),
+	bool on = bin_launch(e->lane_order, b, e->d_enc, sizeof(EncState),
 			     (int) offsetof(EncState, par),
 			     (int) (offsetof(EncState, qpar) + offsetof(QuantParam, uv_flag)), d_act,
 			     e->channels, s);
@@ -567,7 +568,7 @@ static int dec_launch(melpe_engine *e, int16_t *d_sp, const uint8_t *d_bits, con
 		      hipStream_t s)
 {
 	BinBuf &b = e->bin_dec;
-	bool on = bin_launch(b, e->d_dec, sizeof(DecState),
+	bool on = bin_launch(e->lane_order, b, e->d_dec, sizeof(DecState),
 			     (int) offsetof(DecState, par),
 			     (int) (offsetof(DecState, qpar) + offsetof(QuantParam, uv_flag)), d_act,
 			     e->channels, s);
@@ -665,6 +666,14 @@ int melpe_engine_create(melpe_engine **out, int device, int channels)
 		return r;
 	}
 	*out = e;
+	return 0;
+}
+
+int melpe_engine_set_lane_order(melpe_engine *e, int on)
+{
+	if (!e)
+		return fail_msg("melpe_engine_set_lane_order: null engine");
+	e->lane_order = on ? 1 : 0;
 	return 0;
 }
 
