@@ -395,6 +395,7 @@ static int stage_get(int dev, size_t bytes, void **out)
  * atomics and is not reproducible, which nothing depends on.
  */
 #define NBIN 128
+static_assert(NBIN < 0xff, "class ids and the not-live mark 0xff must fit the uint8 keys");
 struct BinBuf {
 	int *perm = nullptr;	/* [C] lane -> channel */
 	uint8_t *key = nullptr;	/* [C] class of each channel (0xff: not live) */
