@@ -1662,6 +1662,32 @@ MD void fc_corr10(const int16_t *in, int hp, int win, Word40 *A)
 		A[n] = 2 * acc[n];
 }
 
+/* The same ten sums without a branch on the parity of hp.  Lanes of a wave
+ * carry different pitches, so fc_corr10<0> and fc_corr10<1> would both run,
+ * each on part of the wave.  Odd hp's lag n has the window of even hp+1's
+ * lag n+1 (lo = n/2 + 1 = (n + 2)/2), so one pass of the even pattern over
+ * eleven lags of hpe = hp + (hp & 1) holds both: lag n is sum n + (hp & 1).
+ * The b-stream starts at in[hpe - 6], even for every lane, so the pair
+ * streams of all lanes also share their alignment. */
+struct FcLags11 {
+	static constexpr int NA = 6, NB = 6;
+	static constexpr int lon(int n) { return (n + 1) / 2; }
+	static constexpr int oa(int n) { return lon(n); }
+	static constexpr int ob(int n) { return lon(n) - n + 5; }
+};
+
+MD void fc_corr_any(const int16_t *in, int hp, int win, Word40 *A)
+{
+	const int odd = hp & 1;
+	int32_t hl[22];
+	xcorr_pairs<11, FcLags11, true>(in, &in[hp + odd - 6], win, hl);
+	#pragma unroll
+	for (int n = 0; n < 10; n++) {
+		int32_t h = odd ? hl[n + 1] : hl[n], l = odd ? hl[12 + n] : hl[11 + n];
+		A[n] = 2 * (256 * (int64_t) h + l);
+	}
+}
+
 /* frac_cor :504 -- best normalised correlation within +-5 of pitch */
 MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 {
@@ -1702,6 +1728,41 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 	int lo = 0, hi = hp;
 	const bool blocked = (hp - lp) == 10;
 	Word40 blk[10];
+#if !defined(MELPE_OPCOUNT)
+	if (blocked)
+		fc_corr_any(in, hp, win, blk);
+	/* The r0 / rk updates alternate with the parity of the lag, which
+	 * differs between lanes: one update of the selected side per lag,
+	 * branch-free (the reference's L40_msu / L40_mac pairs, in order). */
+	for (Word16 i = sub(hp, 1); i >= lp; i--) {
+		const bool ev = (i & 1) == 0;	/* i >= MINPITCH > 0 */
+		hi -= !ev;
+		const int ia = ev ? lo : hi;
+		const int16_t x1 = in[ia], x2 = in[ia + win];
+		const Word40 p1 = (Word40) x1 * x1 * 2, p2 = (Word40) x2 * x2 * 2;
+		Word40 v = L40_shr((Word40) (ev ? Lr0 : Lrk), ev ? r0s : rks);
+		v = clamp40(ev ? v - p1 : v + p1);
+		v = clamp40(ev ? v + p2 : v - p2);
+		Word16 vs;
+		Word32 vL;
+		norm40(&v, &vs, &vL);
+		Lr0 = ev ? vL : Lr0;
+		r0s = ev ? vs : r0s;
+		Lrk = ev ? Lrk : vL;
+		rks = ev ? rks : vs;
+		lo += ev;
+		if (blocked) {
+			A = blk[hp - 1 - i];
+		} else {
+			A = 0;
+			for (int j = lo; j < lo + win; j++)
+				A = L40_mac(A, in[j], in[j + i]);
+		}
+		Word16 g = cor_gain(&Lr0, &r0s, rks, Lrk, A, false);
+		if (g > maxgp)
+			maxgp = g;
+	}
+#else
 	if (blocked) {
 		if (hp & 1)
 			fc_corr10<1>(in, hp, win, blk);
@@ -1734,6 +1795,7 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 		if (g > maxgp)
 			maxgp = g;
 	}
+#endif
 	return maxgp;
 }
 

@@ -1212,14 +1212,20 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 		v_copy(D->disp_del, &sb[len + BEGIN - DISP_ORD], DISP_ORD);
 		zerflt_Q(&sb[BEGIN], TB(disp_cof), &sb[BEGIN], DISP_ORD, len, 15);
 		if (add(sb0, len) >= FRAME) {
+			/* the reference postfilters the frame here (melp_syn.c:
+			 * 448); that is always the loop's last period and
+			 * nothing below reads out[] or the postfilter state, so
+			 * the call moves after the loop -- where every lane of
+			 * the wave makes it together, instead of once per period
+			 * count the wave's channels end their frames on */
 			v_copy(&out[sb0], &sb[BEGIN], FRAME - sb0);
-			postfilt(D, out, prev->lsf, par->lsf);
 			v_copy(D->sigsave, &sb[BEGIN + FRAME - sb0], len - (FRAME - sb0));
 		} else {
 			v_copy(&out[sb0], &sb[BEGIN], len);
 		}
 		D->syn_begin = add(sb0, len);
 	}
+	postfilt(D, out, prev->lsf, par->lsf);
 	v_copy(D->prev_pcof, cur_p, MIX_ORD + 1);
 	v_copy(D->prev_ncof, cur_n, MIX_ORD + 1);
 	*prev = *par;

@@ -374,13 +374,17 @@ MD void lspVQ_t(const int16_t *target, const int16_t *weight, int16_t *qout, con
 		 * by later inserts.  The network below is InsertCand's insert
 		 * (before equal distortions, last slot evicted) on registers; the
 		 * rows are written out once the stage's scan is done. */
-		int16_t dm[LSP_VQ_CAND];
-		int32_t tag[LSP_VQ_CAND];
+		/* Each slot is one int32 key = dm * 65536 + tag bits: 0x8000 | r
+		 * for row r, (c1 << 9) | e for a new entry (c1 < 8, e < 512).
+		 * Bits below 2^16 never reorder distortions, so key < d * 65536
+		 * exactly when dm < d, and a slot keeps or shifts in one compare
+		 * and two selects.  Lanes insert at different entries, so the
+		 * wave runs this network for most entries of a scan: its length
+		 * is what the scan costs beyond WeightedMSE. */
+		int32_t key[LSP_VQ_CAND];
 #pragma unroll
-		for (int k = 0; k < LSP_VQ_CAND; k++) {
-			dm[k] = SW_MAX_;
-			tag[k] = -1 - k;
-		}
+		for (int k = 0; k < LSP_VQ_CAND; k++)
+			key[k] = SW_MAX_ * 65536 + (0x8000 | k);
 		Word16 maxd = SW_MAX_;
 		for (int c1 = 0; c1 < ncPrev; c1++) {
 			off = 0;
@@ -403,17 +407,16 @@ MD void lspVQ_t(const int16_t *target, const int16_t *weight, int16_t *qout, con
 				for (int e = 0; e < un; e++) {
 					Word16 d = WeightedMSE_t<DIM>(wr, ucb + e * DIM, ct, maxd);
 					if (d < maxd) {
-						int32_t nt = (c1 << 16) | e;
+						const int32_t dk = (int32_t) d * 65536;
+						const int32_t nk = dk + ((c1 << 9) | e);
+						bool kp[LSP_VQ_CAND];
 #pragma unroll
-						for (int k = LSP_VQ_CAND - 1; k >= 0; k--) {
-							bool keep = dm[k] < d;
-							bool prev = k == 0 || dm[k > 0 ? k - 1 : 0] < d;
-							int16_t pd = k > 0 ? dm[k - 1] : d;
-							int32_t pt = k > 0 ? tag[k - 1] : nt;
-							dm[k] = keep ? dm[k] : (prev ? d : pd);
-							tag[k] = keep ? tag[k] : (prev ? nt : pt);
-						}
-						maxd = dm[LSP_VQ_CAND - 1];
+						for (int k = 0; k < LSP_VQ_CAND; k++)
+							kp[k] = key[k] < dk;
+#pragma unroll
+						for (int k = LSP_VQ_CAND - 1; k >= 0; k--)
+							key[k] = kp[k] ? key[k] : ((k == 0 || kp[k > 0 ? k - 1 : 0]) ? nk : key[k > 0 ? k - 1 : 0]);
+						maxd = (Word16) (key[LSP_VQ_CAND - 1] >> 16);
 					}
 					off = add(off, (Word16) dim);
 				}
@@ -423,20 +426,22 @@ MD void lspVQ_t(const int16_t *target, const int16_t *weight, int16_t *qout, con
 		{
 			int16_t rows[LSP_VQ_CAND][LSP_VQ_STAGES];
 			for (int k = 0; k < LSP_VQ_CAND; k++) {
-				if (tag[k] >= 0) {
-					int c1 = tag[k] >> 16;
+				const int t = key[k] & 0xffff;
+				if (!(t & 0x8000)) {
+					int c1 = t >> 9;
 					for (int i = 0; i < s1; i++)
 						rows[k][i] = index[c1][i];
-					rows[k][s1] = (int16_t) (tag[k] & 0xffff);
+					rows[k][s1] = (int16_t) (t & 511);
 				} else {
 					for (int i = 0; i <= s1; i++)
-						rows[k][i] = nextIndex[-1 - tag[k]][i];
+						rows[k][i] = nextIndex[t & 0x7fff][i];
 				}
 			}
 			for (int k = 0; k < LSP_VQ_CAND; k++)
 				for (int i = 0; i <= s1; i++)
 					nextIndex[k][i] = rows[k][i];
-			v_copy(dMin, dm, LSP_VQ_CAND);
+			for (int k = 0; k < LSP_VQ_CAND; k++)
+				dMin[k] = (int16_t) (key[k] >> 16);
 		}
 		if (!flag && s1 == tos - 1) {
 			ncPrev = 1;

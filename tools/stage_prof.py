@@ -3,7 +3,11 @@
 function, the wave-cycles it took per superframe (inclusive of callees),
 as a share of encode_superframe / decode_superframe.
 
-  python tools/stage_prof.py [channels] [superframes]
+  python tools/stage_prof.py [channels] [superframes] [same]
+
+same=1 gives every channel synthetic channel 0's signal (no divergence
+inside a wave), so a stage's share against the default run prices the
+divergence of its channels.
 """
 import os
 import sys
@@ -15,7 +19,7 @@ os.environ.setdefault("MELPE_AMD_LIB", os.path.join(ROOT, "pairphone_amd", "libm
 import numpy as np  # noqa: E402
 
 
-def main(C=65536, nsf=4):
+def main(C=65536, nsf=4, same=0):
     import torch
     import bench
     from pairphone_amd import MelpeEngine, load_library
@@ -30,6 +34,8 @@ def main(C=65536, nsf=4):
     eng.synth_seed(bench.RUN_SEED)
     for k in range(nsf):
         eng.synth_dev(pcm[k].data_ptr(), 540, s)
+    if same:
+        pcm[:] = pcm[:, :1, :]
     buf = np.zeros(64, np.uint64)
     lib.melpe_prof_read(buf.ctypes.data, 64)
     for k in range(nsf):
@@ -46,7 +52,8 @@ def main(C=65536, nsf=4):
     for title, v, tot in (("encode", enc, ("npp_frame", "analysis")),
                           ("decode", dec, ("decode_superframe",))):
         t = float(sum(v[names.index(n)] for n in tot))
-        print("%s: %d channels, %d superframes; wave-cycles per superframe, inclusive" % (title, C, nsf))
+        print("%s: %d channels, %d superframes%s; wave-cycles per superframe, inclusive"
+              % (title, C, nsf, ", every channel channel 0's signal" if same else ""))
         for i in np.argsort(-v.astype(np.float64)):
             if i < len(names) and v[i]:
                 print("  %-20s %12.0f  %5.1f%%" % (names[i], v[i] / waves / nsf, 100 * v[i] / t))
