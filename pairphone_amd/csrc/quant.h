@@ -562,26 +562,27 @@ MN void lsf_vq(EncState *E, MelpParam *par)
 				v_scale(wgt[1], 6554, LPC_ORD);
 		}
 	}
-	if (uvc == 7 || uvc == 6 || uvc == 5 || uvc == 3) {
+	/* One call site per quantisation, its codebook chosen per lane: the
+	 * lanes of a wave carry different voicing patterns, and a call site per
+	 * (branch, codebook) ran each scan once per site the wave's lanes
+	 * used.  lspVQ's scan serialises over the distinct codebooks itself.
+	 * Frame 2 is quantised the same way in both of the reference's branches
+	 * (melp_cb or the 512-entry uv codebook by its own voicing), only the
+	 * candidate list kept differs (flag), so it is one call. */
+	const bool sep = uvc == 7 || uvc == 6 || uvc == 5 || uvc == 3;
+	if (sep) {
 		/* at most one voiced frame: each frame on its own */
-		for (int i = 0; i < NF; i++) {
+		for (int i = 0; i < NF - 1; i++) {
 			bool uv = (uvc >> (NF - 1 - i)) & 1;
-			if (uv)
-				lspVQ(lsp(i), wgt[i], lsp(i), cb_uv, 1, uv_cb_size, q->lsf_index[i],
-				      LPC_ORD, false);
-			else
-				lspVQ(lsp(i), wgt[i], lsp(i), cb_v, 4, melp_cb_size, q->lsf_index[i],
-				      LPC_ORD, false);
+			lspVQ(lsp(i), wgt[i], lsp(i), uv ? cb_uv : cb_v, uv ? 1 : 4,
+			      uv ? uv_cb_size : melp_cb_size, q->lsf_index[i], LPC_ORD, false);
 		}
-	} else {
-		int tos;
-		if (uvc == 1) {
-			tos = 1;
-			lspVQ(lsp(2), wgt[2], lcand[0], cb_uv, tos, uv_cb_size, lidx, LPC_ORD, true);
-		} else {
-			tos = 4;
-			lspVQ(lsp(2), wgt[2], lcand[0], cb_v, tos, melp_cb_size, lidx, LPC_ORD, true);
-		}
+	}
+	const bool uv2 = uvc & 1;
+	const int tos = uv2 ? 1 : 4;
+	lspVQ(lsp(2), wgt[2], sep ? lsp(2) : lcand[0], uv2 ? cb_uv : cb_v, tos,
+	      uv2 ? uv_cb_size : melp_cb_size, sep ? q->lsf_index[2] : lidx, LPC_ORD, !sep);
+	if (!sep) {
 		Word32 minErr = LW_MAX_;
 		int cand = 0;
 		int16_t inp = 0;
