@@ -893,6 +893,29 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 #endif
 	t = frac_pch(&sb[2 + PITCH_FR / 2], &pcorr, pest, 5, PITCHMIN, PITCHMAX,
 		     PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
+#if !defined(MELPE_OPCOUNT)
+	/* The reference's two double_chk calls (pit_lib.c:650 / :663) differ only in
+	 * the threshold t2 and run on the same window, so lanes of both
+	 * branches share one call site (a wave with both kinds of lanes would
+	 * run the check twice). */
+	const bool low = pcorr < 9831;
+	if (low) {
+		v_copy(&sb[LPF_ORD], &speech[-PITCHMAX], PITCH_FR);
+		int64_t tail = 0;
+		for (int i = 2 + PITCH_FR; i < LPF_ORD + PITCH_FR; i++)
+			tail += 2 * (int64_t) ((int32_t) sb[i] * sb[i]);
+		f_pitch_scale(&sb[2], &sb[2], PITCH_FR, &ex, tail);
+		t = frac_pch(&sb[LPF_ORD + PITCH_FR / 2], &pcorr, pest, 0, PITCHMIN, PITCHMAX,
+			     PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
+	}
+	if (low && pcorr < 9012) {
+		pitch = pavg;
+	} else {
+		t2 = low ? ((t > 12800) ? 89 : 115) : ((t > 12800) ? 64 : 96);
+		pitch = double_chk(&sb[LPF_ORD + PITCH_FR / 2], &pcorr, t, t2, PITCHMIN, PITCHMAX,
+				   PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
+	}
+#else
 	if (pcorr < 9831) {
 		v_copy(&sb[LPF_ORD], &speech[-PITCHMAX], PITCH_FR);
 		/* the frac_pch calls below read up to sb[LPF_ORD + PITCH_FR): past
@@ -916,6 +939,7 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 		pitch = double_chk(&sb[LPF_ORD + PITCH_FR / 2], &pcorr, t, t2, PITCHMIN, PITCHMAX,
 				   PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
 	}
+#endif
 	if (pcorr < 9012)
 		pitch = pavg;
 	*pcorr2 = pcorr;

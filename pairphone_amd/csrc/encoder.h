@@ -96,11 +96,11 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 	pcorr = 0;
 #endif
 	for (int i = 0; i < NUM_GAINFR; i++) {
-		if (par->bpvc[0] > BPTHRESH_Q14)
-			par->gain[i] = gain_ana(&speech[FRAME_BEG + (i + 1) * 90], sub_pitch, 120, 320);
-		else
-			par->gain[i] = gain_ana(&speech[FRAME_BEG + (i + 1) * 90],
-						R24 ? 15257 : 15258, 0, 320);
+		/* one call site, its window arguments by voicing (a wave with both
+		 * kinds of frames would run two) */
+		const bool v = par->bpvc[0] > BPTHRESH_Q14;
+		par->gain[i] = gain_ana(&speech[FRAME_BEG + (i + 1) * 90],
+					v ? sub_pitch : (Word16) (R24 ? 15257 : 15258), v ? 120 : 0, 320);
 	}
 	t = (par->gain[NUM_GAINFR - 1] > 7680) ? pcorr : (Word16) 0;
 	E->pitch_avg = p_avg_update(E, par->pitch, t, VMIN_Q14);
