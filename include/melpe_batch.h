@@ -69,6 +69,14 @@ int melpe_engine_reset_dev(melpe_engine *e, const void *d_mask, int which, void 
  * differs. */
 int melpe_engine_set_lane_order(melpe_engine *e, int on);
 
+/* Waves per 64 channels of the analysis kernel: 1 = one lane per channel;
+ * 2 or 4 = each channel's independent analysis chains (bandpass-voicing
+ * bands, LPC/LSF, pitch tracking, classification) spread over that many
+ * waves of one workgroup, for channel counts that would leave SIMDs idle;
+ * 0 (default) = chosen from the channel count.  Bits are the same either
+ * way. */
+int melpe_engine_set_ana_waves(melpe_engine *e, int waves);
+
 /* Per-channel state records, for checkpoint / resume and for moving channels
  * between engines or GPUs (e.g. re-balancing ragged streams).  which: 1 =
  * encoder (EncState), 2 = decoder (DecState).  melpe_engine_state_bytes gives

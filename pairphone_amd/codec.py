@@ -39,6 +39,7 @@ def load_library(path=None):
         "melpe_engine_reset": (i32, [vp, vp, i32]),
         "melpe_engine_reset_dev": (i32, [vp, vp, i32, vp]),
         "melpe_engine_set_lane_order": (i32, [vp, i32]),
+        "melpe_engine_set_ana_waves": (i32, [vp, i32]),
         "melpe_engine_state_bytes": (ctypes.c_long, [i32]),
         "melpe_engine_export": (i32, [vp, i32, i32, i32, vp]),
         "melpe_engine_import": (i32, [vp, i32, i32, i32, vp]),
@@ -218,6 +219,12 @@ class MelpeEngine:
         """pitch-class lane order of the analysis / synthesis kernels on or
         off (results are the same either way)"""
         _check(self.lib.melpe_engine_set_lane_order(self.h, 1 if on else 0))
+
+    def set_ana_waves(self, waves):
+        """waves per 64 channels of the analysis kernel: 1 lane per channel,
+        2 or 4 waves per channel group (ana_mw.h), 0 = by channel count
+        (results are the same either way)"""
+        _check(self.lib.melpe_engine_set_ana_waves(self.h, int(waves)))
 
     def reset_dev(self, d_mask=None, which=3, stream=None):
         """reset enqueued on `stream` (ordered with the *_dev calls on it)"""

@@ -1,0 +1,215 @@
+/*
+ * ana_mw.h -- analysis() (melpe/melp_ana.c:119-267) of one channel split
+ * over the waves of a workgroup: the lanes-per-channel mode of the analysis
+ * kernel (k_enc_ana_mw).
+ *
+ * A superframe's analysis is three frames of melp_ana followed by sc_ana,
+ * the quantisers and the channel packing.  Inside melp_ana several chains
+ * touch disjoint state (state.h groups) and meet only at a few scalars:
+ *   v0  lowpass + find_pitch -> band 0 of bpvc_ana -> residual / peakiness
+ *       -> pitch_ana -> gains -> pitch average            (the driver chain)
+ *   v1  LPC -> LSFs (lpc_pred2lsp is the costly part); bands 1, 2
+ *   v2  pitchAuto of both subframes (corPeak over 127 lags); band 3
+ *   v3  classify of both subframes, one frame behind pitchAuto; band 4
+ * Bands 1..4 need band 0's pitch of the same frame, classify needs
+ * pitchAuto's peak pitch / correlation of the same subframe; each of those
+ * crosses waves through the per-channel exchange block (LDS on the GPU),
+ * in a phase after the one that produced it.  Phase 2i runs frame i's first
+ * half, phase 2i+1 its bands and pitch/gain, phase 6 the last classify, and
+ * phase 7 the tail on v0 after it has gathered classify's and pitchAuto's
+ * tracks (through the HBM record) and the other waves' LSFs and band
+ * voicings (through the exchange block).
+ *
+ * Every chain keeps the reference's operation order on its own data, so the
+ * result is bit-identical to the serial analysis() whatever the number of
+ * physical waves NW: virtual wave v runs on physical wave v % NW, and the
+ * virtual waves that share a physical wave share its copy of the state
+ * (their write sets are disjoint).  NW = 1 is the serial order itself.
+ */
+#ifndef MELPE_ANA_MW_H
+#define MELPE_ANA_MW_H
+
+#include "encoder.h"
+
+namespace mlp {
+
+#define MW_NV 4	/* virtual waves of the schedule */
+#define MW_PHASES (2 * NF + 2)
+
+/* the per-channel exchange block, in int16 words */
+enum {
+	XS_SUBPITCH = 0,	/* [NF] band 0's pitch of frame i (v0 -> v1..v3) */
+	XS_BPVC = XS_SUBPITCH + NF,	/* [NF][NUM_BANDS] bands 1..4 (-> v0) */
+	XS_LSF = XS_BPVC + NF * NUM_BANDS,	/* [NF][LPC_ORD] (v1 -> v0) */
+	XS_CSPC = XS_LSF + NF * LPC_ORD,	/* [2 NF][2] pitchAuto's pitch, corx (v2 -> v3) */
+	XS_WORDS = XS_CSPC + 2 * NF * 2
+};
+
+typedef int16_t __attribute__((__may_alias__)) i16_alias;
+
+/* int16 copy of a record field (no alignment beyond 2 assumed) */
+MD void lane_copy16(void *dst, const void *src, size_t bytes)
+{
+	i16_alias *d = (i16_alias *) dst;
+	const i16_alias *s = (const i16_alias *) src;
+	for (size_t i = 0; i < bytes / 2; i++)
+		d[i] = s[i];
+}
+
+/* what v0 keeps from a frame's first phase for its second and the tail */
+struct AnaMwTmp {
+	int16_t sub_pitch[NF];
+	int16_t peak[NF];
+};
+
+/* the part of each physical wave's private copy that differs from the HBM
+ * record before any phase: dc removal of the three frames (melp_ana.c:
+ * 140-145; each wave filters its own copy, only wave 0 keeps the result) */
+MD void ana_mw_begin(EncState *E, const int16_t *sp_in)
+{
+	for (int i = 0; i < NF; i++)
+		dc_rmv(&sp_in[i * FRAME], &E->hpspeech[IN_BEG + i * FRAME], E->dcdelin, E->dcdelout_hi,
+		       E->dcdelout_lo, FRAME);
+}
+
+/* band k (1..4) of frame i on a non-driver wave */
+template <class X>
+MD void ana_mw_band(EncState *E, X &xc, int i, int k)
+{
+	if (!E->bp_started && i == 0)	/* bpvc_ana's first call, on this band's copy */
+		bpvc_init_band(E, k);
+	const int16_t *speech = &E->hpspeech[i * FRAME];
+	int16_t *b = &E->par[i].bpvc[k];
+	bpvc_band(E, &speech[FRAME_END], k, xc.get(XS_SUBPITCH + i), b);
+	xc.put(XS_BPVC + i * NUM_BANDS + k, *b);
+}
+
+/* classify of frame i's two subframes, with pitchAuto's results of those
+ * subframes taken from the exchange block; the frame's autocorrelation is
+ * recomputed here (lpc_acor, a few hundred ops) instead of exchanged */
+template <class X>
+MD void ana_mw_classify(EncState *E, X &xc, int i)
+{
+	const int16_t *speech = &E->hpspeech[i * FRAME];
+	int16_t ac[17];
+	lpc_acor(&speech[FRAME_END - LPC_FRAME / 2], TB(win_cof), ac, 4, 16, LPC_FRAME);
+	for (int s = 0; s < PIT_SUBNUM; s++) {
+		ClassParam *cs = &E->classStat[CUR_TRACK + i * PIT_SUBNUM + s + 1];
+		cs->pitch = xc.get(XS_CSPC + 2 * (i * PIT_SUBNUM + s));
+		cs->corx = xc.get(XS_CSPC + 2 * (i * PIT_SUBNUM + s) + 1);
+		ana_track_cl(E, speech, i, s, ac);
+	}
+}
+
+/* virtual wave v's work in phase p; rec is the channel's HBM record, which
+ * carries classify's and pitchAuto's tracks to v0 between phases 6 and 7 */
+template <class X>
+MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, AnaMwTmp &tmp, int v, int p)
+{
+	if (p < 2 * NF) {
+		const int i = p >> 1;
+		const int16_t *speech = &E->hpspeech[i * FRAME];
+		MelpParam *par = &E->par[i];
+		if ((p & 1) == 0) {
+			if (v == 0) {
+				int16_t ac[17], lpc[LPC_ORD + 1];
+				Word16 sp;
+				ana_first(E);
+				ana_global_pitch(E, speech);
+				bpvc_init(E);
+				bpvc_band0(E, &speech[FRAME_END], E->fpitch, &par->bpvc[0], &sp);
+				par->jitter = (par->bpvc[0] < VJIT_Q14) ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;
+				ana_lpc<false>(E, speech, ac, lpc, nullptr);
+				Word16 t = ana_resid(E, speech, lpc);
+				ana_peaky(par->bpvc, t, 0, 0);
+				tmp.sub_pitch[i] = sp;
+				tmp.peak[i] = t;
+				xc.put(XS_SUBPITCH + i, sp);
+			} else if (v == 1) {
+				int16_t ac[17], lpc[LPC_ORD + 1];
+				ana_lpc<false>(E, speech, ac, lpc, par->lsf);
+				for (int k = 0; k < LPC_ORD; k++)
+					xc.put(XS_LSF + i * LPC_ORD + k, par->lsf[k]);
+			} else if (v == 2) {
+				for (int s = 0; s < PIT_SUBNUM; s++) {
+					ana_track_pa(E, speech, i, s);
+					const ClassParam *cs = &E->classStat[CUR_TRACK + i * PIT_SUBNUM + s + 1];
+					xc.put(XS_CSPC + 2 * (i * PIT_SUBNUM + s), cs->pitch);
+					xc.put(XS_CSPC + 2 * (i * PIT_SUBNUM + s) + 1, cs->corx);
+				}
+			} else if (i > 0) {
+				ana_mw_classify(E, xc, i - 1);
+			}
+		} else {
+			if (v == 0) {
+				ana_pitch_gain<false>(E, speech, par, tmp.sub_pitch[i]);
+			} else if (v == 1) {
+				ana_mw_band(E, xc, i, 1);
+				ana_mw_band(E, xc, i, 2);
+			} else {
+				ana_mw_band(E, xc, i, v + 1);
+			}
+		}
+	} else if (p == 2 * NF) {
+		if (v == 2) {
+			lane_copy16(rec->pitTrack, E->pitTrack, sizeof(E->pitTrack));
+		} else if (v == 3) {
+			ana_mw_classify(E, xc, NF - 1);
+			lane_copy16(rec->classStat, E->classStat, sizeof(E->classStat));
+			rec->voicedEn = E->voicedEn;
+			rec->silenceEn = E->silenceEn;
+			rec->voicedCnt = E->voicedCnt;
+		}
+	} else if (v == 0) {
+		lane_copy16(E->pitTrack, rec->pitTrack, sizeof(E->pitTrack));
+		lane_copy16(E->classStat, rec->classStat, sizeof(E->classStat));
+		E->voicedEn = rec->voicedEn;
+		E->silenceEn = rec->silenceEn;
+		E->voicedCnt = rec->voicedCnt;
+		for (int i = 0; i < NF; i++) {
+			MelpParam *par = &E->par[i];
+			for (int k = 0; k < LPC_ORD; k++)
+				par->lsf[k] = xc.get(XS_LSF + i * LPC_ORD + k);
+			for (int k = 1; k < NUM_BANDS; k++)
+				par->bpvc[k] = xc.get(XS_BPVC + i * NUM_BANDS + k);
+			ana_peaky(par->bpvc, tmp.peak[i], 1, 2);
+		}
+		analysis_tail(E);
+	}
+}
+
+/* the byte ranges of the record virtual wave v owns (and writes back) */
+MD int ana_mw_owned(int v, size_t *off, size_t *len)
+{
+	const size_t cls = offsetof(EncState, cls), pa = offsetof(EncState, pa);
+	const size_t bs = sizeof(BandState);
+	auto band = [&](int k) { return offsetof(EncState, band) + k * bs; };
+	switch (v) {
+	case 0:
+		off[0] = offsetof(EncState, hpspeech);
+		len[0] = cls - off[0];
+		off[1] = band(0);
+		len[1] = bs;
+		return 2;
+	case 1:
+		off[0] = band(1);
+		len[0] = 2 * bs;
+		return 1;
+	case 2:
+		off[0] = pa;
+		len[0] = sizeof(PautoState);
+		off[1] = band(3);
+		len[1] = bs;
+		return 2;
+	default:
+		off[0] = cls;
+		len[0] = sizeof(ClsState);
+		off[1] = band(4);
+		len[1] = bs;
+		return 2;
+	}
+}
+
+}  // namespace mlp
+
+#endif

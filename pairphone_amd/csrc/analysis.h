@@ -949,6 +949,26 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 /* ------------------------------------------------------------------ */
 /* bpvc_ana, melpe/melp_sub.c:77 -- 5-band bandpass voicing           */
 /* ------------------------------------------------------------------ */
+/* bpvc_ana's first-call zeroing of the band memories (melp_sub.c:91-101) */
+MD void bpvc_init_band(EncState *E, int b)
+{
+	BandState *B = &E->band[b];
+	v_zero(B->fsp, PITCH_FR - FRAME);
+	v_zero(B->delin, BPF_ORD);
+	v_zero(B->delout, BPF_ORD);
+	v_zero(B->env, ENV_ORD);
+	B->env2 = 0;
+}
+
+MD void bpvc_init(EncState *E)
+{
+	if (!E->bp_started) {
+		for (int i = 0; i < NUM_BANDS; i++)
+			bpvc_init_band(E, i);
+		E->bp_started = 1;
+	}
+}
+
 #if defined(MELPE_OPCOUNT)
 /* census build: the reference's pass structure, op for op */
 MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
@@ -958,21 +978,13 @@ MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int1
 	int16_t sb[BPF_ORD + PITCH_FR];
 	Word16 pcorr, t, sc;
 	const int16_t *bden = TB(bpf_den), *bnum = TB(bpf_num);
-	if (!E->bp_started) {
-		for (int i = 0; i < NUM_BANDS; i++) {
-			v_zero(E->bpfsp[i], PITCH_FR - FRAME);
-			v_zero(E->bpfdelin[i], BPF_ORD);
-			v_zero(E->bpfdelout[i], BPF_ORD);
-			v_zero(E->envdel[i], ENV_ORD);
-		}
-		v_zero(E->envdel2, NUM_BANDS);
-		E->bp_started = 1;
-	}
+	bpvc_init(E);
 	const int NEW = BPF_ORD + PITCH_FR - FRAME;	/* 147 */
-	v_copy(&sb[BPF_ORD], E->bpfsp[0], PITCH_FR - FRAME);
+	BandState *B = &E->band[0];
+	v_copy(&sb[BPF_ORD], B->fsp, PITCH_FR - FRAME);
 	v_copy(&sb[NEW], &speech[PITCH_FR - FRAME - PITCHMAX], FRAME);
-	iir3_s(&sb[NEW], bden, bnum, E->bpfdelin[0], E->bpfdelout[0], FRAME, 0);
-	v_copy(E->bpfsp[0], &sb[BPF_ORD + FRAME], PITCH_FR - FRAME);
+	iir3_s(&sb[NEW], bden, bnum, B->delin, B->delout, FRAME, 0);
+	v_copy(B->fsp, &sb[BPF_ORD + FRAME], PITCH_FR - FRAME);
 	f_pitch_scale(&sb[BPF_ORD], &sb[BPF_ORD], PITCH_FR);
 	*pitch = frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[0], fpitch[0], 5, PITCHMIN, PITCHMAX,
 			  PITCHMIN_Q7, PITCHMAX_Q7, 160);
@@ -985,20 +997,21 @@ MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int1
 		}
 	}
 	for (int i = 1; i < NUM_BANDS; i++) {
-		v_copy(&sb[BPF_ORD], E->bpfsp[i], PITCH_FR - FRAME);
+		B = &E->band[i];
+		v_copy(&sb[BPF_ORD], B->fsp, PITCH_FR - FRAME);
 		v_copy(&sb[NEW], &speech[PITCH_FR - FRAME - PITCHMAX], FRAME);
 		int fi = i * (BPF_ORD / 2) * 3;
-		iir3_s(&sb[NEW], bden + fi, bnum + fi, E->bpfdelin[i], E->bpfdelout[i], FRAME, 0);
-		v_copy(E->bpfsp[i], &sb[BPF_ORD + FRAME], PITCH_FR - FRAME);
+		iir3_s(&sb[NEW], bden + fi, bnum + fi, B->delin, B->delout, FRAME, 0);
+		v_copy(B->fsp, &sb[BPF_ORD + FRAME], PITCH_FR - FRAME);
 		sc = f_pitch_scale(&sb[BPF_ORD], &sb[BPF_ORD], PITCH_FR);
 		frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[i], *pitch, 0, PITCHMIN, PITCHMAX,
 			 PITCHMIN_Q7, PITCHMAX_Q7, 160);
 		/* envelope: the history samples are re-scaled to this frame's scale */
-		t = shr(E->envdel2[i], sc);
-		E->envdel2[i] = shr(sb[BPF_ORD + FRAME - 1], (Word16) -sc);
-		v_equ_shr(&sb[BPF_ORD - ENV_ORD], E->envdel[i], sc, ENV_ORD);
+		t = shr(B->env2, sc);
+		B->env2 = shr(sb[BPF_ORD + FRAME - 1], (Word16) -sc);
+		v_equ_shr(&sb[BPF_ORD - ENV_ORD], B->env, sc, ENV_ORD);
 		envelope(&sb[BPF_ORD], t, &sb[BPF_ORD], PITCH_FR);
-		v_equ_shr(E->envdel[i], &sb[BPF_ORD + FRAME - ENV_ORD], (Word16) -sc, ENV_ORD);
+		v_equ_shr(B->env, &sb[BPF_ORD + FRAME - ENV_ORD], (Word16) -sc, ENV_ORD);
 		f_pitch_scale(&sb[BPF_ORD], &sb[BPF_ORD], PITCH_FR);
 		frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, *pitch, 0, PITCHMIN, PITCHMAX,
 			 PITCHMIN_Q7, PITCHMAX_Q7, 160);
@@ -1048,58 +1061,71 @@ MD int64_t bp_window(int16_t *hist, const int16_t *sp, int16_t *w, const int16_t
 	return e;
 }
 
+/* band 0 of bpvc_ana (melp_sub.c:104-135): the lowest band's window, the
+ * better of the two pitch candidates' correlations -> bpvc[0], *pitch.
+ * `speech` as bpvc_ana's. */
+MN void bpvc_band0(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc0,
+		   Word16 *pitch)
+{
+	int16_t sb[BPF_ORD + PITCH_FR];
+	Word16 pcorr, t;
+	BandState *B = &E->band[0];
+	const int16_t *sp = &speech[PITCH_FR - FRAME - PITCHMAX];
+	int16_t *w = &sb[BPF_ORD];
+	int64_t e = bp_window(B->fsp, sp, w, TB(bpf_den), TB(bpf_num), B->delin, B->delout);
+	bool ex;
+	f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
+	*pitch = frac_pch(&sb[BPF_ORD + PITCHMAX], bpvc0, fpitch[0], 5, PITCHMIN, PITCHMAX,
+			  PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
+	for (int i = 1; i < 2; i++) {	/* NUM_PITCHES */
+		t = frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, fpitch[i], 5, PITCHMIN, PITCHMAX,
+			     PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
+		if (pcorr > *bpvc0) {
+			*pitch = t;
+			*bpvc0 = pcorr;
+		}
+	}
+}
+
+/* band i = 1..4 of bpvc_ana (melp_sub.c:137-189): the band's window and
+ * its envelope, each correlated at band 0's pitch; only band i's memories
+ * and bpvc[i] are touched, so the four bands are independent chains */
+MN void bpvc_band(EncState *E, const int16_t *speech, int i, Word16 pitch, int16_t *bpvci)
+{
+	int16_t sb[BPF_ORD + PITCH_FR];
+	Word16 pcorr, t, sc;
+	BandState *B = &E->band[i];
+	const int16_t *sp = &speech[PITCH_FR - FRAME - PITCHMAX];
+	int16_t *w = &sb[BPF_ORD];
+	const int fi = i * (BPF_ORD / 2) * 3;
+	bool ex;
+	int64_t e = bp_window(B->fsp, sp, w, TB(bpf_den) + fi, TB(bpf_num) + fi, B->delin, B->delout);
+	sc = f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
+	frac_pch(&sb[BPF_ORD + PITCHMAX], bpvci, pitch, 0, PITCHMIN, PITCHMAX, PITCHMIN_Q7,
+		 PITCHMAX_Q7, 160, ex);
+	/* envelope: the history samples are re-scaled to this frame's scale */
+	t = shr(B->env2, sc);
+	B->env2 = shr(sb[BPF_ORD + FRAME - 1], (Word16) -sc);
+	v_equ_shr(&sb[BPF_ORD - ENV_ORD], B->env, sc, ENV_ORD);
+	e = envelope_e(w, t, w, PITCH_FR);
+	v_equ_shr(B->env, &sb[BPF_ORD + FRAME - ENV_ORD], (Word16) -sc, ENV_ORD);
+	f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
+	frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, pitch, 0, PITCHMIN, PITCHMAX, PITCHMIN_Q7,
+		 PITCHMAX_Q7, 160, ex);
+	pcorr = sub(pcorr, 1638);
+	if (pcorr > *bpvci)
+		*bpvci = pcorr;
+}
+
 /* bpvc_ana, melpe/melp_sub.c:77 */
 MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
 		 Word16 *pitch)
 {
 	PROF_SCOPE(4);
-	int16_t sb[BPF_ORD + PITCH_FR];
-	Word16 pcorr, t, sc;
-	const int16_t *bden = TB(bpf_den), *bnum = TB(bpf_num);
-	if (!E->bp_started) {
-		for (int i = 0; i < NUM_BANDS; i++) {
-			v_zero(E->bpfsp[i], PITCH_FR - FRAME);
-			v_zero(E->bpfdelin[i], BPF_ORD);
-			v_zero(E->bpfdelout[i], BPF_ORD);
-			v_zero(E->envdel[i], ENV_ORD);
-		}
-		v_zero(E->envdel2, NUM_BANDS);
-		E->bp_started = 1;
-	}
-	const int16_t *sp = &speech[PITCH_FR - FRAME - PITCHMAX];
-	int16_t *w = &sb[BPF_ORD];
-	int64_t e = bp_window(E->bpfsp[0], sp, w, bden, bnum, E->bpfdelin[0], E->bpfdelout[0]);
-	bool ex;
-	f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
-	*pitch = frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[0], fpitch[0], 5, PITCHMIN, PITCHMAX,
-			  PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
-	for (int i = 1; i < 2; i++) {	/* NUM_PITCHES */
-		t = frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, fpitch[i], 5, PITCHMIN, PITCHMAX,
-			     PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
-		if (pcorr > bpvc[0]) {
-			*pitch = t;
-			bpvc[0] = pcorr;
-		}
-	}
-	for (int i = 1; i < NUM_BANDS; i++) {
-		int fi = i * (BPF_ORD / 2) * 3;
-		e = bp_window(E->bpfsp[i], sp, w, bden + fi, bnum + fi, E->bpfdelin[i], E->bpfdelout[i]);
-		sc = f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
-		frac_pch(&sb[BPF_ORD + PITCHMAX], &bpvc[i], *pitch, 0, PITCHMIN, PITCHMAX,
-			 PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
-		/* envelope: the history samples are re-scaled to this frame's scale */
-		t = shr(E->envdel2[i], sc);
-		E->envdel2[i] = shr(sb[BPF_ORD + FRAME - 1], (Word16) -sc);
-		v_equ_shr(&sb[BPF_ORD - ENV_ORD], E->envdel[i], sc, ENV_ORD);
-		e = envelope_e(w, t, w, PITCH_FR);
-		v_equ_shr(E->envdel[i], &sb[BPF_ORD + FRAME - ENV_ORD], (Word16) -sc, ENV_ORD);
-		f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
-		frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, *pitch, 0, PITCHMIN, PITCHMAX,
-			 PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
-		pcorr = sub(pcorr, 1638);
-		if (pcorr > bpvc[i])
-			bpvc[i] = pcorr;
-	}
+	bpvc_init(E);
+	bpvc_band0(E, speech, fpitch, &bpvc[0], pitch);
+	for (int i = 1; i < NUM_BANDS; i++)
+		bpvc_band(E, speech, i, *pitch, &bpvc[i]);
 }
 
 #endif
@@ -1502,14 +1528,14 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 MN void pitchAuto(EncState *E, const int16_t *in, PitTrack *pt, ClassParam *cs)
 {
 	PROF_SCOPE(5);
-	if (!E->pauto_started) {
-		v_zero(E->lpbuf, PIT_COR_LEN);
-		v_zero(E->ivbuf, PIT_COR_LEN);
-		E->pauto_started = 1;
+	if (!E->pa.pauto_started) {
+		v_zero(E->pa.lpbuf, PIT_COR_LEN);
+		v_zero(E->pa.ivbuf, PIT_COR_LEN);
+		E->pa.pauto_started = 1;
 	}
-	lpfilt(in, E->lpbuf, PIT_SUBFRAME);
-	ivfilt(E->ivbuf, E->lpbuf, PIT_SUBFRAME);
-	corPeak(E->ivbuf, pt, cs);
+	lpfilt(in, E->pa.lpbuf, PIT_SUBFRAME);
+	ivfilt(E->pa.ivbuf, E->pa.lpbuf, PIT_SUBFRAME);
+	corPeak(E->pa.ivbuf, pt, cs);
 }
 
 /* multiCheck :433 */
@@ -1832,7 +1858,7 @@ MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *
 	 * the previous call's tail (back_sigbuf) except on the first call */
 	int16_t so[BPF_ORD / 3 + PIT_COR_LEN];
 	int16_t insp[PIT_SUBFRAME];
-	const bool first = !E->cls_started;
+	const bool first = !E->cls.cls_started;
 	const int KEEP = PIT_COR_LEN - PIT_SUBFRAME;	/* 130 */
 	const int16_t *x;
 	int16_t *y;
@@ -1841,16 +1867,16 @@ MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *
 		E->voicedEn = 10240;
 		E->silenceEn = 6144;
 		E->voicedCnt = 0;
-		v_zero(E->bpfdel, BPF_ORD + BPF_ORD / 3);
+		v_zero(E->cls.bpfdel, BPF_ORD + BPF_ORD / 3);
 		slen = PIT_COR_LEN;
 		x = &in[(PIT_SUBFRAME - PIT_COR_LEN) / 2];
 		y = &so[2];
-		E->cls_started = 1;
+		E->cls.cls_started = 1;
 	} else {
 		slen = PIT_SUBFRAME;
 		x = &in[(PIT_COR_LEN - PIT_SUBFRAME) / 2];
 		y = &so[2 + KEEP];
-		v_copy(&so[2], E->back_sigbuf, KEEP);
+		v_copy(&so[2], E->cls.back_sigbuf, KEEP);
 	}
 	/* The reference runs the three sections one after the other through
 	 * ping-pong buffers (:126-168), section s reading its two past inputs
@@ -1869,10 +1895,10 @@ MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *
 			bq[k].n2 = pn[3 * k + 2];
 			bq[k].d1 = pd[3 * k + 1];
 			bq[k].d2 = pd[3 * k + 2];
-			bq[k].i0 = E->bpfdel[2 * k + 1];
-			bq[k].i1 = E->bpfdel[2 * k];
-			bq[k].o0 = E->bpfdel[2 * k + 3];
-			bq[k].o1 = E->bpfdel[2 * k + 2];
+			bq[k].i0 = E->cls.bpfdel[2 * k + 1];
+			bq[k].i1 = E->cls.bpfdel[2 * k];
+			bq[k].o0 = E->cls.bpfdel[2 * k + 3];
+			bq[k].o1 = E->cls.bpfdel[2 * k + 2];
 		}
 		int j = 0;
 		for (; j + 2 <= slen; j += 2) {
@@ -1881,13 +1907,13 @@ MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *
 			y[j + 1] = biq_step(bq[2], biq_step(bq[1], biq_step(bq[0], v1)));
 		}
 		for (int k = 0; k < 3; k++) {
-			E->bpfdel[2 * k] = bq[k].i1;
-			E->bpfdel[2 * k + 1] = bq[k].i0;
+			E->cls.bpfdel[2 * k] = bq[k].i1;
+			E->cls.bpfdel[2 * k + 1] = bq[k].i0;
 		}
-		E->bpfdel[BPF_ORD] = bq[2].o1;
-		E->bpfdel[BPF_ORD + 1] = bq[2].o0;
+		E->cls.bpfdel[BPF_ORD] = bq[2].o1;
+		E->cls.bpfdel[BPF_ORD + 1] = bq[2].o0;
 	}
-	v_copy(E->back_sigbuf, &so[2 + PIT_SUBFRAME], KEEP);
+	v_copy(E->cls.back_sigbuf, &so[2 + PIT_SUBFRAME], KEEP);
 
 	Word16 mx = 0, t1, t2, sh1 = 0;
 	Word32 L1, L2 = 0;

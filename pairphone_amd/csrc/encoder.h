@@ -24,13 +24,14 @@ namespace mlp {
  * prices it in the product code itself, free of profiler perturbation.
  * The output of such a build is wrong by construction. */
 
-template <bool R24>
-MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
+/* melp_ana's parts.  Each touches only its own chain's state (state.h
+ * groups), so melp_ana below runs them in the reference's order while the
+ * multi-wave analysis kernel (ana_mw.h) runs the independent chains on
+ * different waves of one workgroup. */
+
+/* the first call's initialisation (melp_ana.c:300-306) */
+MD void ana_first(EncState *E)
 {
-	PROF_SCOPE(1);
-	int16_t *sb = E->sigbuf;
-	int16_t ac[17], lpc[LPC_ORD + 1];
-	Word16 sub_pitch, t, dontcare, pcorr;
 	if (!E->ana_started) {
 		v_zero(E->lpfsp_delin, LPF_ORD);
 		v_zero(E->lpfsp_delout, LPF_ORD);
@@ -38,56 +39,90 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 		v_set(E->fpitch, DEFAULT_PITCH_Q7, 2);
 		E->ana_started = 1;
 	}
-	/* lowpass for the global pitch; the filter memory advances by FRAME only
-	 * (melp_ana.c:324-346) */
+}
+
+/* lowpass for the global pitch, whose filter memory advances by FRAME only,
+ * then the integer pitch search (melp_ana.c:324-354) -> fpitch[1] (Q7);
+ * sigbuf is this frame's scratch */
+MN void ana_global_pitch(EncState *E, const int16_t *speech)
+{
+	int16_t *sb = E->sigbuf;
+	Word16 dontcare;
 	v_copy(&sb[LPF_ORD], &speech[PITCH_BEG], PITCH_FR);
 	iir3_s(&sb[LPF_ORD], TB(lpf_den), TB(lpf_num), E->lpfsp_delin, E->lpfsp_delout,
 	       PITCH_FR, FRAME);
 	bool ex;
 	f_pitch_scale(&sb[LPF_ORD], &sb[LPF_ORD], PITCH_FR, &ex);
-	E->fpitch[1] = find_pitch(&sb[LPF_ORD + PITCH_FR / 2], &dontcare, 2 * PITCHMIN,
-				  PITCHMAX, PITCHMAX, ex);
+	E->fpitch[1] = find_pitch(&sb[LPF_ORD + PITCH_FR / 2], &dontcare, 2 * PITCHMIN, PITCHMAX,
+				  PITCHMAX, ex);
 	E->fpitch[1] = shl(E->fpitch[1], 7);
-#if !defined(MELPE_KO_BPVC)
-	bpvc_ana(E, &speech[FRAME_END], E->fpitch, par->bpvc, &sub_pitch);
-#else
-	sub_pitch = E->fpitch[0];
-	v_set(par->bpvc, 0, NUM_BANDS);
-#endif
-	par->jitter = (par->bpvc[0] < VJIT_Q14) ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;
+}
+
+/* LPC analysis (melp_ana.c:366-393): ac[17] (the autocorrelation classify
+ * also reads), lpc[0..LPC_ORD] and, when lsf is given, the LSFs */
+template <bool R24>
+MN void ana_lpc(EncState *E, const int16_t *speech, int16_t *ac, int16_t *lpc, int16_t *lsf)
+{
 	lpc_acor(&speech[FRAME_END - LPC_FRAME / 2], TB(win_cof), ac, 4, R24 ? LPC_ORD : 16,
 		 LPC_FRAME);
 	lpc[0] = 4096;
 	lpc_schr(ac, &lpc[1], LPC_ORD);
 	if (R24) {
-		lpc_pred2lsp(&lpc[1], par->lsf, LPC_ORD);
+		lpc_pred2lsp(&lpc[1], lsf, LPC_ORD);
 		v_copy(E->top_lpc, &lpc[1], LPC_ORD);
 	} else {
 		lpc_bwex(&lpc[1], &lpc[1], 32571, LPC_ORD);
-		lpc_pred2lsp(&lpc[1], par->lsf, LPC_ORD);
-		lpc_clmp(par->lsf, 409, LPC_ORD);
-	}
-	zerflt(&speech[PITCH_BEG], lpc, &sb[LPF_ORD], LPC_ORD, PITCH_FR);
-	t = peakiness(&sb[LPF_ORD + PITCHMAX / 2], PITCHMAX);
-	if (t > 5488)
-		par->bpvc[0] = 16384;
-	if (t > 6553) {
-		par->bpvc[1] = 16384;
-		par->bpvc[2] = 16384;
-	}
-	if (!R24) {
-		int ct = CUR_TRACK + subnum * PIT_SUBNUM;
-		for (int i = 0; i < PIT_SUBNUM; i++) {
-#if !defined(MELPE_KO_PAUTO)
-			pitchAuto(E, &speech[FRAME_END + i * PIT_SUBFRAME + PIT_COR_LEN / 2],
-				  &E->pitTrack[ct + i + 1], &E->classStat[ct + i + 1]);
-#endif
-#if !defined(MELPE_KO_CLASSIFY)
-			classify(E, &speech[FRAME_END + i * PIT_SUBFRAME + PIT_SUBFRAME / 2],
-				 &E->classStat[ct + i + 1], ac);
-#endif
+		if (lsf) {
+			lpc_pred2lsp(&lpc[1], lsf, LPC_ORD);
+			lpc_clmp(lsf, 409, LPC_ORD);
 		}
 	}
+}
+
+/* the prediction residual into sigbuf and its peakiness (melp_ana.c:395-399) */
+MN Word16 ana_resid(EncState *E, const int16_t *speech, const int16_t *lpc)
+{
+	int16_t *sb = E->sigbuf;
+	zerflt(&speech[PITCH_BEG], lpc, &sb[LPF_ORD], LPC_ORD, PITCH_FR);
+	return peakiness(&sb[LPF_ORD + PITCHMAX / 2], PITCHMAX);
+}
+
+/* extreme peakiness forces the lower bands voiced (melp_ana.c:401-410) */
+MD void ana_peaky(int16_t *bpvc, Word16 t, int lo, int hi)
+{
+	if (t > 5488 && lo == 0)
+		bpvc[0] = 16384;
+	if (t > 6553)
+		for (int k = lo > 1 ? lo : 1; k <= hi && k <= 2; k++)
+			bpvc[k] = 16384;
+}
+
+/* pitchAuto + classify of one 90-sample subframe of frame subnum
+ * (melp_ana.c:411-426): sub 0 / 1 */
+MN void ana_track_pa(EncState *E, const int16_t *speech, int subnum, int sub)
+{
+	int ct = CUR_TRACK + subnum * PIT_SUBNUM;
+#if !defined(MELPE_KO_PAUTO)
+	pitchAuto(E, &speech[FRAME_END + sub * PIT_SUBFRAME + PIT_COR_LEN / 2],
+		  &E->pitTrack[ct + sub + 1], &E->classStat[ct + sub + 1]);
+#endif
+}
+
+MN void ana_track_cl(EncState *E, const int16_t *speech, int subnum, int sub, const int16_t *ac)
+{
+	int ct = CUR_TRACK + subnum * PIT_SUBNUM;
+#if !defined(MELPE_KO_CLASSIFY)
+	classify(E, &speech[FRAME_END + sub * PIT_SUBFRAME + PIT_SUBFRAME / 2],
+		 &E->classStat[ct + sub + 1], ac);
+#endif
+}
+
+/* final pitch, gains, pitch average and voicing (melp_ana.c:428-468) */
+template <bool R24>
+MN void ana_pitch_gain(EncState *E, const int16_t *speech, MelpParam *par, Word16 sub_pitch)
+{
+	int16_t *sb = E->sigbuf;
+	Word16 pcorr, t;
 #if !defined(MELPE_KO_PITCHANA)
 	par->pitch = pitch_ana(E, &speech[FRAME_END], &sb[LPF_ORD + PITCHMAX], sub_pitch,
 			       E->pitch_avg, &pcorr);
@@ -107,6 +142,32 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 	if (!R24)
 		par->uv_flag = (par->bpvc[0] > BPTHRESH_Q14) ? 0 : 1;
 	E->fpitch[0] = E->fpitch[1];
+}
+
+template <bool R24>
+MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
+{
+	PROF_SCOPE(1);
+	int16_t ac[17], lpc[LPC_ORD + 1];
+	Word16 sub_pitch;
+	ana_first(E);
+	ana_global_pitch(E, speech);
+#if !defined(MELPE_KO_BPVC)
+	bpvc_ana(E, &speech[FRAME_END], E->fpitch, par->bpvc, &sub_pitch);
+#else
+	sub_pitch = E->fpitch[0];
+	v_set(par->bpvc, 0, NUM_BANDS);
+#endif
+	par->jitter = (par->bpvc[0] < VJIT_Q14) ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;
+	ana_lpc<R24>(E, speech, ac, lpc, par->lsf);
+	ana_peaky(par->bpvc, ana_resid(E, speech, lpc), 0, 2);
+	if (!R24) {
+		for (int i = 0; i < PIT_SUBNUM; i++) {
+			ana_track_pa(E, speech, subnum, i);
+			ana_track_cl(E, speech, subnum, i, ac);
+		}
+	}
+	ana_pitch_gain<R24>(E, speech, par, sub_pitch);
 }
 
 /* subenergyRelation1/2 :955/:980 (plain int arithmetic, as the reference) */

@@ -66,6 +66,8 @@ int kl_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active, int n, hipStre
 int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
 	       const int *perm, const int *nlive,
 	       hipStream_t s);
+int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
+		  const int *perm, const int *nlive, int nw, hipStream_t s);
 int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto, hipStream_t s);
 int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
 	      const int *perm, const int *nlive,
@@ -399,7 +401,15 @@ static_assert(NBIN < 0xff, "class ids and the not-live mark 0xff must fit the ui
 struct BinBuf {
 	int *perm = nullptr;	/* [C] lane -> channel */
 	uint8_t *key = nullptr;	/* [C] class of each channel (0xff: not live) */
-	unsigned *ctl = nullptr;	/* [0,64) counts, [64,128) next slot, [128] live count */
+	/* [0, NBIN) counts, [NBIN, 2 NBIN) next slot of each class, [2 NBIN]
+	 * the live count */
+	unsigned *ctl = nullptr;
+	/* The buffers are one per engine and direction, but *_dev calls may
+	 * come on different streams: the sort of a call waits for the kernel
+	 * that read the previous call's order (its stream recorded `done`). */
+	hipEvent_t done = nullptr;
+	hipStream_t last = nullptr;
+	bool used = false;
 };
 
 static hipError_t bin_alloc(BinBuf *b, int channels)
@@ -409,6 +419,11 @@ static hipError_t bin_alloc(BinBuf *b, int channels)
 	hipError_t er = hipMalloc(&p, pb + cb + (size_t) channels);
 	if (er != hipSuccess)
 		return er;
+	er = hipEventCreateWithFlags(&b->done, hipEventDisableTiming);
+	if (er != hipSuccess) {
+		hipFree(p);
+		return er;
+	}
 	b->perm = (int *) p;
 	b->ctl = (unsigned *) (p + pb);
 	b->key = (uint8_t *) (p + pb + cb);
@@ -521,18 +536,36 @@ static int bin_key_mode(void)
 	return v;
 }
 
-static bool bin_launch(int order, BinBuf &b, const void *rec, size_t stride, int off_par,
-		       int off_uv, const uint8_t *active, int n, hipStream_t s)
+/* *on: whether the order is used (false: identity lanes + mask) */
+static hipError_t bin_launch(int order, BinBuf &b, const void *rec, size_t stride, int off_par,
+			     int off_uv, const uint8_t *active, int n, hipStream_t s, bool *on)
 {
-	if (order == 0 || (order < 0 && !bin_enabled()))
-		return false;
+	*on = !(order == 0 || (order < 0 && !bin_enabled()));
+	if (!*on)
+		return hipSuccess;
+	hipError_t er;
+	if (b.used && b.last != s && (er = hipStreamWaitEvent(s, b.done, 0)) != hipSuccess)
+		return er;
 	unsigned g = (unsigned) ((n + 255) / 256);
-	hipMemsetAsync(b.ctl, 0, sizeof(unsigned) * NBIN, s);
+	if ((er = hipMemsetAsync(b.ctl, 0, sizeof(unsigned) * NBIN, s)) != hipSuccess)
+		return er;
 	k_bin_count<<<g, 256, 0, s>>>((const char *) rec, stride, off_par, off_uv, active, n, b,
 				      bin_key_mode());
+	if ((er = hipGetLastError()) != hipSuccess)
+		return er;
 	k_bin_scan<<<1, WAVE, 0, s>>>(b);
+	if ((er = hipGetLastError()) != hipSuccess)
+		return er;
 	k_bin_scatter<<<g, 256, 0, s>>>(n, b);
-	return true;
+	return hipGetLastError();
+}
+
+/* after the kernel that reads b's order, on the same stream */
+static hipError_t bin_release(BinBuf &b, hipStream_t s)
+{
+	b.last = s;
+	b.used = true;
+	return hipEventRecord(b.done, s);
 }
 
 struct melpe_engine {
@@ -549,32 +582,69 @@ struct melpe_engine {
 	int16_t *d_npp = nullptr;	/* staging of melpe_npp_host, grown on demand */
 	BinBuf bin_enc, bin_dec;	/* pitch-class lane order of k_enc_ana / k_decode */
 	int lane_order = -1;	/* 1 on, 0 off, -1 the MELPE_BIN default */
+	int ana_waves = 0;	/* waves per 64 channels in k_enc_ana(_mw); 0: by channel count */
 	size_t npp_bytes = 0;
 	float last_ms = 0.f;
 };
+
+/*
+ * Waves per 64 channels of the analysis kernel.  Lane-per-channel (1) needs
+ * about four waves per SIMD to hide its scratch latency; below that the
+ * channel count leaves SIMDs idle or alone, and the multi-wave kernel
+ * (k_enc_ana_mw, ana_mw.h) spreads each channel's independent chains over
+ * 2 or 4 waves instead.  MELPE_ANA_NW overrides (diagnostics).
+ */
+static int ana_waves_for(melpe_engine *e)
+{
+	static int env = -2;
+	if (env == -2) {
+		const char *v = getenv("MELPE_ANA_NW");
+		env = v ? atoi(v) : -1;
+	}
+	int nw = env >= 0 ? env : e->ana_waves;
+	if (nw == 1 || nw == 2 || nw == 4)
+		return nw;
+	long waves = (e->channels + WAVE - 1) / WAVE;
+	return waves <= 1024 ? 4 : waves <= 2048 ? 2 : 1;
+}
 
 static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, const uint8_t *d_act,
 		      hipStream_t s)
 {
 	BinBuf &b = e->bin_enc;
-	bool on = bin_launch(e->lane_order, b, e->d_enc, sizeof(EncState),
-			     (int) offsetof(EncState, par),
-			     (int) (offsetof(EncState, qpar) + offsetof(QuantParam, uv_flag)), d_act,
-			     e->channels, s);
-	return kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, on ? b.perm : nullptr,
-			  on ? (const int *) (b.ctl + 2 * NBIN) : nullptr, s);
+	bool on;
+	hipError_t er = bin_launch(e->lane_order, b, e->d_enc, sizeof(EncState),
+				   (int) offsetof(EncState, par),
+				   (int) (offsetof(EncState, qpar) + offsetof(QuantParam, uv_flag)),
+				   d_act, e->channels, s, &on);
+	if (er != hipSuccess)
+		return (int) er;
+	const int *perm = on ? b.perm : nullptr;
+	const int *nlive = on ? (const int *) (b.ctl + 2 * NBIN) : nullptr;
+	int nw = ana_waves_for(e);
+	int rc = nw == 1 ? kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, s)
+			 : kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nw, s);
+	if (rc == 0 && on)
+		rc = (int) bin_release(b, s);
+	return rc;
 }
 
 static int dec_launch(melpe_engine *e, int16_t *d_sp, const uint8_t *d_bits, const uint8_t *d_act,
 		      hipStream_t s)
 {
 	BinBuf &b = e->bin_dec;
-	bool on = bin_launch(e->lane_order, b, e->d_dec, sizeof(DecState),
-			     (int) offsetof(DecState, par),
-			     (int) (offsetof(DecState, qpar) + offsetof(QuantParam, uv_flag)), d_act,
-			     e->channels, s);
-	return kl_decode(e->d_dec, d_sp, d_bits, d_act, e->channels, on ? b.perm : nullptr,
-			 on ? (const int *) (b.ctl + 2 * NBIN) : nullptr, s);
+	bool on;
+	hipError_t er = bin_launch(e->lane_order, b, e->d_dec, sizeof(DecState),
+				   (int) offsetof(DecState, par),
+				   (int) (offsetof(DecState, qpar) + offsetof(QuantParam, uv_flag)),
+				   d_act, e->channels, s, &on);
+	if (er != hipSuccess)
+		return (int) er;
+	int rc = kl_decode(e->d_dec, d_sp, d_bits, d_act, e->channels, on ? b.perm : nullptr,
+			   on ? (const int *) (b.ctl + 2 * NBIN) : nullptr, s);
+	if (rc == 0 && on)
+		rc = (int) bin_release(b, s);
+	return rc;
 }
 
 static std::mutex g_dev_mu;
@@ -678,6 +748,14 @@ int melpe_engine_set_lane_order(melpe_engine *e, int on)
 	return 0;
 }
 
+int melpe_engine_set_ana_waves(melpe_engine *e, int waves)
+{
+	if (!e || !(waves == 0 || waves == 1 || waves == 2 || waves == 4))
+		return fail_msg("melpe_engine_set_ana_waves: waves must be 0 (auto), 1, 2 or 4");
+	e->ana_waves = waves;
+	return 0;
+}
+
 int melpe_engine_destroy(melpe_engine *e)
 {
 	if (!e)
@@ -694,6 +772,10 @@ int melpe_engine_destroy(melpe_engine *e)
 	hipFree(e->d_mask);
 	hipFree(e->bin_enc.perm);
 	hipFree(e->bin_dec.perm);
+	if (e->bin_enc.done)
+		hipEventDestroy(e->bin_enc.done);
+	if (e->bin_dec.done)
+		hipEventDestroy(e->bin_dec.done);
 	if (e->ev0)
 		hipEventDestroy(e->ev0);
 	if (e->ev1)

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "codec.h"
+#include "ana_mw.h"
 #include "codec2400.h"
 #include "voice_crypt.h"
 #include "vad.h"
@@ -113,6 +114,48 @@ int emu_encode_ana(emu_engine *e, unsigned char *bits, const int16_t *sp)
 		analysis(&e->enc[c], sp + (size_t) c * BLOCK);
 		for (int k = 0; k < 11; k++)
 			bits[c * 11 + k] = e->enc[c].chbuf[k];
+	}
+	return 0;
+}
+
+/* the multi-wave analysis (ana_mw.h) as k_enc_ana_mw runs it: nw physical
+ * waves, each with its own private copy of the record, phase by phase (the
+ * barriers), the exchange block and the HBM record the only shared data;
+ * each wave writes back the state groups of its virtual waves */
+struct HostXch {
+	int16_t w[XS_WORDS];
+	int16_t get(int k) const { return w[k]; }
+	void put(int k, int16_t v) { w[k] = v; }
+};
+
+int emu_encode_ana_mw(emu_engine *e, unsigned char *bits, const int16_t *sp, int nw)
+{
+	if (nw < 1 || nw > MW_NV)
+		return -1;
+	std::vector<EncState> W(nw);
+	for (int c = 0; c < e->channels; c++) {
+		EncState &rec = e->enc[c];
+		const int16_t *x = sp + (size_t) c * BLOCK;
+		HostXch xc;
+		memset(&xc, 0x5a, sizeof xc);	/* nothing may read a slot before it is written */
+		AnaMwTmp tmp[MW_NV];
+		for (int w = 0; w < nw; w++) {
+			W[w] = rec;
+			ana_mw_begin(&W[w], x);
+		}
+		for (int p = 0; p < MW_PHASES; p++)
+			for (int w = 0; w < nw; w++)
+				for (int v = w; v < MW_NV; v += nw)
+					ana_mw_phase(&W[w], &rec, xc, tmp[w], v, p);
+		for (int w = 0; w < nw; w++)
+			for (int v = w; v < MW_NV; v += nw) {
+				size_t off[2], len[2];
+				int n = ana_mw_owned(v, off, len);
+				for (int k = 0; k < n; k++)
+					memcpy((char *) &rec + off[k], (const char *) &W[w] + off[k], len[k]);
+			}
+		for (int k = 0; k < 11; k++)
+			bits[c * 11 + k] = rec.chbuf[k];
 	}
 	return 0;
 }

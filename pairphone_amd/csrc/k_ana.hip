@@ -6,6 +6,7 @@
  */
 #include <stdlib.h>
 #include "kern.h"
+#include "ana_mw.h"
 
 MELPE_TU(ana)
 
@@ -37,6 +38,92 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 	lane_copy((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, ENC_ANA_BYTES);
 	for (int k = 0; k < 11; k++)
 		bits[(size_t) c * 11 + k] = L.S.chbuf[k];
+}
+
+/*
+ * Lanes-per-channel analysis (ana_mw.h): a workgroup of NW waves runs the
+ * same 64 channels, lane t of every wave on channel t, each wave on its own
+ * private copy of the record.  The superframe's independent chains (band 0
+ * + pitch/gain, LPC + bands 1-2, pitchAuto + band 3, classify + band 4)
+ * run on different waves; the few scalars one chain hands another cross
+ * through the per-channel exchange block in LDS, ordered by the barrier
+ * between phases.  Used when the channels alone would leave SIMDs idle
+ * (engine.hip ana_waves): at 32,768 channels lane-per-channel is 512 waves
+ * for 1,024 SIMDs.
+ */
+struct LdsXch {
+	int16_t *w;
+	int t;
+	__device__ int16_t get(int k) const { return w[k * WAVE + t]; }
+	__device__ void put(int k, int16_t v) { w[k * WAVE + t] = v; }
+};
+
+struct AnaMwLane {
+	uint8_t guard[FLAT_GUARD_BYTES];
+	EncState S;	/* only the part after the NPP state is live */
+	int16_t x[BLOCK];
+	AnaMwTmp tmp;
+};
+
+template <int NW>
+__global__ __launch_bounds__(WAVE * NW, MELPE_ENC_WAVES) void k_enc_ana_mw(EncState *enc, const int16_t *sp,
+									    uint8_t *bits, const uint8_t *active,
+									    int n, const int *perm, const int *nlive)
+{
+	__shared__ int16_t xs[XS_WORDS * WAVE];
+	const int w = threadIdx.x / WAVE, t = threadIdx.x % WAVE;
+	int c = blockIdx.x * WAVE + t;
+	bool live;
+	if (perm) {
+		live = c < *nlive;
+		c = live ? perm[c] : 0;
+	} else {
+		live = c < n && (!active || active[c]);
+	}
+	AnaMwLane L;
+	PIN_FRAME(L);
+	LdsXch xc{xs, t};
+	EncState *rec = &enc[c];
+	if (live) {
+		lane_copy((char *) &L.S + ENC_ANA_OFF, (const char *) rec + ENC_ANA_OFF, ENC_ANA_BYTES);
+		lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
+		ana_mw_begin(&L.S, L.x);
+	}
+	for (int p = 0; p < MW_PHASES; p++) {
+		if (live)
+			for (int v = w; v < MW_NV; v += NW)
+				ana_mw_phase(&L.S, rec, xc, L.tmp, v, p);
+		/* phase 2 NF hands classify's / pitchAuto's tracks to wave 0
+		 * through the record: device-scope fences around the barrier */
+		if (p == 2 * NF)
+			__threadfence();
+		__syncthreads();
+		if (p == 2 * NF)
+			__threadfence();
+	}
+	if (!live)
+		return;
+	for (int v = w; v < MW_NV; v += NW) {
+		size_t off[2], len[2];
+		int m = ana_mw_owned(v, off, len);
+		for (int k = 0; k < m; k++)
+			lane_copy((char *) rec + off[k], (const char *) &L.S + off[k], len[k]);
+	}
+	if (w == 0)
+		for (int k = 0; k < 11; k++)
+			bits[(size_t) c * 11 + k] = L.S.chbuf[k];
+}
+
+extern "C" int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
+			     int n, const int *perm, const int *nlive, int nw, hipStream_t s)
+{
+	if (nw == 2)
+		k_enc_ana_mw<2><<<grid_for(n), WAVE * 2, 0, s>>>(enc, sp, bits, active, n, perm, nlive);
+	else if (nw == 4)
+		k_enc_ana_mw<4><<<grid_for(n), WAVE * 4, 0, s>>>(enc, sp, bits, active, n, perm, nlive);
+	else
+		return (int) hipErrorInvalidValue;
+	return (int) hipGetLastError();
 }
 
 /* debug aid: analysis cut after `upto` stages (0 = nothing) */

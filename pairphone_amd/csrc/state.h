@@ -89,8 +89,36 @@ struct PitTrack {	/* pitTrackParam, melpe/cprv.h:34 */
 	int16_t pit[NODE], weight[NODE], cost[NODE];
 };
 
+/* The analysis state is grouped by the task chain that owns it, each group
+ * dword-aligned and contiguous, so the multi-wave analysis kernel
+ * (ana_mw.h) can hand each group back to HBM from the wave that ran that
+ * chain: the driver group (frames' pitch/gain chain, sc_ana, quantisers,
+ * packing), classify's, pitchAuto's, and one per bandpass-voicing band. */
+
+/* melpe/classify.c statics */
+struct alignas(4) ClsState {
+	int16_t cls_started;
+	int16_t bpfdel[BPF_ORD + BPF_ORD / 3];
+	int16_t back_sigbuf[PIT_COR_LEN - PIT_SUBFRAME];
+};
+
+/* melpe/pitch.c statics */
+struct alignas(4) PautoState {
+	int16_t pauto_started;
+	int16_t lpbuf[PIT_COR_LEN], ivbuf[PIT_COR_LEN];
+};
+
+/* one band of melpe/melp_sub.c bpvc_ana's statics (:81-86 keep them as
+ * [NUM_BANDS][..] arrays; here band-major) */
+struct alignas(4) BandState {
+	int16_t fsp[PITCH_FR - FRAME];	/* bpfsp[b] */
+	int16_t delin[BPF_ORD], delout[BPF_ORD];	/* bpfdelin/out[b] */
+	int16_t env[ENV_ORD], env2;	/* envdel[b], envdel2[b] */
+};
+
 struct EncState {
 	NppState npp;
+	/* ---- driver group ---- */
 	/* melpe/global.c */
 	int16_t hpspeech[IN_BEG + BLOCK];
 	int16_t dcdelin[DC_ORD], dcdelout_hi[DC_ORD], dcdelout_lo[DC_ORD];
@@ -106,18 +134,8 @@ struct EncState {
 	int16_t lpfsp_delin[LPF_ORD], lpfsp_delout[LPF_ORD];
 	int16_t pitch_avg, fpitch[2];
 	int16_t sc_prev_sbp3, sc_prev_uv, sc_prev_pitch;
-	/* melpe/classify.c */
-	int16_t cls_started;
-	int16_t bpfdel[BPF_ORD + BPF_ORD / 3];
-	int16_t back_sigbuf[PIT_COR_LEN - PIT_SUBFRAME];
-	/* melpe/pitch.c */
-	int16_t pauto_started;
-	int16_t lpbuf[PIT_COR_LEN], ivbuf[PIT_COR_LEN];
-	/* melpe/melp_sub.c (bpvc_ana) */
+	/* melpe/melp_sub.c bpvc_ana's first-call flag */
 	int16_t bp_started;
-	int16_t bpfsp[NUM_BANDS][PITCH_FR - FRAME];
-	int16_t bpfdelin[NUM_BANDS][BPF_ORD], bpfdelout[NUM_BANDS][BPF_ORD];
-	int16_t envdel[NUM_BANDS][ENV_ORD], envdel2[NUM_BANDS];
 	/* melpe/pit_lib.c */
 	int16_t pavg_started, good_pitch[NF];
 	int16_t pana_started;
@@ -136,6 +154,10 @@ struct EncState {
 	int16_t top_lpc[LPC_ORD];
 	int16_t qg_prev_gain;
 	int16_t pad24_;
+	/* ---- the other chains' groups ---- */
+	ClsState cls;
+	PautoState pa;
+	BandState band[NUM_BANDS];	/* band[0] belongs to the driver group */
 };
 
 #define MIX_ORD 32
