@@ -32,9 +32,10 @@ the committed rocprofv3 --pmc passes at this channel count
 (profiles/pmc_latest.json, which names its source file).
 
 cpu_baseline: the reference codec itself (oracle/_ref/ref_tool, compiled from
-/root/reference by oracle/Makefile), one single-channel process per core on a
-bounded sample of the same channels; its bitstreams double as a parity spot
-check of the timed GPU output.
+/root/reference by oracle/Makefile), one single-channel process per host
+core on a bounded sample of the same channels, measured at 16, 64 and all
+usable cores (the value is the all-cores point); its bitstreams double as a
+parity spot check of the timed GPU output.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--channels C]
                   [--total-channels T]
@@ -66,7 +67,6 @@ PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12     # INT32 lane-ops/s, T
 # 24 rot, chi 75 (not, and, xor per lane), iota 1 = 155 64-bit ops; x 24 rounds
 VC_OPS_PER_PACKET = 2 * 155 * 24
 REF_TOOL = os.path.join(ROOT, "oracle", "_ref", "ref_tool")
-BOX_CPU_SHARE = 16      # host cores a one-GPU job may use on the GPU box
 
 
 def parse(argv=None):
@@ -85,7 +85,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-channels", type=int, default=128)
     ap.add_argument("--cpu-jobs", type=int, default=0,
-                    help="0 = min(%d, usable cores)" % BOX_CPU_SHARE)
+                    help="one point at this many processes (0 = the curve 16, 64, all cores)")
     return ap.parse_args(argv)
 
 
@@ -278,34 +278,61 @@ def usable_cores():
         return os.cpu_count() or 1
 
 
-def cpu_baseline(args, gpu_bits):
-    """Reference codec, one single-channel process per core, on channels
-    0..S-1 of the same synthetic input.  Returns (baseline dict, parity
-    dict)."""
-    if args.no_cpu_baseline or not os.path.exists(REF_TOOL):
-        return None, None
-    usable = usable_cores()
-    jobs = args.cpu_jobs or min(BOX_CPU_SHARE, usable)
-    S = max(args.cpu_sample_channels, 4 * jobs)
-    nsf = max(149, gpu_bits.shape[0])
+def cgroup_cpu_quota():
+    """cores' worth of CPU time the job's cgroup grants (cpu.max), or None"""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
+def _ref_encode_rate(jobs, S, nsf, first=0):
+    """the reference encoding S channels x nsf superframes, `jobs` single-
+    channel processes at a time: (channel-s/s, wall s, bits [S, nsf*11])"""
     with tempfile.TemporaryDirectory() as tmp:
         out = os.path.join(tmp, "b.bits")
         t0 = time.perf_counter()
-        subprocess.run([REF_TOOL, "jobs", str(jobs), "encgen", str(RUN_SEED), "0", str(S),
+        subprocess.run([REF_TOOL, "jobs", str(jobs), "encgen", str(RUN_SEED), str(first), str(S),
                         str(nsf), out], check=True)
         dt = time.perf_counter() - t0
-        ref = np.fromfile(out, dtype=np.uint8).reshape(S, nsf * SF_BYTES)
-    value = S * nsf * SF_SECONDS / dt
-    base = {"value": value, "unit": "channel-s/s", "cores": jobs, "kind": "reference",
-            "per_core": value / jobs, "host_cores_visible": usable,
-            "host_cores_note": "the GPU box gives a one-GPU job a %d-core share of the host; "
-                               "per_core x host_cores_visible is the whole-host extrapolation"
-                               % BOX_CPU_SHARE,
-            "host_extrapolated": value / jobs * usable,
-            "sample": "%d channels x %d superframes (%.1f s of audio each), melpe_a, one forked "
-                      "single-channel reference process per channel, %d at a time, %.1f s wall"
-                      % (S, nsf, nsf * SF_SECONDS, jobs, dt)}
-    n = min(S, gpu_bits.shape[1])
+        bits = np.fromfile(out, dtype=np.uint8).reshape(S, nsf * SF_BYTES)
+    return S * nsf * SF_SECONDS / dt, dt, bits
+
+
+def cpu_baseline(args, gpu_bits):
+    """The reference codec, one single-channel process per host core
+    (north_star), on a bounded sample of the same channels: a curve over 16,
+    64 and all usable cores, each point 2 channels per process x 10 s of
+    audio; the line's value is the all-cores point.  The first point's
+    bitstreams double as a parity spot check of the timed GPU output.
+    Returns (baseline dict, parity dict)."""
+    if args.no_cpu_baseline or not os.path.exists(REF_TOOL):
+        return None, None
+    usable = usable_cores()
+    nsf = max(149, gpu_bits.shape[0])
+    points = sorted(set([args.cpu_jobs] if args.cpu_jobs else
+                        [n for n in (16, 64) if n < usable] + [usable]))
+    curve, ref = [], None
+    for jobs in points:
+        S = max(args.cpu_sample_channels, 2 * jobs)
+        value, dt, bits = _ref_encode_rate(jobs, S, nsf)
+        if ref is None:
+            ref = bits
+        curve.append({"processes": jobs, "channels": S, "value": value, "wall_s": dt,
+                      "per_process": value / jobs})
+        log("cpu baseline: %d processes, %d channels: %.0f channel-s/s (%.1f s)"
+            % (jobs, S, value, dt))
+    top = curve[-1]
+    quota = cgroup_cpu_quota()
+    base = {"value": top["value"], "unit": "channel-s/s", "cores": top["processes"],
+            "kind": "reference", "host_cores_visible": usable, "cgroup_cpu_quota_cores": quota,
+            "curve": curve,
+            "sample": "channels 0..S-1 x %d superframes (%.1f s of audio each), melpe_a, one "
+                      "forked single-channel reference process per channel, `processes` at a "
+                      "time; value = the all-cores point (%d processes, %d channels, %.1f s wall)"
+                      % (nsf, nsf * SF_SECONDS, top["processes"], top["channels"], top["wall_s"])}
+    n = min(ref.shape[0], gpu_bits.shape[1])
     k = gpu_bits.shape[0]
     g = np.ascontiguousarray(gpu_bits[:, :n, :].transpose(1, 0, 2)).reshape(n, k * SF_BYTES)
     same = bool(np.array_equal(g, ref[:n, :k * SF_BYTES]))

@@ -243,6 +243,12 @@ int melpe_demodulate_dev(void *d_state, const void *d_pcm, long stride, void *d_
  * reference's operators. */
 int melpe_ops_eval_dev(int op, const void *d_a, const void *d_b, const void *d_c, void *d_out,
 		       long n, void *hip_stream);
+/* Device self-test of the sample-stream and exact-correlator helpers the
+ * codec kernels use (pairphone_amd/csrc/helpers_eval.h): n lanes, lane i on
+ * its own 464 int16 of d_src at the offsets / length d_args[4i .. 4i+2],
+ * 512 int32 results per lane in d_out.  tests/test_device_helpers.py. */
+int melpe_helpers_eval_dev(int mode, const void *d_src, const void *d_args, void *d_out, int n,
+			   void *hip_stream);
 
 /* Diagnostics: per-stage wave-cycle totals of a profiling build
  * (libmelpe_amd_prof.so, -DMELPE_PROF; tools/stage_prof.py), read and

@@ -131,7 +131,7 @@ def device_disassembly(obj):
 # to the private segment is aperture-checked before its offset is added,
 # which faulted on gfx950 (kern.h FLAT_GUARD_BYTES)
 NO_FLAT = ("k_enc_ana", "k_decode", "k_vad", "k_enc_npp", "k_npp", "k_demodulate", "k_enc24",
-           "k_dec24")
+           "k_dec24", "k_helpers_eval")
 
 
 def check_no_flat(objdir):

@@ -48,6 +48,7 @@ def load_library(path=None):
         "melpe_modulate_dev": (i32, [vp, vp, vp, i32, i32, vp, vp]),
         "melpe_demodulate_dev": (i32, [vp, vp, ctypes.c_long, vp, vp, vp, vp, i32, i32, vp, vp]),
         "melpe_ops_eval_dev": (i32, [i32, vp, vp, vp, vp, ctypes.c_long, vp]),
+        "melpe_helpers_eval_dev": (i32, [i32, vp, vp, vp, i32, vp]),
         "melpe_encode_host": (i32, [vp, vp, vp, vp]),
         "melpe_encode_dev": (i32, [vp, vp, vp, vp, vp]),
         "melpe_encode_npp_dev": (i32, [vp, vp, vp, vp]),

@@ -27,6 +27,7 @@
 #include "voice_crypt.h"
 #include "vad.h"
 #include "ops_eval.h"
+#include "helpers_eval.h"
 #define MODEM_FN __host__ __device__ static inline
 #include "modem.h"
 #include "../../include/melpe.h"
@@ -308,6 +309,31 @@ __global__ __launch_bounds__(256) void k_ops_eval(int op, const int64_t *A, cons
 	default: r = 0;
 	}
 	out[i] = r;
+}
+
+/* device helper self-test (helpers_eval.h): lane i copies its HE_N
+ * samples into a private array -- the codec's streams read the private
+ * segment, at per-lane alignments -- and runs helper `mode` on it with
+ * (a, b, len) = args[4i .. 4i+2], HE_OUT int32 results per lane */
+__global__ __launch_bounds__(WAVE) void k_helpers_eval(int mode, const int16_t *src, const int32_t *args,
+						       int32_t *out, int n)
+{
+	int i = blockIdx.x * WAVE + threadIdx.x;
+	if (i >= n)
+		return;
+	struct {
+		uint8_t guard[FLAT_GUARD_BYTES];
+		int16_t buf[HE_N];
+		int32_t o[HE_OUT];
+	} L;
+	PIN_FRAME(L);
+	for (int k = 0; k < HE_N; k++)
+		L.buf[k] = src[(size_t) i * HE_N + k];
+	for (int k = 0; k < HE_OUT; k++)
+		L.o[k] = 0;
+	he_eval(mode, L.buf, args[4 * i], args[4 * i + 1], args[4 * i + 2], L.o);
+	for (int k = 0; k < HE_OUT; k++)
+		out[(size_t) i * HE_OUT + k] = L.o[k];
 }
 
 /* ------------------------------------------------------------------ */
@@ -1400,6 +1426,19 @@ int melpe_ops_eval_dev(int op, const void *d_a, const void *d_b, const void *d_c
 	k_ops_eval<<<(unsigned) ((n + 255) / 256), 256, 0, (hipStream_t) hip_stream>>>(
 		op, (const int64_t *) d_a, (const int32_t *) d_b, (const int32_t *) d_c,
 		(int64_t *) d_out, n);
+	HIPCHK(hipGetLastError());
+	return 0;
+}
+
+int melpe_helpers_eval_dev(int mode, const void *d_src, const void *d_args, void *d_out, int n,
+			   void *hip_stream)
+{
+	if (!d_src || !d_args || !d_out || n < 0 || mode < 0 || mode > 8)
+		return fail_msg("melpe_helpers_eval_dev: bad arguments");
+	if (n == 0)
+		return 0;
+	k_helpers_eval<<<grid_for(n), WAVE, 0, (hipStream_t) hip_stream>>>(
+		mode, (const int16_t *) d_src, (const int32_t *) d_args, (int32_t *) d_out, n);
 	HIPCHK(hipGetLastError());
 	return 0;
 }

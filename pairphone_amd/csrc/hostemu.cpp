@@ -15,6 +15,7 @@
 
 #include "codec.h"
 #include "ana_mw.h"
+#include "helpers_eval.h"
 #include "codec2400.h"
 #include "voice_crypt.h"
 #include "vad.h"
@@ -156,6 +157,20 @@ int emu_encode_ana_mw(emu_engine *e, unsigned char *bits, const int16_t *sp, int
 			}
 		for (int k = 0; k < 11; k++)
 			bits[c * 11 + k] = rec.chbuf[k];
+	}
+	return 0;
+}
+
+/* host build of the helper self-test (helpers_eval.h), same layout as
+ * melpe_helpers_eval_dev */
+int emu_helpers_eval(int mode, const int16_t *src, const int32_t *args, int32_t *out, int n)
+{
+	for (int i = 0; i < n; i++) {
+		alignas(4) int16_t buf[HE_N];
+		memcpy(buf, src + (size_t) i * HE_N, sizeof buf);
+		int32_t *o = out + (size_t) i * HE_OUT;
+		memset(o, 0, sizeof(int32_t) * HE_OUT);
+		he_eval(mode, buf, args[4 * i], args[4 * i + 1], args[4 * i + 2], o);
 	}
 	return 0;
 }
