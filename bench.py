@@ -349,16 +349,21 @@ def encode_leg(rig, wl, K, W):
 def tx_leg(rig, args, rank, world):
     """BASELINE config 5: the TX front end (tx.c:232-246: VAD gate, then
     melpe_a on the superframes it opens) on ragged streams, per-channel
-    lengths uniform in [1 s, 20 s] (seeded), channels of this rank only.
-    One step = one superframe of every channel whose stream is still
-    running; the job is done when the longest stream ends.  Whole-job
-    throughput = channel-seconds of all streams / wall time."""
+    lengths uniform in [1 s, 20 s] (seeded), world x --tx-channels streams
+    in all.  Ranks own contiguous ranges balanced by total superframes
+    (shard.superframe_range), so a rank's step count follows its longest
+    stream.  One step = one superframe of every channel whose stream is
+    still running; the job is done when the longest stream ends.  Whole-job
+    throughput = channel-seconds of all streams / wall time (max over
+    ranks)."""
     import torch
     from pairphone_amd import MelpeEngine
-    C = args.tx_channels
-    lo = rank * C
+    from pairphone_amd.shard import superframe_range
     g = np.random.default_rng(RUN_SEED + 5)
-    lengths = g.integers(15, 297, size=world * C)[lo:lo + C]     # 1 s .. 20 s
+    lengths_all = g.integers(15, 297, size=world * args.tx_channels)     # 1 s .. 20 s
+    lo, hi = superframe_range(rank, world, lengths_all)
+    lengths = lengths_all[lo:hi]
+    C = hi - lo
     nsf = int(lengths.max())
     eng = MelpeEngine(C, device=rig.dev.index)
     lib = eng.lib
@@ -377,20 +382,22 @@ def tx_leg(rig, args, rank, world):
     rig.sync()
 
     def step(s):
-        eng.tx_dev(vst.data_ptr(), bits[s].data_ptr(), pcm[s].data_ptr(), votes[s].data_ptr(),
-                   gate[s].data_ptr(), act[s].data_ptr(), rig.sptr)
-    dt, (kms,) = timed(rig, [step], nsf, 0)
-    chs = float(lengths.sum()) * SF_SECONDS
-    tot = torch.tensor([chs], dtype=torch.float64, device=rig.dev)
-    if world > 1:
-        rig.dist.all_reduce(tot)
-    res = {"workload": "config 5: %d channels per GPU, ragged lengths uniform in [1 s, 20 s] "
-                       "(seed %d), VAD2 gate + melpe_a on the opened superframes" % (C, RUN_SEED + 5),
-           "value": float(tot.item()) / dt, "unit": "channel-s/s (whole streams)",
-           "wall_s": dt, "steps": nsf, "mean_step_ms": kms,
-           "channel_seconds": float(tot.item()),
+        if s < nsf:
+            eng.tx_dev(vst.data_ptr(), bits[s].data_ptr(), pcm[s].data_ptr(), votes[s].data_ptr(),
+                       gate[s].data_ptr(), act[s].data_ptr(), rig.sptr)
+    # every rank runs the job's step count (its own streams may end sooner)
+    steps = int(rig.max_over_ranks(float(nsf)))
+    dt, (kms,) = timed(rig, [step], steps, 0)
+    chs = float(lengths_all.sum()) * SF_SECONDS
+    res = {"workload": "config 5: %d streams (%d per GPU on average), ragged lengths uniform in "
+                       "[1 s, 20 s] (seed %d), VAD2 gate + melpe_a on the opened superframes"
+                       % (len(lengths_all), args.tx_channels, RUN_SEED + 5),
+           "value": chs / dt, "unit": "channel-s/s (whole streams)",
+           "wall_s": dt, "steps": steps, "mean_step_ms": kms,
+           "channel_seconds": chs,
            "gated_open_fraction": float(gate.float().sum().item() / act.float().sum().item()),
-           "sharding": "contiguous channel ranges per rank"}
+           "sharding": "shard.superframe_range: contiguous channel ranges balanced by total "
+                       "superframes (rank 0: channels %d..%d)" % (lo, hi - 1)}
     eng.close()
     return res
 

@@ -61,8 +61,11 @@ def gather_bitstreams(bits, channels_total):
     if bits.shape[1] != mine[1] - mine[0]:
         raise ValueError("local shard has %d channels, expected %d"
                          % (bits.shape[1], mine[1] - mine[0]))
-    pad = torch.zeros((steps, width, SF_BYTES), dtype=torch.uint8, device=bits.device)
-    pad[:, :bits.shape[1]] = bits
+    # RCCL gathers device tensors over xGMI; gloo (CPU ranks, or ranks that
+    # share one GPU in the tests) gathers host tensors
+    on = bits.device if dist.get_backend() != "gloo" else torch.device("cpu")
+    pad = torch.zeros((steps, width, SF_BYTES), dtype=torch.uint8, device=on)
+    pad[:, :bits.shape[1]] = bits.to(on)
     parts = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(parts, pad)
-    return torch.cat([p[:, :hi - lo] for p, (lo, hi) in zip(parts, sizes)], dim=1)
+    return torch.cat([p[:, :hi - lo] for p, (lo, hi) in zip(parts, sizes)], dim=1).to(bits.device)

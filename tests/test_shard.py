@@ -185,3 +185,69 @@ def test_bench_run_world2_gloo():
     want = torch.stack([((g[:, None] * 31 + s * 7 + torch.arange(11)) % 251).to(torch.uint8)
                         for s in range(1, 4)]).numpy()
     assert allbits.shape == (3, 10, 11) and (allbits == want).all()
+
+
+def _gpu_bench_worker(rank, world, port, C, q):
+    """one rank of bench.run with the real engine; every rank on GPU 0 (the
+    one-GPU box), collectives over gloo"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    import pairphone_amd.shard as shard
+
+    class SharedGpuRig(bench.GpuRig):
+        def __init__(self, local, world):
+            super().__init__(0, world)
+
+        def max_over_ranks(self, x):
+            t = torch.tensor([x], dtype=torch.float64)
+            if self.world > 1:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+    got = {}
+    real = shard.gather_bitstreams
+
+    def spy(bits, total):
+        out = real(bits, total)
+        got["all"] = out.cpu().clone()
+        return out
+    shard.gather_bitstreams = spy
+    args = bench.parse(["--gpus", str(world), "--steps", "3", "--warmup", "1", "--channels", str(C),
+                        "--total-channels", "0", "--tx-channels", "0", "--no-side-legs",
+                        "--no-cpu-baseline", "--no-decode"])
+    line = bench.run(args, rank, world, rank, backend="gloo", rig_cls=SharedGpuRig)
+    if rank == 0:
+        q.put((line, got["all"].numpy().copy()))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _spawn_bench(world, C):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_bench_worker, args=(r, world, port, C, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    line, allbits = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return line, allbits
+
+
+@pytest.mark.gpu
+def test_bench_run_world2_real_engine():
+    """bench.run on two processes with the real engine (one engine per
+    process, both on GPU 0 of the box, gloo in place of RCCL): the line
+    counts both ranks, and the gathered bitstreams of 2 x 2,048 channels are
+    the bits a one-rank run of the same 4,096 channels produces."""
+    line2, bits2 = _spawn_bench(2, 2048)
+    line1, bits1 = _spawn_bench(1, 4096)
+    assert line2["n_gpus"] == 2 and line2["config"]["channels_total"] == 4096
+    assert line2["bitstream_gather"]["collective"] == "all_gather"
+    assert bits2.shape == bits1.shape == (3, 4096, 11)
+    assert (bits2 == bits1).all()
+    assert bits1.any()
