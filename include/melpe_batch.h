@@ -27,10 +27,13 @@
  * All functions return 0 on success and a negative code on error;
  * melpe_last_error() describes the last error of the calling thread.
  *
- * Ordering: the *_dev calls are ordered by their stream only.  The *_host
- * calls, melpe_engine_reset and the state export/import synchronise the
- * device first, so they run after every *_dev call already enqueued on any
- * stream.  To reset channels in stream order (no host sync), use
+ * Ordering: the *_dev calls are ordered by their stream only; two *_dev
+ * calls of one engine on different streams may run concurrently when their
+ * active masks are disjoint (the engine orders its own shared scratch).  The
+ * *_host calls, melpe_engine_reset and the state export/import first wait
+ * for every *_dev call of the same engine already enqueued, on any stream
+ * (the engine records an event on each stream it is given), and for nothing
+ * else on the device.  To reset channels in stream order (no host sync), use
  * melpe_engine_reset_dev on the stream that carries the encode/decode work.
  * Entry points restore the calling thread's current HIP device on return.
  */
@@ -84,7 +87,9 @@ int melpe_engine_set_ana_waves(melpe_engine *e, int waves);
  * (count * bytes), import writes them back into any engine of the same
  * library build.  A record is opaque and carries a channel's complete codec
  * state: continuing an imported channel gives the bits / PCM the exporting
- * engine would have produced. */
+ * engine would have produced.  Each record carries a format tag (layout
+ * version and size); import rejects a batch holding any record of another
+ * layout (e.g. a checkpoint of an older build) and writes nothing. */
 long melpe_engine_state_bytes(int which);
 int melpe_engine_export(melpe_engine *e, int which, int first, int count, void *host_out);
 int melpe_engine_import(melpe_engine *e, int which, int first, int count, const void *host_in);

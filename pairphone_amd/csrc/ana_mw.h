@@ -15,10 +15,15 @@
  * pitchAuto's peak pitch / correlation of the same subframe; each of those
  * crosses waves through the per-channel exchange block (LDS on the GPU),
  * in a phase after the one that produced it.  Phase 2i runs frame i's first
- * half, phase 2i+1 its bands and pitch/gain, phase 6 the last classify, and
- * phase 7 the tail on v0 after it has gathered classify's and pitchAuto's
- * tracks (through the HBM record) and the other waves' LSFs and band
- * voicings (through the exchange block).
+ * half, phase 2i+1 its bands and pitch/gain.  The tail (melp_ana.c:162-265)
+ * splits the same way where the reference's order allows it:
+ *   phase 6  v1 lsf_vq (it reads only the LSFs and voicing), v3 the last
+ *            classify, v0 gain_vq and the jitter quantiser
+ *   phase 7  v0 sc_ana, pitch_vq, quant_bp, quant_jitter, after gathering
+ *            classify's and pitchAuto's tracks (through the HBM record) and
+ *            the band voicings and quantised LSFs (exchange block)
+ *   phase 8  find_harm of frame i on v(i+1)
+ *   phase 9  v0 quant_fsmag, the channel write.
  *
  * Every chain keeps the reference's operation order on its own data, so the
  * result is bit-identical to the serial analysis() whatever the number of
@@ -34,7 +39,7 @@
 namespace mlp {
 
 #define MW_NV 4	/* virtual waves of the schedule */
-#define MW_PHASES (2 * NF + 2)
+#define MW_PHASES (2 * NF + 4)
 
 /* the per-channel exchange block, in int16 words */
 enum {
@@ -42,7 +47,13 @@ enum {
 	XS_BPVC = XS_SUBPITCH + NF,	/* [NF][NUM_BANDS] bands 1..4 (-> v0) */
 	XS_LSF = XS_BPVC + NF * NUM_BANDS,	/* [NF][LPC_ORD] (v1 -> v0) */
 	XS_CSPC = XS_LSF + NF * LPC_ORD,	/* [2 NF][2] pitchAuto's pitch, corx (v2 -> v3) */
-	XS_WORDS = XS_CSPC + 2 * NF * 2
+	XS_UV = XS_CSPC + 2 * NF * 2,	/* [NF] voicing of frame i (v0 -> v1's lsf_vq) */
+	XS_LIDX = XS_UV + NF,	/* [NF][MAX_LSF_STAGE] lsf_vq's indices (v1 -> v0) */
+	XS_QPLSP = XS_LIDX + NF * MAX_LSF_STAGE,	/* [LPC_ORD] + started flag (v1 -> v0) */
+	XS_FHP = XS_QPLSP + LPC_ORD + 1,	/* [NF] quantised pitch (v0 -> find_harm's waves) */
+	XS_FHUV = XS_FHP + NF,	/* [NF] voicing after quant_bp (ditto) */
+	XS_FSMAG = XS_FHUV + NF,	/* [NF][NUM_HARM] find_harm's magnitudes (-> v0) */
+	XS_WORDS = XS_FSMAG + NF * NUM_HARM
 };
 
 typedef int16_t __attribute__((__may_alias__)) i16_alias;
@@ -143,6 +154,7 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, AnaMwTmp &tmp, int v, in
 		} else {
 			if (v == 0) {
 				ana_pitch_gain<false>(E, speech, par, tmp.sub_pitch[i]);
+				xc.put(XS_UV + i, par->uv_flag);
 			} else if (v == 1) {
 				ana_mw_band(E, xc, i, 1);
 				ana_mw_band(E, xc, i, 2);
@@ -151,30 +163,83 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, AnaMwTmp &tmp, int v, in
 			}
 		}
 	} else if (p == 2 * NF) {
-		if (v == 2) {
+		MelpParam *par = E->par;
+		if (v == 0) {
+			gain_vq(E, par);
+			for (int i = 0; i < NF; i++)
+				quant_u(&par[i].jitter, &E->qpar.jit_index[i], 0, MAX_JITTER_Q15, 2,
+					SW_MAX_, true, 7);
+		} else if (v == 1) {
+			for (int i = 0; i < NF; i++)
+				par[i].uv_flag = xc.get(XS_UV + i);
+#if !defined(MELPE_KO_LSFVQ)
+			lsf_vq(E, par);
+#endif
+			for (int i = 0; i < NF; i++) {
+				for (int k = 0; k < LPC_ORD; k++)
+					xc.put(XS_LSF + i * LPC_ORD + k, par[i].lsf[k]);
+				for (int k = 0; k < MAX_LSF_STAGE; k++)
+					xc.put(XS_LIDX + i * MAX_LSF_STAGE + k, E->qpar.lsf_index[i][k]);
+			}
+			for (int k = 0; k < LPC_ORD; k++)
+				xc.put(XS_QPLSP + k, E->qplsp[k]);
+			xc.put(XS_QPLSP + LPC_ORD, E->lsf_started);
+		} else if (v == 2) {
 			lane_copy16(rec->pitTrack, E->pitTrack, sizeof(E->pitTrack));
-		} else if (v == 3) {
+		} else {
 			ana_mw_classify(E, xc, NF - 1);
 			lane_copy16(rec->classStat, E->classStat, sizeof(E->classStat));
 			rec->voicedEn = E->voicedEn;
 			rec->silenceEn = E->silenceEn;
 			rec->voicedCnt = E->voicedCnt;
 		}
-	} else if (v == 0) {
+	} else if (p == 2 * NF + 1) {
+		if (v != 0)
+			return;
+		MelpParam *par = E->par;
 		lane_copy16(E->pitTrack, rec->pitTrack, sizeof(E->pitTrack));
 		lane_copy16(E->classStat, rec->classStat, sizeof(E->classStat));
 		E->voicedEn = rec->voicedEn;
 		E->silenceEn = rec->silenceEn;
 		E->voicedCnt = rec->voicedCnt;
 		for (int i = 0; i < NF; i++) {
-			MelpParam *par = &E->par[i];
-			for (int k = 0; k < LPC_ORD; k++)
-				par->lsf[k] = xc.get(XS_LSF + i * LPC_ORD + k);
 			for (int k = 1; k < NUM_BANDS; k++)
-				par->bpvc[k] = xc.get(XS_BPVC + i * NUM_BANDS + k);
-			ana_peaky(par->bpvc, tmp.peak[i], 1, 2);
+				par[i].bpvc[k] = xc.get(XS_BPVC + i * NUM_BANDS + k);
+			ana_peaky(par[i].bpvc, tmp.peak[i], 1, 2);
+			for (int k = 0; k < LPC_ORD; k++)
+				par[i].lsf[k] = xc.get(XS_LSF + i * LPC_ORD + k);
+			for (int k = 0; k < MAX_LSF_STAGE; k++)
+				E->qpar.lsf_index[i][k] = xc.get(XS_LIDX + i * MAX_LSF_STAGE + k);
 		}
-		analysis_tail(E);
+		for (int k = 0; k < LPC_ORD; k++)
+			E->qplsp[k] = xc.get(XS_QPLSP + k);
+		E->lsf_started = xc.get(XS_QPLSP + LPC_ORD);
+		/* analysis_tail's order without lsf_vq / gain_vq / quant_u (done) */
+		sc_ana(E, par);
+		pitch_vq(E, par);
+		quant_bp(E, par);
+		quant_jitter(E, par);
+		for (int i = 0; i < NF; i++) {
+			xc.put(XS_FHP + i, par[i].pitch);
+			xc.put(XS_FHUV + i, par[i].uv_flag);
+		}
+	} else if (p == 2 * NF + 2) {
+		if (v == 0)
+			return;
+		const int i = v - 1;
+		MelpParam *par = &E->par[i];
+		for (int k = 0; k < LPC_ORD; k++)
+			par->lsf[k] = xc.get(XS_LSF + i * LPC_ORD + k);
+		par->pitch = xc.get(XS_FHP + i);
+		par->uv_flag = xc.get(XS_FHUV + i);
+		ana_fsmag_frame(E, par, i);
+		for (int k = 0; k < NUM_HARM; k++)
+			xc.put(XS_FSMAG + i * NUM_HARM + k, par->fs_mag[k]);
+	} else if (v == 0) {
+		for (int i = 0; i < NF; i++)
+			for (int k = 0; k < NUM_HARM; k++)
+				E->par[i].fs_mag[k] = xc.get(XS_FSMAG + i * NUM_HARM + k);
+		ana_pack(E);
 	}
 }
 

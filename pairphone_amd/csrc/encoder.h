@@ -433,12 +433,39 @@ MD void analysis_frame(EncState *E, const int16_t *sp_in, int i)
 	melp_ana<false>(E, &E->hpspeech[i * FRAME], &E->par[i], i);
 }
 
+/* the Fourier magnitudes of frame i (melp_ana.c:224-236): the LPC residual
+ * of the quantised LSFs, windowed, through find_harm; 8192s when unvoiced */
+MN void ana_fsmag_frame(EncState *E, MelpParam *par, int i)
+{
+	int16_t lpc[LPC_ORD + 1];
+	lpc[0] = 4096;
+	v_set(par->fs_mag, 8192, NUM_HARM);
+	if (!par->uv_flag) {
+		lpc_lsp2pred(par->lsf, &lpc[1], LPC_ORD);
+		zerflt(&E->hpspeech[i * FRAME + FRAME_END - LPC_FRAME / 2], lpc, E->sigbuf, LPC_ORD,
+		       LPC_FRAME);
+		window(E->sigbuf, TB(win_cof), E->sigbuf, LPC_FRAME);
+#if !defined(MELPE_KO_HARM)
+		find_harm(E->sigbuf, par->fs_mag, par->pitch, NUM_HARM, LPC_FRAME);
+#endif
+	}
+}
+
+/* quant_fsmag, the channel write and the history shift (melp_ana.c:238-265) */
+MN void ana_pack(EncState *E)
+{
+	MelpParam *par = E->par;
+	quant_fsmag(E, par);
+	for (int i = 0; i < NF; i++)
+		E->qpar.uv_flag[i] = par[i].uv_flag;
+	low_rate_chn_write(E);
+	v_copy(E->hpspeech, &E->hpspeech[NF * FRAME], IN_BEG);
+}
+
 MN void analysis_tail(EncState *E)
 {
 	MelpParam *par = E->par;
-	int16_t lpc[LPC_ORD + 1];
 	sc_ana(E, par);
-	lpc[0] = 4096;
 #if !defined(MELPE_KO_LSFVQ)
 	lsf_vq(E, par);
 #endif
@@ -449,23 +476,9 @@ MN void analysis_tail(EncState *E)
 			true, 7);
 	quant_bp(E, par);
 	quant_jitter(E, par);
-	for (int i = 0; i < NF; i++) {
-		v_set(par[i].fs_mag, 8192, NUM_HARM);
-		if (!par[i].uv_flag) {
-			lpc_lsp2pred(par[i].lsf, &lpc[1], LPC_ORD);
-			zerflt(&E->hpspeech[i * FRAME + FRAME_END - LPC_FRAME / 2], lpc, E->sigbuf,
-			       LPC_ORD, LPC_FRAME);
-			window(E->sigbuf, TB(win_cof), E->sigbuf, LPC_FRAME);
-#if !defined(MELPE_KO_HARM)
-			find_harm(E->sigbuf, par[i].fs_mag, par[i].pitch, NUM_HARM, LPC_FRAME);
-#endif
-		}
-	}
-	quant_fsmag(E, par);
 	for (int i = 0; i < NF; i++)
-		E->qpar.uv_flag[i] = par[i].uv_flag;
-	low_rate_chn_write(E);
-	v_copy(E->hpspeech, &E->hpspeech[NF * FRAME], IN_BEG);
+		ana_fsmag_frame(E, &par[i], i);
+	ana_pack(E);
 }
 
 MN void analysis(EncState *E, const int16_t *sp_in)

@@ -20,6 +20,7 @@
 #include <stdint.h>
 #include <string>
 #include <mutex>
+#include <vector>
 
 #include "kern.h"
 #define SYN_FN __host__ __device__ static inline
@@ -609,6 +610,10 @@ struct melpe_engine {
 	BinBuf bin_enc, bin_dec;	/* pitch-class lane order of k_enc_ana / k_decode */
 	int lane_order = -1;	/* 1 on, 0 off, -1 the MELPE_BIN default */
 	int ana_waves = 0;	/* waves per 64 channels in k_enc_ana(_mw); 0: by channel count */
+	/* one event per stream this engine's *_dev calls have used, recorded
+	 * after each call: the host-side calls wait on these (engine_wait)
+	 * instead of the whole device */
+	std::vector<std::pair<hipStream_t, hipEvent_t>> marks;
 	size_t npp_bytes = 0;
 	float last_ms = 0.f;
 };
@@ -713,6 +718,33 @@ static void ev_end(melpe_engine *e, hipStream_t s, bool sync)
 	}
 }
 
+/* after enqueueing this engine's work on stream s */
+static int engine_mark(melpe_engine *e, hipStream_t s)
+{
+	for (auto &m : e->marks)
+		if (m.first == s) {
+			HIPCHK(hipEventRecord(m.second, s));
+			return 0;
+		}
+	hipEvent_t ev;
+	HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+	e->marks.emplace_back(s, ev);
+	HIPCHK(hipEventRecord(ev, s));
+	return 0;
+}
+
+/* the host waits for every call of this engine already enqueued, on any
+ * stream (not for other engines or unrelated work on the device) */
+static int engine_wait(melpe_engine *e)
+{
+	for (auto &m : e->marks)
+		HIPCHK(hipEventSynchronize(m.second));
+	HIPCHK(hipStreamSynchronize(e->stream));
+	return 0;
+}
+#define ENGINE_WAIT(e) do { if (int _r = engine_wait(e)) return _r; } while (0)
+#define ENGINE_MARK(e, s) do { if (int _r = engine_mark(e, s)) return _r; } while (0)
+
 extern "C" {
 
 const char *melpe_last_error(void)
@@ -798,6 +830,8 @@ int melpe_engine_destroy(melpe_engine *e)
 	hipFree(e->d_mask);
 	hipFree(e->bin_enc.perm);
 	hipFree(e->bin_dec.perm);
+	for (auto &m : e->marks)
+		hipEventDestroy(m.second);
 	if (e->bin_enc.done)
 		hipEventDestroy(e->bin_enc.done);
 	if (e->bin_dec.done)
@@ -837,6 +871,7 @@ int melpe_engine_reset_dev(melpe_engine *e, const void *d_mask, int which, void 
 	k_reset<<<grid_for(e->channels), WAVE, 0, (hipStream_t) hip_stream>>>(
 		e->d_enc, e->d_dec, (const uint8_t *) d_mask, e->channels, which);
 	HIPCHK(hipGetLastError());
+	ENGINE_MARK(e, (hipStream_t) hip_stream);
 	return 0;
 }
 
@@ -845,9 +880,9 @@ int melpe_engine_reset(melpe_engine *e, const uint8_t *mask_host, int which)
 	if (!e || which < 1 || which > 3)
 		return fail_msg("melpe_engine_reset: bad arguments");
 	DEVGUARD(e->device);
-	/* ordered after every *_dev call already enqueued on any stream of the
-	 * device: those read and write the same channel records */
-	HIPCHK(hipDeviceSynchronize());
+	/* ordered after every *_dev call of this engine already enqueued, on
+	 * any stream: those read and write the same channel records */
+	ENGINE_WAIT(e);
 	int rc;
 	const uint8_t *m = stage_mask(e, mask_host, &rc);
 	if (rc)
@@ -868,6 +903,7 @@ static int npp_launch(melpe_engine *e, int16_t *d_sp, int frames, int stride,
 	ev_begin(e, s);
 	HIPCHK((hipError_t) kl_npp(e->d_enc, d_sp, frames, stride, d_act, e->channels, rate1200, s));
 	ev_end(e, s, sync);
+	ENGINE_MARK(e, s);
 	return 0;
 }
 
@@ -885,7 +921,7 @@ int melpe_npp_host(melpe_engine *e, int16_t *sp, int frames, int stride, const u
 	if (!e || !sp || stride <= 0)
 		return fail_msg("melpe_npp_host: bad arguments");
 	DEVGUARD(e->device);
-	HIPCHK(hipDeviceSynchronize());
+	ENGINE_WAIT(e);
 	size_t bytes = sizeof(int16_t) * (size_t) stride * e->channels;
 	if (e->npp_bytes < bytes) {
 		HIPCHK(hipFree(e->d_npp));
@@ -919,6 +955,7 @@ static int encode_launch(melpe_engine *e, unsigned char *d_bits, int16_t *d_sp,
 	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, d_sp, d_act, e->channels, s));
 	HIPCHK((hipError_t) ana_launch(e, d_sp, d_bits, d_act, s));
 	ev_end(e, s, sync);
+	ENGINE_MARK(e, s);
 	return 0;
 }
 
@@ -938,6 +975,7 @@ int melpe_encode_npp_dev(melpe_engine *e, void *d_sp, const void *d_active, void
 	DEVGUARD(e->device);
 	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, (int16_t *) d_sp, (const uint8_t *) d_active,
 				       e->channels, (hipStream_t) hip_stream));
+	ENGINE_MARK(e, (hipStream_t) hip_stream);
 	return 0;
 }
 
@@ -949,6 +987,7 @@ int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const 
 	DEVGUARD(e->device);
 	HIPCHK((hipError_t) ana_launch(e, (const int16_t *) d_sp, (uint8_t *) d_bits,
 				       (const uint8_t *) d_active, (hipStream_t) hip_stream));
+	ENGINE_MARK(e, (hipStream_t) hip_stream);
 	return 0;
 }
 
@@ -957,7 +996,7 @@ int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const u
 	if (!e || !bits || !sp)
 		return fail_msg("melpe_encode_host: null argument");
 	DEVGUARD(e->device);
-	HIPCHK(hipDeviceSynchronize());
+	ENGINE_WAIT(e);
 	size_t pb = sizeof(int16_t) * BLOCK * (size_t) e->channels;
 	size_t bb = (size_t) 11 * e->channels;
 	int rc;
@@ -983,6 +1022,7 @@ static int decode_launch(melpe_engine *e, int16_t *d_sp, const unsigned char *d_
 	ev_begin(e, s);
 	HIPCHK((hipError_t) dec_launch(e, d_sp, d_bits, d_act, s));
 	ev_end(e, s, sync);
+	ENGINE_MARK(e, s);
 	return 0;
 }
 
@@ -1001,7 +1041,7 @@ int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
 	if (!e || !bits || !sp)
 		return fail_msg("melpe_decode_host: null argument");
 	DEVGUARD(e->device);
-	HIPCHK(hipDeviceSynchronize());
+	ENGINE_WAIT(e);
 	size_t pb = sizeof(int16_t) * BLOCK * (size_t) e->channels;
 	size_t bb = (size_t) 11 * e->channels;
 	int rc;
@@ -1030,6 +1070,7 @@ static int encode24_launch(melpe_engine *e, unsigned char *d_bits, int16_t *d_sp
 	HIPCHK((hipError_t) kl_npp(e->d_enc, d_sp, 1, MELPE_FRAME_SAMPLES, d_act, e->channels, 0, s));
 	HIPCHK((hipError_t) kl_enc24(e->d_enc, d_sp, d_bits, d_act, e->channels, s));
 	ev_end(e, s, sync);
+	ENGINE_MARK(e, s);
 	return 0;
 }
 
@@ -1053,6 +1094,7 @@ int melpe_decode2400_dev(melpe_engine *e, void *d_sp, const void *d_bits, const 
 	HIPCHK((hipError_t) kl_dec24(e->d_dec, (int16_t *) d_sp, (const uint8_t *) d_bits,
 				     (const uint8_t *) d_active, e->channels, s));
 	ev_end(e, s, false);
+	ENGINE_MARK(e, s);
 	return 0;
 }
 
@@ -1061,7 +1103,7 @@ int melpe_encode2400_host(melpe_engine *e, unsigned char *bits, int16_t *sp, con
 	if (!e || !bits || !sp)
 		return fail_msg("melpe_encode2400_host: null argument");
 	DEVGUARD(e->device);
-	HIPCHK(hipDeviceSynchronize());
+	ENGINE_WAIT(e);
 	size_t pb = sizeof(int16_t) * MELPE_FRAME_SAMPLES * (size_t) e->channels;
 	size_t bb = (size_t) MELPE_R24_BYTES * e->channels;
 	int rc;
@@ -1086,7 +1128,7 @@ int melpe_decode2400_host(melpe_engine *e, int16_t *sp, const unsigned char *bit
 	if (!e || !bits || !sp)
 		return fail_msg("melpe_decode2400_host: null argument");
 	DEVGUARD(e->device);
-	HIPCHK(hipDeviceSynchronize());
+	ENGINE_WAIT(e);
 	size_t pb = sizeof(int16_t) * MELPE_FRAME_SAMPLES * (size_t) e->channels;
 	size_t bb = (size_t) MELPE_R24_BYTES * e->channels;
 	int rc;
@@ -1128,7 +1170,7 @@ int melpe_engine_export(melpe_engine *e, int which, int first, int count, void *
 	if (!host_out && count)
 		return fail_msg("melpe_engine_export: null buffer");
 	DEVGUARD(e->device);
-	HIPCHK(hipDeviceSynchronize());
+	ENGINE_WAIT(e);
 	HIPCHK(hipMemcpy(host_out, base + rec * first, rec * count, hipMemcpyDeviceToHost));
 	return 0;
 }
@@ -1141,8 +1183,17 @@ int melpe_engine_import(melpe_engine *e, int which, int first, int count, const 
 		return r;
 	if (!host_in && count)
 		return fail_msg("melpe_engine_import: null buffer");
+	const uint32_t want = which == 1 ? ENC_REC_FMT : DEC_REC_FMT;
+	const size_t tag = which == 1 ? offsetof(EncState, fmt) : offsetof(DecState, fmt);
+	for (int k = 0; k < count; k++) {
+		uint32_t f;
+		memcpy(&f, (const char *) host_in + rec * k + tag, sizeof f);
+		if (f != want)
+			return fail_msg("melpe_engine_import: record " + std::to_string(k) +
+					" is not a state record of this library's layout");
+	}
 	DEVGUARD(e->device);
-	HIPCHK(hipDeviceSynchronize());
+	ENGINE_WAIT(e);
 	HIPCHK(hipMemcpy(base + rec * first, host_in, rec * count, hipMemcpyHostToDevice));
 	return 0;
 }
@@ -1167,6 +1218,7 @@ int melpe_synth_dev(melpe_engine *e, void *d_sp, int samples, void *hip_stream)
 	k_synth<<<grid_for(e->channels), WAVE, 0, (hipStream_t) hip_stream>>>(
 		e->d_syn, (int16_t *) d_sp, samples, e->channels);
 	HIPCHK(hipGetLastError());
+	ENGINE_MARK(e, (hipStream_t) hip_stream);
 	return 0;
 }
 

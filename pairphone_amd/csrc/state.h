@@ -158,6 +158,9 @@ struct EncState {
 	ClsState cls;
 	PautoState pa;
 	BandState band[NUM_BANDS];	/* band[0] belongs to the driver group */
+	/* record format tag (reset sets it, no kernel writes it):
+	 * melpe_engine_import rejects records of another layout */
+	uint32_t fmt;
 };
 
 #define MIX_ORD 32
@@ -191,7 +194,14 @@ struct DecState {
 	uint32_t seed;
 	/* 2400 bps path: melpe/melp_sub.c q_gain_dec prev_gain, prev_gain_err */
 	int16_t qgd_prev_gain, qgd_prev_err;
+	uint32_t fmt;	/* record format tag, as EncState's */
 };
+
+/* Layout version of the records (bump on any change to EncState /
+ * DecState); the tag also folds in the record size. */
+#define MELPE_REC_LAYOUT 3u
+#define ENC_REC_FMT (0x4d450000u ^ (MELPE_REC_LAYOUT << 24) ^ (uint32_t) sizeof(EncState))
+#define DEC_REC_FMT (0x4d440000u ^ (MELPE_REC_LAYOUT << 24) ^ (uint32_t) sizeof(DecState))
 
 /* melp_ana_init, melpe/melp_ana.c:475-506 (the part melpe_i re-runs) */
 MD void enc_melpe_i(EncState *e)
@@ -226,6 +236,7 @@ MD void enc_reset(EncState *e)
 	e->pvq_prev_qpitch = LOG_UV_PITCH_Q12;
 	e->fsm_prev_uv = 1;	/* qnt12.c:1279 */
 	enc_melpe_i(e);
+	e->fmt = ENC_REC_FMT;
 }
 
 /* melp_syn_init, melpe/melp_syn.c:478-502 (the part melpe_i re-runs) */
@@ -258,6 +269,7 @@ MD void dec_reset(DecState *d)
 	d->rd_prev_uv = 1;	/* melp_chn.c:460 */
 	d->seed = 1;	/* dsp_sub.c:369 */
 	dec_melpe_i(d);
+	d->fmt = DEC_REC_FMT;
 }
 
 }  // namespace mlp

@@ -90,3 +90,20 @@ def test_reset_dev_is_stream_ordered():
     np.testing.assert_array_equal(b[nsf, 1], b[0, 1])
     np.testing.assert_array_equal(b[nsf, [0, 2, 3]], 0)   # masked off: untouched
     eng.close()
+
+
+@pytest.mark.gpu
+def test_import_rejects_foreign_records():
+    """a record of another layout (here: a corrupted format tag, as a
+    checkpoint of an older build would carry) is refused, nothing written"""
+    from pairphone_amd import MelpeEngine
+    a = MelpeEngine(2)
+    rec = a.export_state(1)
+    before = rec.copy()
+    bad = rec.copy()
+    bad[1, -4:] ^= 0x5a
+    with pytest.raises(RuntimeError, match="layout"):
+        a.import_state(1, bad)
+    np.testing.assert_array_equal(a.export_state(1), before)
+    a.import_state(1, rec)    # its own records go back in
+    a.close()
