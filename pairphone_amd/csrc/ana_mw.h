@@ -10,26 +10,28 @@
  *       -> pitch_ana -> gains -> pitch average            (the driver chain)
  *   v1  LPC -> LSFs (lpc_pred2lsp is the costly part); bands 1, 2
  *   v2  pitchAuto of both subframes (corPeak over 127 lags); band 3
- *   v3  classify of both subframes, one frame behind pitchAuto; band 4
- * Bands 1..4 need band 0's pitch of the same frame, classify needs
- * pitchAuto's peak pitch / correlation of the same subframe; each of those
- * crosses waves through the per-channel exchange block (LDS on the GPU),
- * in a phase after the one that produced it.  Phase 2i runs frame i's first
- * half, phase 2i+1 its bands and pitch/gain.  The tail (melp_ana.c:162-265)
- * splits the same way where the reference's order allows it:
- *   phase 6  v1 lsf_vq (it reads only the LSFs and voicing), v3 the last
- *            classify, v0 gain_vq and the jitter quantiser
- *   phase 7  v0 sc_ana, pitch_vq, quant_bp, quant_jitter, after gathering
- *            classify's and pitchAuto's tracks (through the HBM record) and
- *            the band voicings and quantised LSFs (exchange block)
- *   phase 8  find_harm of frame i on v(i+1)
- *   phase 9  v0 quant_fsmag, the channel write.
+ *   v3  classify of both subframes; band 4
+ * Bands 1..4 of a frame need band 0's pitch of that frame and classify
+ * needs pitchAuto's peak pitch / correlation of its subframe, so they run
+ * one phase behind: phase i (i < NF) is frame i's driver chain, LPC and
+ * pitchAuto beside frame i-1's bands and classify.  Values cross waves
+ * through the per-channel exchange block (LDS on the GPU), in a phase after
+ * the one that produced them.  The tail (melp_ana.c:162-265) splits the
+ * same way where the reference's order allows it:
+ *   phase NF    v0 lsf_vq (it reads only the LSFs and voicing), v1..v3
+ *               frame NF-1's bands and classify, v2 gain_vq + the jitter
+ *               quantiser
+ *   phase NF+1  v0 sc_ana, pitch_vq, quant_bp, quant_jitter, after gathering
+ *               classify's and pitchAuto's tracks (through the HBM record)
+ *               and the band voicings and gains (exchange block)
+ *   phase NF+2  find_harm of frame i on v(i+1)
+ *   phase NF+3  v0 quant_fsmag, the channel write.
  *
  * Every chain keeps the reference's operation order on its own data, so the
  * result is bit-identical to the serial analysis() whatever the number of
  * physical waves NW: virtual wave v runs on physical wave v % NW, and the
  * virtual waves that share a physical wave share its copy of the state
- * (their write sets are disjoint).  NW = 1 is the serial order itself.
+ * (their write sets are disjoint).  NW = 1 is a serial order itself.
  */
 #ifndef MELPE_ANA_MW_H
 #define MELPE_ANA_MW_H
@@ -39,7 +41,7 @@
 namespace mlp {
 
 #define MW_NV 4	/* virtual waves of the schedule */
-#define MW_PHASES (2 * NF + 4)
+#define MW_PHASES (NF + 4)
 
 /* the per-channel exchange block, in int16 words */
 enum {
@@ -53,7 +55,10 @@ enum {
 	XS_FHP = XS_QPLSP + LPC_ORD + 1,	/* [NF] quantised pitch (v0 -> find_harm's waves) */
 	XS_FHUV = XS_FHP + NF,	/* [NF] voicing after quant_bp (ditto) */
 	XS_FSMAG = XS_FHUV + NF,	/* [NF][NUM_HARM] find_harm's magnitudes (-> v0) */
-	XS_WORDS = XS_FSMAG + NF * NUM_HARM
+	XS_GAIN = XS_FSMAG + NF * NUM_HARM,	/* [NF][NUM_GAINFR] gains (v0 -> v2 -> v0) */
+	XS_JIT = XS_GAIN + NF * NUM_GAINFR,	/* [NF] jitter (v0 -> v2 -> v0) */
+	XS_GJIDX = XS_JIT + NF,	/* gain_index[0], jit_index[NF] (v2 -> v0) */
+	XS_WORDS = XS_GJIDX + 1 + NF
 };
 
 typedef int16_t __attribute__((__may_alias__)) i16_alias;
@@ -67,9 +72,18 @@ MD void lane_copy16(void *dst, const void *src, size_t bytes)
 		d[i] = s[i];
 }
 
+/* dword copy (offsets and sizes multiples of 4) */
+MD void lane_copy32(void *dst, const void *src, size_t bytes)
+{
+	u32_alias *d = (u32_alias *) dst;
+	const u32_alias *s = (const u32_alias *) src;
+#pragma unroll 8
+	for (size_t i = 0; i < bytes / 4; i++)
+		d[i] = s[i];
+}
+
 /* what v0 keeps from a frame's first phase for its second and the tail */
 struct AnaMwTmp {
-	int16_t sub_pitch[NF];
 	int16_t peak[NF];
 };
 
@@ -113,87 +127,96 @@ MD void ana_mw_classify(EncState *E, X &xc, int i)
 }
 
 /* virtual wave v's work in phase p; rec is the channel's HBM record, which
- * carries classify's and pitchAuto's tracks to v0 between phases 6 and 7 */
+ * carries classify's and pitchAuto's tracks to v0 before phase NF+1 */
 template <class X>
 MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, AnaMwTmp &tmp, int v, int p)
 {
-	if (p < 2 * NF) {
-		const int i = p >> 1;
+	if (p < NF) {
+		const int i = p;
 		const int16_t *speech = &E->hpspeech[i * FRAME];
 		MelpParam *par = &E->par[i];
-		if ((p & 1) == 0) {
-			if (v == 0) {
-				int16_t ac[17], lpc[LPC_ORD + 1];
-				Word16 sp;
-				ana_first(E);
-				ana_global_pitch(E, speech);
-				bpvc_init(E);
-				bpvc_band0(E, &speech[FRAME_END], E->fpitch, &par->bpvc[0], &sp);
-				par->jitter = (par->bpvc[0] < VJIT_Q14) ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;
-				ana_lpc<false>(E, speech, ac, lpc, nullptr);
-				Word16 t = ana_resid(E, speech, lpc);
-				ana_peaky(par->bpvc, t, 0, 0);
-				tmp.sub_pitch[i] = sp;
-				tmp.peak[i] = t;
-				xc.put(XS_SUBPITCH + i, sp);
-			} else if (v == 1) {
-				int16_t ac[17], lpc[LPC_ORD + 1];
-				ana_lpc<false>(E, speech, ac, lpc, par->lsf);
-				for (int k = 0; k < LPC_ORD; k++)
-					xc.put(XS_LSF + i * LPC_ORD + k, par->lsf[k]);
-			} else if (v == 2) {
-				for (int s = 0; s < PIT_SUBNUM; s++) {
-					ana_track_pa(E, speech, i, s);
-					const ClassParam *cs = &E->classStat[CUR_TRACK + i * PIT_SUBNUM + s + 1];
-					xc.put(XS_CSPC + 2 * (i * PIT_SUBNUM + s), cs->pitch);
-					xc.put(XS_CSPC + 2 * (i * PIT_SUBNUM + s) + 1, cs->corx);
-				}
-			} else if (i > 0) {
-				ana_mw_classify(E, xc, i - 1);
+		if (v == 0) {
+			int16_t ac[17], lpc[LPC_ORD + 1];
+			Word16 sp;
+			ana_first(E);
+			ana_global_pitch(E, speech);
+			bpvc_init(E);
+			bpvc_band0(E, &speech[FRAME_END], E->fpitch, &par->bpvc[0], &sp);
+			par->jitter = (par->bpvc[0] < VJIT_Q14) ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;
+			ana_lpc<false>(E, speech, ac, lpc, nullptr);
+			Word16 t = ana_resid(E, speech, lpc);
+			ana_peaky(par->bpvc, t, 0, 0);
+			tmp.peak[i] = t;
+			xc.put(XS_SUBPITCH + i, sp);
+			ana_pitch_gain<false>(E, speech, par, sp);
+			xc.put(XS_UV + i, par->uv_flag);
+			for (int k = 0; k < NUM_GAINFR; k++)
+				xc.put(XS_GAIN + i * NUM_GAINFR + k, par->gain[k]);
+			xc.put(XS_JIT + i, par->jitter);
+		} else if (v == 1) {
+			int16_t ac[17], lpc[LPC_ORD + 1];
+			ana_lpc<false>(E, speech, ac, lpc, par->lsf);
+			for (int k = 0; k < LPC_ORD; k++)
+				xc.put(XS_LSF + i * LPC_ORD + k, par->lsf[k]);
+			if (i > 0) {
+				ana_mw_band(E, xc, i - 1, 1);
+				ana_mw_band(E, xc, i - 1, 2);
 			}
-		} else {
-			if (v == 0) {
-				ana_pitch_gain<false>(E, speech, par, tmp.sub_pitch[i]);
-				xc.put(XS_UV + i, par->uv_flag);
-			} else if (v == 1) {
-				ana_mw_band(E, xc, i, 1);
-				ana_mw_band(E, xc, i, 2);
-			} else {
-				ana_mw_band(E, xc, i, v + 1);
+		} else if (v == 2) {
+			for (int s = 0; s < PIT_SUBNUM; s++) {
+				ana_track_pa(E, speech, i, s);
+				const ClassParam *cs = &E->classStat[CUR_TRACK + i * PIT_SUBNUM + s + 1];
+				xc.put(XS_CSPC + 2 * (i * PIT_SUBNUM + s), cs->pitch);
+				xc.put(XS_CSPC + 2 * (i * PIT_SUBNUM + s) + 1, cs->corx);
 			}
+			if (i > 0)
+				ana_mw_band(E, xc, i - 1, 3);
+		} else if (i > 0) {
+			ana_mw_classify(E, xc, i - 1);
+			ana_mw_band(E, xc, i - 1, 4);
 		}
-	} else if (p == 2 * NF) {
+	} else if (p == NF) {
 		MelpParam *par = E->par;
 		if (v == 0) {
+			for (int i = 0; i < NF; i++)
+				for (int k = 0; k < LPC_ORD; k++)
+					par[i].lsf[k] = xc.get(XS_LSF + i * LPC_ORD + k);
+#if !defined(MELPE_KO_LSFVQ)
+			lsf_vq(E, par);
+#endif
+		} else if (v == 1) {
+			ana_mw_band(E, xc, NF - 1, 1);
+			ana_mw_band(E, xc, NF - 1, 2);
+		} else if (v == 2) {
+			ana_mw_band(E, xc, NF - 1, 3);
+			lane_copy16(rec->pitTrack, E->pitTrack, sizeof(E->pitTrack));
+			/* gain_vq and the jitter quantiser read only the gains and
+			 * jitters (melp_ana.c:168-170) */
+			for (int i = 0; i < NF; i++) {
+				for (int k = 0; k < NUM_GAINFR; k++)
+					par[i].gain[k] = xc.get(XS_GAIN + i * NUM_GAINFR + k);
+				par[i].jitter = xc.get(XS_JIT + i);
+			}
 			gain_vq(E, par);
 			for (int i = 0; i < NF; i++)
 				quant_u(&par[i].jitter, &E->qpar.jit_index[i], 0, MAX_JITTER_Q15, 2,
 					SW_MAX_, true, 7);
-		} else if (v == 1) {
-			for (int i = 0; i < NF; i++)
-				par[i].uv_flag = xc.get(XS_UV + i);
-#if !defined(MELPE_KO_LSFVQ)
-			lsf_vq(E, par);
-#endif
 			for (int i = 0; i < NF; i++) {
-				for (int k = 0; k < LPC_ORD; k++)
-					xc.put(XS_LSF + i * LPC_ORD + k, par[i].lsf[k]);
-				for (int k = 0; k < MAX_LSF_STAGE; k++)
-					xc.put(XS_LIDX + i * MAX_LSF_STAGE + k, E->qpar.lsf_index[i][k]);
+				for (int k = 0; k < NUM_GAINFR; k++)
+					xc.put(XS_GAIN + i * NUM_GAINFR + k, par[i].gain[k]);
+				xc.put(XS_JIT + i, par[i].jitter);
+				xc.put(XS_GJIDX + 1 + i, E->qpar.jit_index[i]);
 			}
-			for (int k = 0; k < LPC_ORD; k++)
-				xc.put(XS_QPLSP + k, E->qplsp[k]);
-			xc.put(XS_QPLSP + LPC_ORD, E->lsf_started);
-		} else if (v == 2) {
-			lane_copy16(rec->pitTrack, E->pitTrack, sizeof(E->pitTrack));
+			xc.put(XS_GJIDX, E->qpar.gain_index[0]);
 		} else {
 			ana_mw_classify(E, xc, NF - 1);
+			ana_mw_band(E, xc, NF - 1, 4);
 			lane_copy16(rec->classStat, E->classStat, sizeof(E->classStat));
 			rec->voicedEn = E->voicedEn;
 			rec->silenceEn = E->silenceEn;
 			rec->voicedCnt = E->voicedCnt;
 		}
-	} else if (p == 2 * NF + 1) {
+	} else if (p == NF + 1) {
 		if (v != 0)
 			return;
 		MelpParam *par = E->par;
@@ -206,24 +229,24 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, AnaMwTmp &tmp, int v, in
 			for (int k = 1; k < NUM_BANDS; k++)
 				par[i].bpvc[k] = xc.get(XS_BPVC + i * NUM_BANDS + k);
 			ana_peaky(par[i].bpvc, tmp.peak[i], 1, 2);
-			for (int k = 0; k < LPC_ORD; k++)
-				par[i].lsf[k] = xc.get(XS_LSF + i * LPC_ORD + k);
-			for (int k = 0; k < MAX_LSF_STAGE; k++)
-				E->qpar.lsf_index[i][k] = xc.get(XS_LIDX + i * MAX_LSF_STAGE + k);
+			for (int k = 0; k < NUM_GAINFR; k++)
+				par[i].gain[k] = xc.get(XS_GAIN + i * NUM_GAINFR + k);
+			par[i].jitter = xc.get(XS_JIT + i);
+			E->qpar.jit_index[i] = xc.get(XS_GJIDX + 1 + i);
 		}
-		for (int k = 0; k < LPC_ORD; k++)
-			E->qplsp[k] = xc.get(XS_QPLSP + k);
-		E->lsf_started = xc.get(XS_QPLSP + LPC_ORD);
+		E->qpar.gain_index[0] = xc.get(XS_GJIDX);
 		/* analysis_tail's order without lsf_vq / gain_vq / quant_u (done) */
 		sc_ana(E, par);
 		pitch_vq(E, par);
 		quant_bp(E, par);
 		quant_jitter(E, par);
 		for (int i = 0; i < NF; i++) {
+			for (int k = 0; k < LPC_ORD; k++)
+				xc.put(XS_LSF + i * LPC_ORD + k, par[i].lsf[k]);
 			xc.put(XS_FHP + i, par[i].pitch);
 			xc.put(XS_FHUV + i, par[i].uv_flag);
 		}
-	} else if (p == 2 * NF + 2) {
+	} else if (p == NF + 2) {
 		if (v == 0)
 			return;
 		const int i = v - 1;
@@ -240,6 +263,46 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, AnaMwTmp &tmp, int v, in
 			for (int k = 0; k < NUM_HARM; k++)
 				E->par[i].fs_mag[k] = xc.get(XS_FSMAG + i * NUM_HARM + k);
 		ana_pack(E);
+	}
+}
+
+/* Physical wave w's private copy of the record, before any phase: wave 0
+ * takes the driver group and band 0 whole; every other virtual wave on any
+ * wave only what its chains read -- the speech history and dc memories (it
+ * runs dc_rmv itself), the parameters, the tracks and trackers (pitchAuto /
+ * classify fill them, sc_ana's shift is wave 0's), lsf_vq's memory -- plus
+ * its own group.  Nothing else of the copy is read before it is written;
+ * the host build (emu_encode_ana_mw) fills the rest of each copy with a
+ * pattern to check exactly that. */
+MD void ana_mw_copy_in(EncState *E, const EncState *rec, int w, int nw)
+{
+	auto cp32 = [&](size_t off, size_t len) {
+		lane_copy32((char *) E + off, (const char *) rec + off, len);
+	};
+	auto cp16 = [&](size_t off, size_t len) {
+		lane_copy16((char *) E + off, (const char *) rec + off, len);
+	};
+	const size_t bs = sizeof(BandState), band0 = offsetof(EncState, band);
+	if (w == 0) {
+		cp32(offsetof(EncState, hpspeech), offsetof(EncState, cls) - offsetof(EncState, hpspeech));
+		cp32(band0, bs);
+	} else {
+		cp32(offsetof(EncState, hpspeech), sizeof(int16_t) * IN_BEG);
+		cp32(offsetof(EncState, dcdelin), offsetof(EncState, sigbuf) - offsetof(EncState, dcdelin));
+		cp16(offsetof(EncState, classStat), offsetof(EncState, ana_started) - offsetof(EncState, classStat));
+		cp16(offsetof(EncState, bp_started), sizeof(int16_t));
+		cp16(offsetof(EncState, lsf_started), sizeof(int16_t) * (1 + LPC_ORD));
+	}
+	for (int v = w; v < MW_NV; v += nw) {
+		if (v == 1)
+			cp32(band0 + bs, 2 * bs);
+		else if (v == 2) {
+			cp32(offsetof(EncState, pa), sizeof(PautoState));
+			cp32(band0 + 3 * bs, bs);
+		} else if (v == 3) {
+			cp32(offsetof(EncState, cls), sizeof(ClsState));
+			cp32(band0 + 4 * bs, bs);
+		}
 	}
 }
 

@@ -1132,6 +1132,11 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 		else
 			v_add(cur_n, bpc + i * (MIX_ORD + 1), MIX_ORD + 1);
 	}
+	/* pre[0 .. DISP_ORD): the dispersion history; then the frame's periods
+	 * from syn_begin on, before dispersion (at most FRAME + PITCHMAX) */
+	int16_t pre[DISP_ORD + FRAME + PITCHMAX];
+	const Word16 sb_start = D->syn_begin;
+	v_copy(pre, D->disp_del, DISP_ORD);
 	while (D->syn_begin < FRAME) {
 		Word16 sb0 = D->syn_begin;
 		Word16 ifact = divide_s(sb0, FRAME);
@@ -1208,23 +1213,29 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 		lpc_syn(&sb[BEGIN], &sb[BEGIN], &lpc[1], LPC_ORD, len);
 		v_copy(D->lpc_del, &sb[len + BEGIN - LPC_ORD], LPC_ORD);
 		scale_adj(D, &sb[BEGIN], gain, len, 10, 26214);
-		v_copy(&sb[BEGIN - DISP_ORD], D->disp_del, DISP_ORD);
-		v_copy(D->disp_del, &sb[len + BEGIN - DISP_ORD], DISP_ORD);
-		zerflt_Q(&sb[BEGIN], TB(disp_cof), &sb[BEGIN], DISP_ORD, len, 15);
-		if (add(sb0, len) >= FRAME) {
-			/* the reference postfilters the frame here (melp_syn.c:
-			 * 448); that is always the loop's last period and
-			 * nothing below reads out[] or the postfilter state, so
-			 * the call moves after the loop -- where every lane of
-			 * the wave makes it together, instead of once per period
-			 * count the wave's channels end their frames on */
-			v_copy(&out[sb0], &sb[BEGIN], FRAME - sb0);
-			v_copy(D->sigsave, &sb[BEGIN + FRAME - sb0], len - (FRAME - sb0));
-		} else {
-			v_copy(&out[sb0], &sb[BEGIN], len);
-		}
+		/* the period's pre-dispersion samples join the frame's run */
+		v_copy(&pre[DISP_ORD + sb0 - sb_start], &sb[BEGIN], len);
 		D->syn_begin = add(sb0, len);
 	}
+	/* The dispersion FIR (melp_syn.c:436-440) runs per period on the period
+	 * with the previous period's last DISP_ORD pre-dispersion samples as its
+	 * history (disp_del, also when a period is shorter than that): the same
+	 * FIR over the frame's periods end to end.  It runs here once over the
+	 * whole run, every lane of the wave together, instead of once per
+	 * period count the wave's channels take; each output sample's L_mac
+	 * chain is the reference's.  The run's part past FRAME is the next
+	 * frame's start (sigsave). */
+	{
+		const int total = D->syn_begin - sb_start;
+		v_copy(D->disp_del, &pre[total], DISP_ORD);
+		zerflt_Q(&pre[DISP_ORD], TB(disp_cof), &pre[DISP_ORD], DISP_ORD, total, 15);
+		v_copy(&out[sb_start], &pre[DISP_ORD], FRAME - sb_start);
+		v_copy(D->sigsave, &pre[DISP_ORD + FRAME - sb_start], total - (FRAME - sb_start));
+	}
+	/* the reference postfilters the frame inside the loop, in its last
+	 * period (melp_syn.c:448); nothing after it in the loop reads out[] or
+	 * the postfilter state, so the call follows the loop -- where every
+	 * lane of the wave makes it together */
 	postfilt(D, out, prev->lsf, par->lsf);
 	v_copy(D->prev_pcof, cur_p, MIX_ORD + 1);
 	v_copy(D->prev_ncof, cur_n, MIX_ORD + 1);

@@ -1245,15 +1245,15 @@ int melpe_debug_encode_stage(melpe_engine *e, void *d_sp, int upto)
 
 int melpe_prof_read(uint64_t *out, int n)
 {
-	uint64_t acc[64] = {0};
+	uint64_t acc[128] = {0};
 	int (*rd[])(uint64_t *) = {melpe_tu_eng_prof, melpe_tu_npp_prof, melpe_tu_ana_prof,
 				   melpe_tu_dec_prof, melpe_tu_r24_prof};
 	for (auto f : rd)
 		if (f(acc))
 			return fail_msg("not a profiling build (-DMELPE_PROF)");
-	for (int i = 0; i < n && i < 64; i++)
+	for (int i = 0; i < n && i < 128; i++)
 		out[i] = acc[i];
-	return 64;
+	return 128;
 }
 
 double melpe_last_kernel_ms(const melpe_engine *ce)

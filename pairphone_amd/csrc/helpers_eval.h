@@ -21,8 +21,9 @@
  *   5  xcorr_pairs<11, FcLags11, true>     (frac_cor's eleven lags)
  *   6  xcorr_pairs<12, FpLags<12>, false>  (find_pitch's +-5 pass)
  *   7  fp_sums9                            (frac_pch's nine sums)
- *   8  sdot2 / sdot2_sat / pair_mid / pk_hi8 / pk_lo8 / perm_b32 of the
- *      dwords at buf + a, buf + b (a, b even) and c = len: o[0..5]
+ *   8  sdot2 / sdot2_sat / pair_mid / pk_hi8 / pk_lo8 / perm_b32 (byte
+ *      selects 0..7, as the codec uses it) of the dwords at buf + a,
+ *      buf + b (a, b even) and c = len: o[0..5]
  */
 #ifndef MELPE_HELPERS_EVAL_H
 #define MELPE_HELPERS_EVAL_H
@@ -112,7 +113,7 @@ MD void he_eval(int mode, const int16_t *buf, int a, int b, int len, int32_t *o)
 		o[2] = (int32_t) pair_mid(x, y);
 		o[3] = (int32_t) pk_hi8(x);
 		o[4] = (int32_t) pk_lo8(x);
-		o[5] = (int32_t) perm_b32(x, y, (uint32_t) len);
+		o[5] = (int32_t) perm_b32(x, y, (uint32_t) len & 0x07070707u);	/* byte selects only */
 		break;
 	}
 	}

@@ -141,7 +141,8 @@ int emu_encode_ana_mw(emu_engine *e, unsigned char *bits, const int16_t *sp, int
 		memset(&xc, 0x5a, sizeof xc);	/* nothing may read a slot before it is written */
 		AnaMwTmp tmp[MW_NV];
 		for (int w = 0; w < nw; w++) {
-			W[w] = rec;
+			memset(&W[w], 0xa5 + w, sizeof(EncState));	/* uncopied bytes: a pattern */
+			ana_mw_copy_in(&W[w], &rec, w, nw);
 			ana_mw_begin(&W[w], x);
 		}
 		for (int p = 0; p < MW_PHASES; p++)

@@ -51,6 +51,24 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
  * (engine.hip ana_waves): at 32,768 channels lane-per-channel is 512 waves
  * for 1,024 SIMDs.
  */
+/* phase timers of the profiling build (tools/mw_prof.py): wave-cycles of
+ * virtual wave v in phase p at slot 64 + 5p + v, the phase's wall time seen
+ * by wave 0 (barrier included) at 64 + 5p + 4; copy-in / write-back after */
+#define MW_SLOT(p, v) (64 + 5 * (p) + (v))
+#if defined(MELPE_PROF)
+#define MW_T0(t) unsigned long long t = __builtin_amdgcn_s_memtime()
+#define MW_T1(t, slot)                                                          \
+	do {                                                                    \
+		unsigned long long _d = __builtin_amdgcn_s_memtime() - (t);     \
+		if (__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x) \
+			atomicAdd(&g_prof[slot], _d);                           \
+	} while (0)
+#else
+#define MW_T0(t) (void) 0
+#define MW_T1(t, slot) (void) 0
+#endif
+static_assert(MW_SLOT(MW_PHASES, 1) < 128, "MW timer slots");
+
 struct LdsXch {
 	int16_t *w;
 	int t;
@@ -84,15 +102,21 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_ENC_WAVES) void k_enc_ana_mw(EncSt
 	PIN_FRAME(L);
 	LdsXch xc{xs, t};
 	EncState *rec = &enc[c];
+	MW_T0(tb);
 	if (live) {
-		lane_copy((char *) &L.S + ENC_ANA_OFF, (const char *) rec + ENC_ANA_OFF, ENC_ANA_BYTES);
+		ana_mw_copy_in(&L.S, rec, w, NW);
 		lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
 		ana_mw_begin(&L.S, L.x);
 	}
+	MW_T1(tb, MW_SLOT(MW_PHASES, 0));
 	for (int p = 0; p < MW_PHASES; p++) {
+		MW_T0(tp);
 		if (live)
-			for (int v = w; v < MW_NV; v += NW)
+			for (int v = w; v < MW_NV; v += NW) {
+				MW_T0(tv);
 				ana_mw_phase(&L.S, rec, xc, L.tmp, v, p);
+				MW_T1(tv, MW_SLOT(p, v));
+			}
 		/* phase 2 NF hands classify's / pitchAuto's tracks to wave 0
 		 * through the record: device-scope fences around the barrier */
 		if (p == 2 * NF)
@@ -100,9 +124,12 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_ENC_WAVES) void k_enc_ana_mw(EncSt
 		__syncthreads();
 		if (p == 2 * NF)
 			__threadfence();
+		if (w == 0)
+			MW_T1(tp, MW_SLOT(p, 4));
 	}
 	if (!live)
 		return;
+	MW_T0(te);
 	for (int v = w; v < MW_NV; v += NW) {
 		size_t off[2], len[2];
 		int m = ana_mw_owned(v, off, len);
@@ -112,6 +139,7 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_ENC_WAVES) void k_enc_ana_mw(EncSt
 	if (w == 0)
 		for (int k = 0; k < 11; k++)
 			bits[(size_t) c * 11 + k] = L.S.chbuf[k];
+	MW_T1(te, MW_SLOT(MW_PHASES, 1));
 }
 
 extern "C" int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,

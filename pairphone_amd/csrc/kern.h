@@ -95,10 +95,10 @@ __device__ __forceinline__ void lane_copy(void *dst, const void *src, size_t byt
 #define MELPE_TU_PROF(name)                                                     \
 	extern "C" int melpe_tu_##name##_prof(uint64_t *acc)                    \
 	{                                                                       \
-		unsigned long long h[64];                                       \
+		unsigned long long h[MELPE_PROF_SLOTS];                         \
 		MELPE_CHK(hipDeviceSynchronize());                              \
 		MELPE_CHK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof(h))); \
-		for (int i = 0; i < 64; i++)                                    \
+		for (int i = 0; i < MELPE_PROF_SLOTS; i++)                      \
 			acc[i] += h[i];                                         \
 		memset(h, 0, sizeof(h));                                        \
 		MELPE_CHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), h, sizeof(h))); \

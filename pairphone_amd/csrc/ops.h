@@ -84,11 +84,14 @@ enum { OP_add = 0, OP_sub = 1, OP_L_sub = 3, OP_L_mult = 4, OP_extract_l = 6, OP
 #define PROF_CAT(a, b) PROF_CAT2(a, b)
 /* Stage timer (profiling build only, -DMELPE_PROF): PROF_SCOPE(k) adds the
  * wave's s_memtime ticks spent in the enclosing function to g_prof[k]
- * (inclusive of callees; first active lane records).  tools/stage_prof.py. */
+ * (inclusive of callees; first active lane records).  tools/stage_prof.py.
+ * Slots 0..63 are the named stages (prof_names.txt), 64.. the multi-wave
+ * analysis kernel's phases (ana_mw.h MW_PROF). */
 #if defined(MELPE_PROF) && defined(__HIP__)
 /* one counter block per kernel translation unit (each TU is its own code
  * object; melpe_prof_read sums them) */
-static __device__ unsigned long long g_prof[64];
+#define MELPE_PROF_SLOTS 128
+static __device__ unsigned long long g_prof[MELPE_PROF_SLOTS];
 #endif
 #if defined(MELPE_PROF) && defined(__HIP_DEVICE_COMPILE__)
 struct ProfScope {

@@ -98,7 +98,7 @@ def want(mode, src, args):
             s = ln + int(x[a]) * int(x[b]) + int(x[a + 1]) * int(x[b + 1])
             hi8 = ((int(x[a]) >> 8) & 0xffff) | ((int(x[a + 1]) >> 8) & 0xffff) << 16
             v = xb | xa << 32
-            sel = ln & 0xffffffff
+            sel = ln & 0x07070707
             perm = sum(((v >> (8 * ((sel >> (8 * k)) & 7))) & 0xff) << (8 * k) for k in range(4))
             out[i, :6] = wrap32([s, min(max(s, -2**31), 2**31 - 1), (xb >> 16) | (xa << 16) & 0xffffffff,
                                  hi8, xa & 0x00ff00ff, perm])
