@@ -73,11 +73,11 @@ int melpe_engine_reset_dev(melpe_engine *e, const void *d_mask, int which, void 
 int melpe_engine_set_lane_order(melpe_engine *e, int on);
 
 /* Waves per 64 channels of the analysis kernel: 1 = one lane per channel;
- * 2 or 4 = each channel's independent analysis chains (bandpass-voicing
- * bands, LPC/LSF, pitch tracking, classification) spread over that many
- * waves of one workgroup, for channel counts that would leave SIMDs idle;
- * 0 (default) = chosen from the channel count.  Bits are the same either
- * way. */
+ * 4 = each channel's independent analysis chains (bandpass-voicing bands,
+ * LPC/LSF, pitch tracking, classification, the LSF codebook searches)
+ * spread over four waves of one workgroup, for channel counts that would
+ * leave SIMDs idle (up to 65,536 channels per GPU); 0 (default) = chosen
+ * from the channel count.  Bits are the same either way. */
 int melpe_engine_set_ana_waves(melpe_engine *e, int waves);
 
 /* Per-channel state records, for checkpoint / resume and for moving channels
@@ -256,8 +256,9 @@ int melpe_helpers_eval_dev(int mode, const void *d_src, const void *d_args, void
 			   void *hip_stream);
 
 /* Diagnostics: per-stage wave-cycle totals of a profiling build
- * (libmelpe_amd_prof.so, -DMELPE_PROF; tools/stage_prof.py), read and
- * cleared.  Returns the number of slots, or an error in a normal build. */
+ * (libmelpe_amd_prof.so, -DMELPE_PROF; tools/stage_prof.py,
+ * tools/mw_prof.py), read and cleared.  Returns the number of slots (256),
+ * or an error in a normal build. */
 int melpe_prof_read(uint64_t *out, int n);
 
 /* Extension of the single-stream drop-in (include/melpe.h): return its one

@@ -223,8 +223,8 @@ class MelpeEngine:
 
     def set_ana_waves(self, waves):
         """waves per 64 channels of the analysis kernel: 1 lane per channel,
-        2 or 4 waves per channel group (ana_mw.h), 0 = by channel count
-        (results are the same either way)"""
+        4 waves per channel group (ana_mw.h), 0 = by channel count (results
+        are the same either way)"""
         _check(self.lib.melpe_engine_set_ana_waves(self.h, int(waves)))
 
     def reset_dev(self, d_mask=None, which=3, stream=None):

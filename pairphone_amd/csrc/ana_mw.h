@@ -18,14 +18,16 @@
  * through the per-channel exchange block (LDS on the GPU), in a phase after
  * the one that produced them.  The tail (melp_ana.c:162-265) splits the
  * same way where the reference's order allows it:
- *   phase NF    v0 lsf_vq (it reads only the LSFs and voicing), v1..v3
- *               frame NF-1's bands and classify, v2 gain_vq + the jitter
- *               quantiser
- *   phase NF+1  v0 sc_ana, pitch_vq, quant_bp, quant_jitter, after gathering
+ *   phase NF    v0 lsf_vq's prelude (it reads only the LSFs and voicing),
+ *               v1..v3 frame NF-1's bands and classify, v2 gain_vq + the
+ *               jitter quantiser
+ *   NF+1 ..     lsf_vq's searches, each step scored by all four waves and
+ *               replayed in order by v0 (lsfvq_mw.h)
+ *   MW_PH_SC    v0 sc_ana, pitch_vq, quant_bp, quant_jitter, after gathering
  *               classify's and pitchAuto's tracks (through the HBM record)
  *               and the band voicings and gains (exchange block)
- *   phase NF+2  find_harm of frame i on v(i+1)
- *   phase NF+3  v0 quant_fsmag, the channel write.
+ *   +1          find_harm of frame i on v(i+1)
+ *   +2          v0 quant_fsmag, the channel write.
  *
  * Every chain keeps the reference's operation order on its own data, so the
  * result is bit-identical to the serial analysis() whatever the number of
@@ -36,12 +38,16 @@
 #ifndef MELPE_ANA_MW_H
 #define MELPE_ANA_MW_H
 
-#include "encoder.h"
+#include "lsfvq_mw.h"
 
 namespace mlp {
 
 #define MW_NV 4	/* virtual waves of the schedule */
-#define MW_PHASES (NF + 4)
+/* frames, the lsf block's prelude, its (compute, scan) pairs, sc_ana &c.,
+ * find_harm, packing */
+#define MW_PH_LQ (NF + 1)	/* first compute phase of the lsf block */
+#define MW_PH_SC (MW_PH_LQ + 2 * LQ_SLOTS)
+#define MW_PHASES (MW_PH_SC + 3)
 
 /* the per-channel exchange block, in int16 words */
 enum {
@@ -58,7 +64,8 @@ enum {
 	XS_GAIN = XS_FSMAG + NF * NUM_HARM,	/* [NF][NUM_GAINFR] gains (v0 -> v2 -> v0) */
 	XS_JIT = XS_GAIN + NF * NUM_GAINFR,	/* [NF] jitter (v0 -> v2 -> v0) */
 	XS_GJIDX = XS_JIT + NF,	/* gain_index[0], jit_index[NF] (v2 -> v0) */
-	XS_WORDS = XS_GJIDX + 1 + NF
+	XS_LQ = XS_GJIDX + 1 + NF,	/* the lsf block's words (lsfvq_mw.h XL_*) */
+	XS_WORDS = XS_LQ + XL_WORDS
 };
 
 typedef int16_t __attribute__((__may_alias__)) i16_alias;
@@ -85,6 +92,7 @@ MD void lane_copy32(void *dst, const void *src, size_t bytes)
 /* what v0 keeps from a frame's first phase for its second and the tail */
 struct AnaMwTmp {
 	int16_t peak[NF];
+	LsfLead lq;	/* lsf_vq's leader state (virtual wave 0) */
 };
 
 /* the part of each physical wave's private copy that differs from the HBM
@@ -128,8 +136,8 @@ MD void ana_mw_classify(EncState *E, X &xc, int i)
 
 /* virtual wave v's work in phase p; rec is the channel's HBM record, which
  * carries classify's and pitchAuto's tracks to v0 before phase NF+1 */
-template <class X>
-MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, AnaMwTmp &tmp, int v, int p)
+template <class X, class D>
+MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, D &db, AnaMwTmp &tmp, int v, int p)
 {
 	if (p < NF) {
 		const int i = p;
@@ -181,9 +189,8 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, AnaMwTmp &tmp, int v, in
 			for (int i = 0; i < NF; i++)
 				for (int k = 0; k < LPC_ORD; k++)
 					par[i].lsf[k] = xc.get(XS_LSF + i * LPC_ORD + k);
-#if !defined(MELPE_KO_LSFVQ)
-			lsf_vq(E, par);
-#endif
+			lq_prelude(tmp.lq, E, par);
+			lq_publish(tmp.lq, E, par, xc, XS_LQ);
 		} else if (v == 1) {
 			ana_mw_band(E, xc, NF - 1, 1);
 			ana_mw_band(E, xc, NF - 1, 2);
@@ -216,7 +223,13 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, AnaMwTmp &tmp, int v, in
 			rec->silenceEn = E->silenceEn;
 			rec->voicedCnt = E->voicedCnt;
 		}
-	} else if (p == NF + 1) {
+	} else if (p < MW_PH_SC) {
+		/* the lsf block: (compute on every wave, scan on the leader) */
+		if (((p - MW_PH_LQ) & 1) == 0)
+			lq_compute(xc, XS_LQ, db, v);
+		else if (v == 0)
+			lq_scan(tmp.lq, E, E->par, xc, XS_LQ, db);
+	} else if (p == MW_PH_SC) {
 		if (v != 0)
 			return;
 		MelpParam *par = E->par;
@@ -246,7 +259,7 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, AnaMwTmp &tmp, int v, in
 			xc.put(XS_FHP + i, par[i].pitch);
 			xc.put(XS_FHUV + i, par[i].uv_flag);
 		}
-	} else if (p == NF + 2) {
+	} else if (p == MW_PH_SC + 1) {
 		if (v == 0)
 			return;
 		const int i = v - 1;

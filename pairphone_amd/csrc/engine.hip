@@ -69,7 +69,8 @@ int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *a
 	       const int *perm, const int *nlive,
 	       hipStream_t s);
 int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
-		  const int *perm, const int *nlive, int nw, hipStream_t s);
+		  const int *perm, const int *nlive, int nw, uint32_t *lqbuf, hipStream_t s);
+size_t kl_enc_ana_mw_lq_words(int n);
 int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto, hipStream_t s);
 int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
 	      const int *perm, const int *nlive,
@@ -610,6 +611,7 @@ struct melpe_engine {
 	BinBuf bin_enc, bin_dec;	/* pitch-class lane order of k_enc_ana / k_decode */
 	int lane_order = -1;	/* 1 on, 0 off, -1 the MELPE_BIN default */
 	int ana_waves = 0;	/* waves per 64 channels in k_enc_ana(_mw); 0: by channel count */
+	uint32_t *d_lq = nullptr;	/* k_enc_ana_mw's lsf_vq score rows, allocated on first use */
 	/* one event per stream this engine's *_dev calls have used, recorded
 	 * after each call: the host-side calls wait on these (engine_wait)
 	 * instead of the whole device */
@@ -633,10 +635,10 @@ static int ana_waves_for(melpe_engine *e)
 		env = v ? atoi(v) : -1;
 	}
 	int nw = env >= 0 ? env : e->ana_waves;
-	if (nw == 1 || nw == 2 || nw == 4)
+	if (nw == 1 || nw == 4)
 		return nw;
 	long waves = (e->channels + WAVE - 1) / WAVE;
-	return waves <= 1024 ? 4 : waves <= 2048 ? 2 : 1;
+	return waves <= 1024 ? 4 : 1;
 }
 
 static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, const uint8_t *d_act,
@@ -653,8 +655,17 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 	const int *perm = on ? b.perm : nullptr;
 	const int *nlive = on ? (const int *) (b.ctl + 2 * NBIN) : nullptr;
 	int nw = ana_waves_for(e);
+	if (nw > 1 && !e->d_lq) {
+		/* ordered after any work still reading the engine: a fresh buffer */
+		er = hipMalloc(&e->d_lq, sizeof(uint32_t) * kl_enc_ana_mw_lq_words(e->channels));
+		if (er != hipSuccess) {
+			e->d_lq = nullptr;
+			return (int) er;
+		}
+	}
 	int rc = nw == 1 ? kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, s)
-			 : kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nw, s);
+			 : kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nw,
+					 e->d_lq, s);
 	if (rc == 0 && on)
 		rc = (int) bin_release(b, s);
 	return rc;
@@ -808,8 +819,8 @@ int melpe_engine_set_lane_order(melpe_engine *e, int on)
 
 int melpe_engine_set_ana_waves(melpe_engine *e, int waves)
 {
-	if (!e || !(waves == 0 || waves == 1 || waves == 2 || waves == 4))
-		return fail_msg("melpe_engine_set_ana_waves: waves must be 0 (auto), 1, 2 or 4");
+	if (!e || !(waves == 0 || waves == 1 || waves == 4))
+		return fail_msg("melpe_engine_set_ana_waves: waves must be 0 (auto), 1 or 4");
 	e->ana_waves = waves;
 	return 0;
 }
@@ -830,6 +841,7 @@ int melpe_engine_destroy(melpe_engine *e)
 	hipFree(e->d_mask);
 	hipFree(e->bin_enc.perm);
 	hipFree(e->bin_dec.perm);
+	hipFree(e->d_lq);
 	for (auto &m : e->marks)
 		hipEventDestroy(m.second);
 	if (e->bin_enc.done)
@@ -1243,17 +1255,19 @@ int melpe_debug_encode_stage(melpe_engine *e, void *d_sp, int upto)
 	return 0;
 }
 
+#define MELPE_PROF_SLOTS_ABI 256	/* ops.h MELPE_PROF_SLOTS of the profiling build */
+
 int melpe_prof_read(uint64_t *out, int n)
 {
-	uint64_t acc[128] = {0};
+	uint64_t acc[MELPE_PROF_SLOTS_ABI] = {0};
 	int (*rd[])(uint64_t *) = {melpe_tu_eng_prof, melpe_tu_npp_prof, melpe_tu_ana_prof,
 				   melpe_tu_dec_prof, melpe_tu_r24_prof};
 	for (auto f : rd)
 		if (f(acc))
 			return fail_msg("not a profiling build (-DMELPE_PROF)");
-	for (int i = 0; i < n && i < 128; i++)
+	for (int i = 0; i < n && i < MELPE_PROF_SLOTS_ABI; i++)
 		out[i] = acc[i];
-	return 128;
+	return MELPE_PROF_SLOTS_ABI;
 }
 
 double melpe_last_kernel_ms(const melpe_engine *ce)

@@ -129,6 +129,13 @@ struct HostXch {
 	void put(int k, int16_t v) { w[k] = v; }
 };
 
+/* lsf_vq's per-channel score row (HBM on the GPU) */
+struct HostDb {
+	uint32_t v[LQ_VISITS];
+	uint32_t get(int u) const { return v[u]; }
+	void put(int u, uint32_t x) { v[u] = x; }
+};
+
 int emu_encode_ana_mw(emu_engine *e, unsigned char *bits, const int16_t *sp, int nw)
 {
 	if (nw < 1 || nw > MW_NV)
@@ -139,6 +146,8 @@ int emu_encode_ana_mw(emu_engine *e, unsigned char *bits, const int16_t *sp, int
 		const int16_t *x = sp + (size_t) c * BLOCK;
 		HostXch xc;
 		memset(&xc, 0x5a, sizeof xc);	/* nothing may read a slot before it is written */
+		static HostDb db;
+		memset(&db, 0xa5, sizeof db);
 		AnaMwTmp tmp[MW_NV];
 		for (int w = 0; w < nw; w++) {
 			memset(&W[w], 0xa5 + w, sizeof(EncState));	/* uncopied bytes: a pattern */
@@ -148,7 +157,7 @@ int emu_encode_ana_mw(emu_engine *e, unsigned char *bits, const int16_t *sp, int
 		for (int p = 0; p < MW_PHASES; p++)
 			for (int w = 0; w < nw; w++)
 				for (int v = w; v < MW_NV; v += nw)
-					ana_mw_phase(&W[w], &rec, xc, tmp[w], v, p);
+					ana_mw_phase(&W[w], &rec, xc, db, tmp[w], v, p);
 		for (int w = 0; w < nw; w++)
 			for (int v = w; v < MW_NV; v += nw) {
 				size_t off[2], len[2];

@@ -67,13 +67,22 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 #define MW_T0(t) (void) 0
 #define MW_T1(t, slot) (void) 0
 #endif
-static_assert(MW_SLOT(MW_PHASES, 1) < 128, "MW timer slots");
+static_assert(MW_SLOT(MW_PHASES, 1) < 256, "MW timer slots");
 
 struct LdsXch {
 	int16_t *w;
 	int t;
 	__device__ int16_t get(int k) const { return w[k * WAVE + t]; }
 	__device__ void put(int k, int16_t v) { w[k * WAVE + t] = v; }
+};
+
+/* lsf_vq's score rows (lsfvq_mw.h): visit u of lane `slot` at
+ * p[u * stride + slot], coalesced across the wave */
+struct GlbDb {
+	uint32_t *p;
+	size_t stride;
+	__device__ uint32_t get(int u) const { return p[(size_t) u * stride]; }
+	__device__ void put(int u, uint32_t x) const { p[(size_t) u * stride] = x; }
 };
 
 struct AnaMwLane {
@@ -86,7 +95,8 @@ struct AnaMwLane {
 template <int NW>
 __global__ __launch_bounds__(WAVE * NW, MELPE_ENC_WAVES) void k_enc_ana_mw(EncState *enc, const int16_t *sp,
 									    uint8_t *bits, const uint8_t *active,
-									    int n, const int *perm, const int *nlive)
+									    int n, const int *perm, const int *nlive,
+									    uint32_t *lqbuf)
 {
 	__shared__ int16_t xs[XS_WORDS * WAVE];
 	const int w = threadIdx.x / WAVE, t = threadIdx.x % WAVE;
@@ -101,6 +111,7 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_ENC_WAVES) void k_enc_ana_mw(EncSt
 	AnaMwLane L;
 	PIN_FRAME(L);
 	LdsXch xc{xs, t};
+	GlbDb db{lqbuf + blockIdx.x * WAVE + t, (size_t) gridDim.x * WAVE};
 	EncState *rec = &enc[c];
 	MW_T0(tb);
 	if (live) {
@@ -114,15 +125,17 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_ENC_WAVES) void k_enc_ana_mw(EncSt
 		if (live)
 			for (int v = w; v < MW_NV; v += NW) {
 				MW_T0(tv);
-				ana_mw_phase(&L.S, rec, xc, L.tmp, v, p);
+				ana_mw_phase(&L.S, rec, xc, db, L.tmp, v, p);
 				MW_T1(tv, MW_SLOT(p, v));
 			}
-		/* phase 2 NF hands classify's / pitchAuto's tracks to wave 0
-		 * through the record: device-scope fences around the barrier */
-		if (p == 2 * NF)
+		/* phase NF hands classify's / pitchAuto's tracks to wave 0
+		 * through the record: device-scope fences around the barrier
+		 * (the lsf block's score rows pass within the workgroup, which
+		 * __syncthreads orders) */
+		if (p == NF)
 			__threadfence();
 		__syncthreads();
-		if (p == 2 * NF)
+		if (p == NF)
 			__threadfence();
 		if (w == 0)
 			MW_T1(tp, MW_SLOT(p, 4));
@@ -142,13 +155,20 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_ENC_WAVES) void k_enc_ana_mw(EncSt
 	MW_T1(te, MW_SLOT(MW_PHASES, 1));
 }
 
-extern "C" int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
-			     int n, const int *perm, const int *nlive, int nw, hipStream_t s)
+/* lqbuf: LQ_VISITS x (grid_for(n) * WAVE) dwords (kl_enc_ana_mw_lq_words) */
+extern "C" size_t kl_enc_ana_mw_lq_words(int n)
 {
-	if (nw == 2)
-		k_enc_ana_mw<2><<<grid_for(n), WAVE * 2, 0, s>>>(enc, sp, bits, active, n, perm, nlive);
-	else if (nw == 4)
-		k_enc_ana_mw<4><<<grid_for(n), WAVE * 4, 0, s>>>(enc, sp, bits, active, n, perm, nlive);
+	return (size_t) LQ_VISITS * grid_for(n) * WAVE;
+}
+
+extern "C" int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
+			     int n, const int *perm, const int *nlive, int nw, uint32_t *lqbuf,
+			     hipStream_t s)
+{
+	/* 4 waves per 64 channels (2 measured no better at any channel count
+	 * and cost a third more compile time; ana_mw.h supports any count) */
+	if (nw == 4)
+		k_enc_ana_mw<4><<<grid_for(n), WAVE * 4, 0, s>>>(enc, sp, bits, active, n, perm, nlive, lqbuf);
 	else
 		return (int) hipErrorInvalidValue;
 	return (int) hipGetLastError();

@@ -90,7 +90,7 @@ enum { OP_add = 0, OP_sub = 1, OP_L_sub = 3, OP_L_mult = 4, OP_extract_l = 6, OP
 #if defined(MELPE_PROF) && defined(__HIP__)
 /* one counter block per kernel translation unit (each TU is its own code
  * object; melpe_prof_read sums them) */
-#define MELPE_PROF_SLOTS 128
+#define MELPE_PROF_SLOTS 256
 static __device__ unsigned long long g_prof[MELPE_PROF_SLOTS];
 #endif
 #if defined(MELPE_PROF) && defined(__HIP_DEVICE_COMPILE__)

@@ -15,8 +15,10 @@ os.environ.setdefault("MELPE_AMD_LIB", os.path.join(ROOT, "pairphone_amd", "libm
 
 import numpy as np  # noqa: E402
 
-PHASES = ["frame 0", "frame 1", "frame 2", "3 lsf_vq|bands2", "4 sc_ana..", "5 find_harm",
-          "6 pack"]
+LQ_SLOTS = 7
+PHASES = (["frame 0", "frame 1", "frame 2", "lsf prelude|bands2"]
+          + [n % k for k in range(LQ_SLOTS) for n in ("lsf compute %d", "lsf scan %d")]
+          + ["sc_ana..", "find_harm", "pack"])
 
 
 def main(C=32768, nsf=4):
@@ -35,13 +37,13 @@ def main(C=32768, nsf=4):
     for k in range(2):     # warm up past the first superframes
         eng.encode_dev(bits[k].data_ptr(), pcm[k].data_ptr(), None, s)
     torch.cuda.synchronize()
-    buf = np.zeros(128, np.uint64)
-    lib.melpe_prof_read(buf.ctypes.data, 128)
+    buf = np.zeros(256, np.uint64)
+    lib.melpe_prof_read(buf.ctypes.data, 256)
     for k in range(2, nsf + 2):
         eng.encode_dev(bits[k].data_ptr(), pcm[k].data_ptr(), None, s)
     torch.cuda.synchronize()
-    v = np.zeros(128, np.uint64)
-    lib.melpe_prof_read(v.ctypes.data, 128)
+    v = np.zeros(256, np.uint64)
+    lib.melpe_prof_read(v.ctypes.data, 256)
     wg = C // 64 * nsf
     nw = int(os.environ.get("MELPE_ANA_NW", "0"))
     print("k_enc_ana_mw, %d channels, MELPE_ANA_NW=%d, cycles per workgroup per superframe" % (C, nw))
