@@ -2,7 +2,10 @@
 gather (pairphone_amd/shard.py), world size 2 over gloo, plus the bench's
 max-over-ranks timing line with --gpus 2 semantics."""
 import os
+import queue
 import socket
+import sys
+import time
 
 import pytest
 import torch
@@ -171,10 +174,7 @@ def test_bench_run_world2_gloo():
     procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    line, allbits = q.get(timeout=180)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    line, allbits = _collect(procs, q, 180)
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["config"]["channels_total"] == 10
     assert abs(line["value"] - 10 * 3 * 0.0675 / (line["ms_per_step"] * 3 / 1e3)) < 1e-6 * line["value"]
@@ -224,6 +224,26 @@ def _gpu_bench_worker(rank, world, port, C, q):
         dist.destroy_process_group()
 
 
+def _collect(procs, q, limit):
+    """rank 0's result from q; fails at once (instead of waiting out the
+    limit) when a rank exits without one"""
+    t0 = time.monotonic()
+    while True:
+        try:
+            res = q.get(timeout=2)
+            break
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, "a rank exited with %s before rank 0's result" % dead
+            assert time.monotonic() - t0 < limit, "no result within %d s" % limit
+            print("[test_shard] waiting for the ranks (%.0f s)" % (time.monotonic() - t0),
+                  file=sys.stderr, flush=True)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return res
+
+
 def _spawn_bench(world, C):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -231,11 +251,7 @@ def _spawn_bench(world, C):
     procs = [ctx.Process(target=_gpu_bench_worker, args=(r, world, port, C, q)) for r in range(world)]
     for p in procs:
         p.start()
-    line, allbits = q.get(timeout=600)
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
-    return line, allbits
+    return _collect(procs, q, 240)
 
 
 @pytest.mark.gpu
