@@ -55,12 +55,12 @@ def build_oracle():
 PROF_LIB = os.path.join(ROOT, "pairphone_amd", "libmelpe_amd_prof.so")
 
 
-TUS = ("engine", "k_npp", "k_ana", "k_dec", "k_r24")
+TUS = ("engine", "k_npp", "k_ana", "k_ana_mw", "k_dec", "k_r24")
 # the codec TUs compile their whole call tree inline, so every access to a
 # lane's private state is a scratch_/global_ instruction with counted waits
 # instead of a generic FLAT access; this is what costs compile
 # time, hence one TU per kernel, compiled in parallel
-HOT_TUS = ("k_npp", "k_ana", "k_dec", "k_r24")
+HOT_TUS = ("k_npp", "k_ana", "k_ana_mw", "k_dec", "k_r24")
 
 
 def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=HOT_TUS, only=None):

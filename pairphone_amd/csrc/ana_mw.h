@@ -23,11 +23,16 @@
  *               jitter quantiser
  *   NF+1 ..     lsf_vq's searches, each step scored by all four waves and
  *               replayed in order by v0 (lsfvq_mw.h)
- *   MW_PH_SC    v0 sc_ana, pitch_vq, quant_bp, quant_jitter, after gathering
+ *   MW_PH_SC    v0 sc_ana and pitch_vq's prelude, after gathering
  *               classify's and pitchAuto's tracks (through the HBM record)
  *               and the band voicings and gains (exchange block)
- *   +1          find_harm of frame i on v(i+1)
- *   +2          v0 quant_fsmag, the channel write.
+ *   +1          pitch_vq's codebook search, a quarter per wave (pv_slice)
+ *   +2          v0 the search's replay, pitch_vq's finish, quant_bp,
+ *               quant_jitter
+ *   +3          find_harm of frame i on v(i+1)
+ *   +4          v0 quant_fsmag, the channel write.
+ * Phase 0 also runs the global-pitch chain of all three frames on v3 (it
+ * depends on nothing else), so v0 takes frames 1 and 2's from the block.
  *
  * Every chain keeps the reference's operation order on its own data, so the
  * result is bit-identical to the serial analysis() whatever the number of
@@ -47,7 +52,9 @@ namespace mlp {
  * find_harm, packing */
 #define MW_PH_LQ (NF + 1)	/* first compute phase of the lsf block */
 #define MW_PH_SC (MW_PH_LQ + 2 * LQ_SLOTS)
-#define MW_PHASES (MW_PH_SC + 3)
+#define MW_PHASES (MW_PH_SC + 5)
+#define PV_CAP 128	/* kept entries a wave stores per pitch-VQ slice (lqbuf row) */
+static_assert(MW_NV * 2 * PV_CAP <= LQ_ROW, "pitch-VQ survivors exceed the score row");
 
 /* the per-channel exchange block, in int16 words */
 enum {
@@ -64,9 +71,19 @@ enum {
 	XS_GAIN = XS_FSMAG + NF * NUM_HARM,	/* [NF][NUM_GAINFR] gains (v0 -> v2 -> v0) */
 	XS_JIT = XS_GAIN + NF * NUM_GAINFR,	/* [NF] jitter (v0 -> v2 -> v0) */
 	XS_GJIDX = XS_JIT + NF,	/* gain_index[0], jit_index[NF] (v2 -> v0) */
-	XS_LQ = XS_GJIDX + 1 + NF,	/* the lsf block's words (lsfvq_mw.h XL_*) */
-	XS_WORDS = XS_LQ + XL_WORDS
+	XS_GP = XS_GJIDX + 1 + NF,	/* [NF] global pitch fpitch[1] of frame i (v3 -> v0) */
+	XS_LPF = XS_GP + NF,	/* [2 LPF_ORD] its lowpass memories after frame NF-1 (v3 -> v0) */
+	XS_LQ = XS_LPF + 2 * LPF_ORD,	/* the lsf block's words (lsfvq_mw.h XL_*) */
+	XS_WORDS = XS_LQ + XL_WORDS,
+	/* the pitch-VQ search's words, over the lsf block's (done by then) */
+	XP_JOB = XS_LQ,	/* 1: the codebook search runs */
+	XP_CNT,	/* voiced frames (the codebook) */
+	XP_TGT,	/* [NF] */
+	XP_WT = XP_TGT + NF,	/* [NF] */
+	XP_NS = XP_WT + NF,	/* [MW_NV] entries each slice kept (-1: more than PV_CAP) */
+	XP_END = XP_NS + MW_NV
 };
+static_assert(XP_END <= XS_WORDS, "pitch-VQ words overflow the lsf block");
 
 typedef int16_t __attribute__((__may_alias__)) i16_alias;
 
@@ -75,17 +92,40 @@ MD void lane_copy16(void *dst, const void *src, size_t bytes)
 {
 	i16_alias *d = (i16_alias *) dst;
 	const i16_alias *s = (const i16_alias *) src;
-	for (size_t i = 0; i < bytes / 2; i++)
+	const int n = (int) (bytes / 2);
+	int i = 0;
+	for (; i + 32 <= n; i += 32) {	/* 32 loads in flight, as lane_copy32 */
+		int16_t v[32];
+#pragma unroll
+		for (int k = 0; k < 32; k++)
+			v[k] = s[i + k];
+#pragma unroll
+		for (int k = 0; k < 32; k++)
+			d[i + k] = v[k];
+	}
+	for (; i < n; i++)
 		d[i] = s[i];
 }
 
-/* dword copy (offsets and sizes multiples of 4) */
+/* dword copy (offsets and sizes multiples of 4), 32 loads in flight: the
+ * record reads are one channel per lane, each its own cache line, so the
+ * copy is latency-bound */
 MD void lane_copy32(void *dst, const void *src, size_t bytes)
 {
 	u32_alias *d = (u32_alias *) dst;
 	const u32_alias *s = (const u32_alias *) src;
-#pragma unroll 8
-	for (size_t i = 0; i < bytes / 4; i++)
+	const int n = (int) (bytes / 4);
+	int i = 0;
+	for (; i + 32 <= n; i += 32) {
+		uint32_t v[32];
+#pragma unroll
+		for (int k = 0; k < 32; k++)
+			v[k] = s[i + k];
+#pragma unroll
+		for (int k = 0; k < 32; k++)
+			d[i + k] = v[k];
+	}
+	for (; i < n; i++)
 		d[i] = s[i];
 }
 
@@ -93,7 +133,94 @@ MD void lane_copy32(void *dst, const void *src, size_t bytes)
 struct AnaMwTmp {
 	int16_t peak[NF];
 	LsfLead lq;	/* lsf_vq's leader state (virtual wave 0) */
+	PvqWork pv;	/* pitch_vq's prelude, for its finish two phases on */
 };
+
+/*
+ * pitch_vq's codebook search (wvq1, qnt12.c:221) split over the waves: wave
+ * v scans the v-th quarter of the codebook with its own candidate list, kept
+ * by the reference's rule, and stores the entries that list kept, in order.
+ * The reference's list holds the `cand` smallest distortions seen so far
+ * (a kept entry replaces the maximum; an equal one is rejected), so at any
+ * entry its maximum is <= the slice list's, which has seen a subset: an entry
+ * the slice rejected, the reference rejects too.  The leader then replays
+ * the stored entries of slices 0..3 in codebook order through the
+ * reference's update, which is the reference's scan with rejections skipped.
+ */
+template <class X, class D>
+MD void pv_slice(X &xc, D &db, int v)
+{
+	if (!xc.get(XP_JOB))
+		return;
+	PvqWork w;
+	w.cnt = xc.get(XP_CNT);
+	for (int j = 0; j < NF; j++) {
+		w.tgt[j] = xc.get(XP_TGT + j);
+		w.wt[j] = xc.get(XP_WT + j);
+	}
+	int size;
+	const int off = pvq_cb(w, &size);
+	for (;;) {	/* one pass per distinct codebook among the lanes */
+		const int uo = wave_first(off), un = wave_first(size);
+		if (off != uo || size != un)
+			continue;
+		const int16_t *ucb = g_tab + uo;
+		int16_t il[PITCH_VQ_CAND];
+		Word32 dl[PITCH_VQ_CAND];
+		for (int j = 0; j < PITCH_VQ_CAND; j++)
+			dl[j] = LW_MAX_;
+		Word32 maxd = LW_MAX_;
+		int maxi = 0, n = 0;
+		const int lo = v * un / MW_NV, hi = (v + 1) * un / MW_NV;
+		for (int i = lo; i < hi; i++) {
+			const Word32 err = wvq1_err<NF>(w.tgt, w.wt, ucb + i * NF, maxd);
+			if (wvq1_push(err, i, il, dl, maxd, maxi, PITCH_VQ_CAND)) {
+				if (n < PV_CAP) {
+					db.put(v * 2 * PV_CAP + 2 * n, (uint32_t) i);
+					db.put(v * 2 * PV_CAP + 2 * n + 1, (uint32_t) err);
+				}
+				n++;
+			}
+		}
+		xc.put(XP_NS + v, (int16_t) (n > PV_CAP ? -1 : n));
+		break;
+	}
+}
+
+/* the leader's replay of the slices' kept entries: wvq1's il / dl */
+template <class X, class D>
+MD void pv_replay(const PvqWork &w, X &xc, const D &db, int16_t *il, Word32 *dl)
+{
+	int size;
+	const int16_t *cb = g_tab + pvq_cb(w, &size);
+	for (int j = 0; j < PITCH_VQ_CAND; j++)
+		dl[j] = LW_MAX_;
+	Word32 maxd = LW_MAX_;
+	int maxi = 0;
+	for (int v = 0; v < MW_NV; v++) {
+		const int n = xc.get(XP_NS + v);
+		if (n < 0) {	/* more kept entries than stored: rescan the slice */
+			for (int i = v * size / MW_NV; i < (v + 1) * size / MW_NV; i++)
+				wvq1_push(wvq1_err<NF>(w.tgt, w.wt, cb + i * NF, maxd), i, il, dl, maxd,
+					  maxi, PITCH_VQ_CAND);
+			continue;
+		}
+		for (int k0 = 0; k0 < n; k0 += 8) {	/* eight entries' loads at once */
+			uint32_t ib[8], eb[8];
+#pragma unroll
+			for (int b = 0; b < 8; b++) {
+				const bool in = k0 + b < n;
+				ib[b] = in ? db.get(v * 2 * PV_CAP + 2 * (k0 + b)) : 0u;
+				eb[b] = in ? db.get(v * 2 * PV_CAP + 2 * (k0 + b) + 1) : 0u;
+			}
+#pragma unroll
+			for (int b = 0; b < 8; b++)
+				if (k0 + b < n)
+					wvq1_push((Word32) eb[b], (int) ib[b], il, dl, maxd, maxi,
+						  PITCH_VQ_CAND);
+		}
+	}
+}
 
 /* the part of each physical wave's private copy that differs from the HBM
  * record before any phase: dc removal of the three frames (melp_ana.c:
@@ -147,7 +274,12 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, D &db, AnaMwTmp &tmp, in
 			int16_t ac[17], lpc[LPC_ORD + 1];
 			Word16 sp;
 			ana_first(E);
-			ana_global_pitch(E, speech);
+			/* the global pitch of frames 1.. comes from v3, which ran the
+			 * lowpass chain ahead in phase 0 */
+			if (i == 0)
+				ana_global_pitch(E, speech);
+			else
+				E->fpitch[1] = xc.get(XS_GP + i);
 			bpvc_init(E);
 			bpvc_band0(E, &speech[FRAME_END], E->fpitch, &par->bpvc[0], &sp);
 			par->jitter = (par->bpvc[0] < VJIT_Q14) ? (int16_t) MAX_JITTER_Q15 : (int16_t) 0;
@@ -182,6 +314,24 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, D &db, AnaMwTmp &tmp, in
 		} else if (i > 0) {
 			ana_mw_classify(E, xc, i - 1);
 			ana_mw_band(E, xc, i - 1, 4);
+		} else {
+			/* the global pitch chain (lowpass memories + find_pitch) of
+			 * every frame: it reads only the speech and its own memories
+			 * (melp_ana.c:324-354), so it runs here, ahead of v0, which
+			 * repeats frame 0's itself.  It starts from the record's
+			 * memories in local copies: v0 may share this state copy
+			 * (NW < 4) and has already advanced them by frame 0. */
+			int16_t din[LPF_ORD], dout[LPF_ORD], sb[SIG_LENGTH];
+			for (int k = 0; k < LPF_ORD; k++) {
+				din[k] = rec->ana_started ? rec->lpfsp_delin[k] : (int16_t) 0;
+				dout[k] = rec->ana_started ? rec->lpfsp_delout[k] : (int16_t) 0;
+			}
+			for (int k = 0; k < NF; k++)
+				xc.put(XS_GP + k, global_pitch(&E->hpspeech[k * FRAME], sb, din, dout));
+			for (int k = 0; k < LPF_ORD; k++) {
+				xc.put(XS_LPF + k, din[k]);
+				xc.put(XS_LPF + LPF_ORD + k, dout[k]);
+			}
 		}
 	} else if (p == NF) {
 		MelpParam *par = E->par;
@@ -248,9 +398,30 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, D &db, AnaMwTmp &tmp, in
 			E->qpar.jit_index[i] = xc.get(XS_GJIDX + 1 + i);
 		}
 		E->qpar.gain_index[0] = xc.get(XS_GJIDX);
-		/* analysis_tail's order without lsf_vq / gain_vq / quant_u (done) */
+		/* analysis_tail's order without lsf_vq / gain_vq / quant_u (done);
+		 * pitch_vq's codebook search runs on every wave next phase */
 		sc_ana(E, par);
-		pitch_vq(E, par);
+		const int cnt = pvq_prelude(E, par, tmp.pv);
+		xc.put(XP_JOB, cnt >= 2);
+		if (cnt >= 2) {
+			xc.put(XP_CNT, (int16_t) cnt);
+			for (int j = 0; j < NF; j++) {
+				xc.put(XP_TGT + j, tmp.pv.tgt[j]);
+				xc.put(XP_WT + j, tmp.pv.wt[j]);
+			}
+		}
+	} else if (p == MW_PH_SC + 1) {
+		pv_slice(xc, db, v);
+	} else if (p == MW_PH_SC + 2) {
+		if (v != 0)
+			return;
+		MelpParam *par = E->par;
+		if (tmp.pv.cnt >= 2) {
+			int16_t il[PITCH_VQ_CAND];
+			Word32 dl[PITCH_VQ_CAND];
+			pv_replay(tmp.pv, xc, db, il, dl);
+			pvq_finish(E, par, tmp.pv, il, dl);
+		}
 		quant_bp(E, par);
 		quant_jitter(E, par);
 		for (int i = 0; i < NF; i++) {
@@ -259,7 +430,7 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, D &db, AnaMwTmp &tmp, in
 			xc.put(XS_FHP + i, par[i].pitch);
 			xc.put(XS_FHUV + i, par[i].uv_flag);
 		}
-	} else if (p == MW_PH_SC + 1) {
+	} else if (p == MW_PH_SC + 3) {
 		if (v == 0)
 			return;
 		const int i = v - 1;
@@ -275,6 +446,10 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, D &db, AnaMwTmp &tmp, in
 		for (int i = 0; i < NF; i++)
 			for (int k = 0; k < NUM_HARM; k++)
 				E->par[i].fs_mag[k] = xc.get(XS_FSMAG + i * NUM_HARM + k);
+		for (int k = 0; k < LPF_ORD; k++) {
+			E->lpfsp_delin[k] = xc.get(XS_LPF + k);
+			E->lpfsp_delout[k] = xc.get(XS_LPF + LPF_ORD + k);
+		}
 		ana_pack(E);
 	}
 }

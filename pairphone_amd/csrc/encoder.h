@@ -44,18 +44,21 @@ MD void ana_first(EncState *E)
 /* lowpass for the global pitch, whose filter memory advances by FRAME only,
  * then the integer pitch search (melp_ana.c:324-354) -> fpitch[1] (Q7);
  * sigbuf is this frame's scratch */
-MN void ana_global_pitch(EncState *E, const int16_t *speech)
+MN Word16 global_pitch(const int16_t *speech, int16_t *sb, int16_t *delin, int16_t *delout)
 {
-	int16_t *sb = E->sigbuf;
 	Word16 dontcare;
 	v_copy(&sb[LPF_ORD], &speech[PITCH_BEG], PITCH_FR);
-	iir3_s(&sb[LPF_ORD], TB(lpf_den), TB(lpf_num), E->lpfsp_delin, E->lpfsp_delout,
-	       PITCH_FR, FRAME);
+	iir3_s(&sb[LPF_ORD], TB(lpf_den), TB(lpf_num), delin, delout, PITCH_FR, FRAME);
 	bool ex;
 	f_pitch_scale(&sb[LPF_ORD], &sb[LPF_ORD], PITCH_FR, &ex);
-	E->fpitch[1] = find_pitch(&sb[LPF_ORD + PITCH_FR / 2], &dontcare, 2 * PITCHMIN, PITCHMAX,
-				  PITCHMAX, ex);
-	E->fpitch[1] = shl(E->fpitch[1], 7);
+	Word16 p = find_pitch(&sb[LPF_ORD + PITCH_FR / 2], &dontcare, 2 * PITCHMIN, PITCHMAX,
+			      PITCHMAX, ex);
+	return shl(p, 7);
+}
+
+MN void ana_global_pitch(EncState *E, const int16_t *speech)
+{
+	E->fpitch[1] = global_pitch(speech, E->sigbuf, E->lpfsp_delin, E->lpfsp_delout);
 }
 
 /* LPC analysis (melp_ana.c:366-393): ac[17] (the autocorrelation classify

@@ -56,11 +56,13 @@ MELPE_TU(eng)
 extern "C" {
 int melpe_tu_npp_upload(const void *blob, size_t bytes);
 int melpe_tu_ana_upload(const void *blob, size_t bytes);
+int melpe_tu_anamw_upload(const void *blob, size_t bytes);
 int melpe_tu_dec_upload(const void *blob, size_t bytes);
 int melpe_tu_r24_upload(const void *blob, size_t bytes);
 int melpe_tu_r24_prof(uint64_t *acc);
 int melpe_tu_npp_prof(uint64_t *acc);
 int melpe_tu_ana_prof(uint64_t *acc);
+int melpe_tu_anamw_prof(uint64_t *acc);
 int melpe_tu_dec_prof(uint64_t *acc);
 int kl_npp(EncState *enc, int16_t *sp, int frames, int stride, const uint8_t *active, int n,
 	   int rate1200, hipStream_t s);
@@ -637,8 +639,10 @@ static int ana_waves_for(melpe_engine *e)
 	int nw = env >= 0 ? env : e->ana_waves;
 	if (nw == 1 || nw == 4)
 		return nw;
-	long waves = (e->channels + WAVE - 1) / WAVE;
-	return waves <= 1024 ? 4 : 1;
+	/* k_enc_ana_mw holds two workgroups (of 4 waves) per CU, so it keeps
+	 * every workgroup resident up to 512 of them: 32,768 channels */
+	long groups = (e->channels + WAVE - 1) / WAVE;
+	return groups <= 512 ? 4 : 1;
 }
 
 static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, const uint8_t *d_act,
@@ -704,7 +708,7 @@ static int ensure_device_tables(int dev)
 		return fail_msg("embedded table blob has the wrong size");
 	DEVGUARD(dev);
 	int (*up[])(const void *, size_t) = {melpe_tu_eng_upload, melpe_tu_npp_upload,
-					     melpe_tu_ana_upload, melpe_tu_dec_upload,
+					     melpe_tu_ana_upload, melpe_tu_anamw_upload, melpe_tu_dec_upload,
 					     melpe_tu_r24_upload};
 	for (auto f : up)
 		if (int rc = f(melpe_tables_blob, bytes))
@@ -1260,7 +1264,7 @@ int melpe_debug_encode_stage(melpe_engine *e, void *d_sp, int upto)
 int melpe_prof_read(uint64_t *out, int n)
 {
 	uint64_t acc[MELPE_PROF_SLOTS_ABI] = {0};
-	int (*rd[])(uint64_t *) = {melpe_tu_eng_prof, melpe_tu_npp_prof, melpe_tu_ana_prof,
+	int (*rd[])(uint64_t *) = {melpe_tu_eng_prof, melpe_tu_npp_prof, melpe_tu_ana_prof, melpe_tu_anamw_prof,
 				   melpe_tu_dec_prof, melpe_tu_r24_prof};
 	for (auto f : rd)
 		if (f(acc))

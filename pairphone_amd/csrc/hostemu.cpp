@@ -131,7 +131,7 @@ struct HostXch {
 
 /* lsf_vq's per-channel score row (HBM on the GPU) */
 struct HostDb {
-	uint32_t v[LQ_VISITS];
+	uint32_t v[LQ_ROW];
 	uint32_t get(int u) const { return v[u]; }
 	void put(int u, uint32_t x) { v[u] = x; }
 };

@@ -41,7 +41,9 @@ namespace mlp {
  * separate frames take at most 4 + 1 + 1 */
 #define LQ_SLOTS 7
 #define LQ_VISITS 512	/* the most entries one stage scores */
+#define LQ_ROW 1024	/* dwords per channel of the score buffer (visits, pitch-VQ survivors) */
 #define LQ_NV 4	/* slices per step (the schedule's virtual waves) */
+#define LQ_BATCH 16	/* stored pairs read per batch by the leader's scan */
 #define LQ_PAIRS (LSP_INP_CAND * 16)	/* interpolation (candidate, pattern) pairs */
 
 /* the lsf block's exchange words (offsets from its base in the block) */
@@ -238,25 +240,36 @@ MD void lq_vq_scan(LsfLead &L, const D &db)
 		key[k] = SW_MAX_ * 65536 + (0x8000 | k);
 	Word16 maxd = SW_MAX_;
 	int c1 = 0, e = 0;
-	for (int u = 0; u < n; u++) {
-		const uint32_t pr = db.get(u);
-		const int16_t h = (int16_t) (pr & 0xffff), f = (int16_t) (pr >> 16);
-		const Word16 d = (h >= maxd) ? (Word16) SW_MAX_ : f;
-		if (d < maxd) {
-			const int32_t dk = (int32_t) d * 65536;
-			const int32_t nk = dk + ((c1 << 9) | e);
-			bool kp[LSP_VQ_CAND];
+	/* the stored pairs are read LQ_BATCH at a time, every load of a batch
+	 * issued before the first is used (one memory latency per batch instead
+	 * of one per visit); the visits themselves stay in order */
+	for (int u0 = 0; u0 < n; u0 += LQ_BATCH) {
+		uint32_t buf[LQ_BATCH];
 #pragma unroll
-			for (int k = 0; k < LSP_VQ_CAND; k++)
-				kp[k] = key[k] < dk;
+		for (int b = 0; b < LQ_BATCH; b++)
+			buf[b] = (u0 + b < n) ? db.get(u0 + b) : 0u;
 #pragma unroll
-			for (int k = LSP_VQ_CAND - 1; k >= 0; k--)
-				key[k] = kp[k] ? key[k] : ((k == 0 || kp[k > 0 ? k - 1 : 0]) ? nk : key[k > 0 ? k - 1 : 0]);
-			maxd = (Word16) (key[LSP_VQ_CAND - 1] >> 16);
-		}
-		if (++e == size) {
-			e = 0;
-			c1++;
+		for (int b = 0; b < LQ_BATCH; b++) {
+			if (u0 + b >= n)
+				break;
+			const int16_t h = (int16_t) (buf[b] & 0xffff), f = (int16_t) (buf[b] >> 16);
+			const Word16 d = (h >= maxd) ? (Word16) SW_MAX_ : f;
+			if (d < maxd) {
+				const int32_t dk = (int32_t) d * 65536;
+				const int32_t nk = dk + ((c1 << 9) | e);
+				bool kp[LSP_VQ_CAND];
+#pragma unroll
+				for (int k = 0; k < LSP_VQ_CAND; k++)
+					kp[k] = key[k] < dk;
+#pragma unroll
+				for (int k = LSP_VQ_CAND - 1; k >= 0; k--)
+					key[k] = kp[k] ? key[k] : ((k == 0 || kp[k > 0 ? k - 1 : 0]) ? nk : key[k > 0 ? k - 1 : 0]);
+				maxd = (Word16) (key[LSP_VQ_CAND - 1] >> 16);
+			}
+			if (++e == size) {
+				e = 0;
+				c1++;
+			}
 		}
 	}
 	int16_t rows[LSP_VQ_CAND][LSP_VQ_STAGES];

@@ -77,13 +77,49 @@ MD void vq_fsw(int16_t *wfs, int nh, Word16 pitch)
 /* pitch VQ, melpe/qnt12.c:75-353                                      */
 /* ------------------------------------------------------------------ */
 
+/* wvq1's distortion of codebook row `row` (:221-260): the weighted terms in
+ * j order with the reference's early exit once the sum reaches maxd.  The
+ * terms are non-negative and L_add is monotone, so an exited sum is >= maxd,
+ * like the full one: the exit never changes whether the entry is kept. */
+template <int DIM>
+MD Word32 wvq1_err(const int16_t *tgt, const int16_t *wt, const int16_t *row, Word32 maxd)
+{
+	Word32 err = 0;
+	for (int j = 0; j < DIM; j++)
+		if (wt[j] > 0) {
+			Word16 t = sub(tgt[j], row[j]);
+			err = L_add(err, L_shr(L_mult(t, t), 2));
+			if (err >= maxd)
+				break;
+		}
+	return err;
+}
+
+/* wvq1's update with entry i: it replaces the slot holding the current
+ * maximum, then the linear rescan finds the new one (first slot wins).
+ * Returns whether the entry was kept. */
+MD bool wvq1_push(Word32 err, int i, int16_t *index, Word32 *dist, Word32 &maxd, int &maxi,
+		  int cand)
+{
+	if (!(err < maxd))
+		return false;
+	index[maxi] = (int16_t) i;
+	dist[maxi] = err;
+	maxd = 0;
+	for (int j = 0; j < cand; j++)
+		if (dist[j] > maxd) {
+			maxd = dist[j];
+			maxi = j;
+		}
+	return true;
+}
+
 /* wvq1 :221 -- keeps `cand` best entries; a new entry replaces the slot
  * holding the current maximum, exactly as the reference's linear rescan */
 template <int DIM>
 MN void wvq1(const int16_t *tgt_in, const int16_t *wt_in, const int16_t *cb, int cbsize,
 	     int16_t *index, Word32 *dist, int cand)
 {
-	const int dim = DIM;
 	int16_t tgt[DIM], wt[DIM];	/* in registers for the codebook scan */
 #pragma unroll
 	for (int j = 0; j < DIM; j++) {
@@ -102,26 +138,9 @@ MN void wvq1(const int16_t *tgt_in, const int16_t *wt_in, const int16_t *cb, int
 		if (o_lane != uo || cbsize != un)
 			continue;
 		const int16_t *ucb = g_tab + uo;
-		for (int i = 0; i < un; i++) {
-			Word32 err = 0;
-			for (int j = 0; j < dim; j++)
-				if (wt[j] > 0) {
-					Word16 t = sub(tgt[j], ucb[i * DIM + j]);
-					err = L_add(err, L_shr(L_mult(t, t), 2));
-					if (err >= maxd)
-						break;
-				}
-			if (err < maxd) {
-				index[maxi] = (int16_t) i;
-				dist[maxi] = err;
-				maxd = 0;
-				for (int j = 0; j < cand; j++)
-					if (dist[j] > maxd) {
-						maxd = dist[j];
-						maxi = j;
-					}
-			}
-		}
+		for (int i = 0; i < un; i++)
+			wvq1_push(wvq1_err<DIM>(tgt, wt, ucb + i * DIM, maxd), i, index, dist, maxd, maxi,
+				  cand);
 		break;
 	}
 }
@@ -158,34 +177,46 @@ MN int16_t wvq2(const int16_t *tgt_in, const int16_t *wt_in, const int16_t *cb,
 	return ind;
 }
 
-/* pitch_vq :75 */
-MN void pitch_vq(EncState *E, MelpParam *par)
-{
-	PROF_SCOPE(10);
-	QuantParam *q = &E->qpar;
+/* pitch_vq :75, in three parts so the multi-wave kernel can spread the
+ * codebook search (ana_mw.h): the prelude (targets, weights, the
+ * differential targets and their state; the scalar-quantiser and all-unvoiced
+ * cases whole), the wvq1 search, and the finish (wvq2 and the outputs) */
+struct PvqWork {
 	int16_t tgt[NF], deltp[NF], deltw[NF], wt[NF];
-	int16_t dcb[PITCH_VQ_CAND * NF], il[PITCH_VQ_CAND];
-	Word32 dl[PITCH_VQ_CAND];
+	int16_t cnt;	/* voiced frames; the codebook search runs when >= 2 */
+};
+
+/* the codebook of the search: all voiced (2048 x 3) or two of three (512) */
+MD int pvq_cb(const PvqWork &w, int *size)
+{
+	*size = w.cnt == NF ? 2048 : 512;
+	return w.cnt == NF ? TOFF_pitch_vq_cb_vvv : TOFF_pitch_vq_cb_uvv;
+}
+
+MN int pvq_prelude(EncState *E, MelpParam *par, PvqWork &w)
+{
+	QuantParam *q = &E->qpar;
 	for (int i = 0; i < NF; i++)
-		tgt[i] = log10_fxp(par[i].pitch, 7);
+		w.tgt[i] = log10_fxp(par[i].pitch, 7);
 	int cnt = 0;
 	for (int i = 0; i < NF; i++) {
 		if (par[i].uv_flag) {
-			wt[i] = 0;
+			w.wt[i] = 0;
 		} else {
-			wt[i] = 1;
+			w.wt[i] = 1;
 			cnt++;
 		}
 	}
+	w.cnt = (int16_t) cnt;
 	for (int i = 0; i < NF; i++) {
 		if (E->pvq_prev_uv_flag || par[i].uv_flag) {
-			deltp[i] = 0;
-			deltw[i] = 0;
+			w.deltp[i] = 0;
+			w.deltw[i] = 0;
 		} else {
-			deltp[i] = sub(tgt[i], E->pvq_prev_pitch);
-			deltw[i] = 1;
+			w.deltp[i] = sub(w.tgt[i], E->pvq_prev_pitch);
+			w.deltw[i] = 1;
 		}
-		E->pvq_prev_pitch = tgt[i];
+		E->pvq_prev_pitch = w.tgt[i];
 		E->pvq_prev_uv_flag = par[i].uv_flag;
 	}
 	if (cnt == 0) {
@@ -195,7 +226,7 @@ MN void pitch_vq(EncState *E, MelpParam *par)
 	} else if (cnt == 1) {
 		for (int i = 0; i < NF; i++) {
 			if (!par[i].uv_flag) {
-				quant_u(&tgt[i], &q->pitch_index, 5329, 9028, 98, 25088, true, 7);
+				quant_u(&w.tgt[i], &q->pitch_index, 5329, 9028, 98, 25088, true, 7);
 				par[i].pitch = quant_u_dec(q->pitch_index, 5329, 9028, 25088, 7);
 			} else {
 				par[i].pitch = LOG_UV_PITCH_Q12;
@@ -204,35 +235,46 @@ MN void pitch_vq(EncState *E, MelpParam *par)
 		E->pvq_prev_qpitch = par[NF - 1].pitch;
 		for (int i = 0; i < NF; i++)
 			par[i].pitch = pow10_fxp(par[i].pitch, 7);
-	} else {
-		const int16_t *cb;
-		int size;
-		if (cnt == NF) {
-			cb = TB(pitch_vq_cb_vvv);
-			size = 2048;
-		} else {
-			cb = TB(pitch_vq_cb_uvv);
-			size = 512;
-		}
-		wvq1<NF>(tgt, wt, cb, size, il, dl, PITCH_VQ_CAND);
-		Word16 k = 0;
-		for (int i = 0; i < PITCH_VQ_CAND; i++) {
-			Word16 t2 = extract_l(L_shr(L_mult(il[i], NF), 1));
-			dcb[k] = sub(cb[t2], E->pvq_prev_qpitch);
-			v_copy(&dcb[k + 1], &cb[t2 + 1], NF - 1);
-			v_sub(&dcb[k + 1], &cb[t2], NF - 1);
-			k = add(k, NF);
-		}
-		int16_t pi = wvq2<NF>(deltp, deltw, dcb, il, dl, PITCH_VQ_CAND);
-		if (par[NF - 1].uv_flag)
-			E->pvq_prev_qpitch = LOG_UV_PITCH_Q12;
-		else
-			E->pvq_prev_qpitch = cb[pi * NF + NF - 1];
-		for (int i = 0; i < NF; i++)
-			par[i].pitch = par[i].uv_flag ? (int16_t) UV_PITCH_Q7
-						      : pow10_fxp(cb[pi * NF + i], 7);
-		q->pitch_index = pi;
 	}
+	return cnt;
+}
+
+MN void pvq_finish(EncState *E, MelpParam *par, const PvqWork &w, const int16_t *il,
+		   const Word32 *dl)
+{
+	int size;
+	const int16_t *cb = g_tab + pvq_cb(w, &size);
+	int16_t dcb[PITCH_VQ_CAND * NF];
+	Word16 k = 0;
+	for (int i = 0; i < PITCH_VQ_CAND; i++) {
+		Word16 t2 = extract_l(L_shr(L_mult(il[i], NF), 1));
+		dcb[k] = sub(cb[t2], E->pvq_prev_qpitch);
+		v_copy(&dcb[k + 1], &cb[t2 + 1], NF - 1);
+		v_sub(&dcb[k + 1], &cb[t2], NF - 1);
+		k = add(k, NF);
+	}
+	int16_t pi = wvq2<NF>(w.deltp, w.deltw, dcb, il, dl, PITCH_VQ_CAND);
+	if (par[NF - 1].uv_flag)
+		E->pvq_prev_qpitch = LOG_UV_PITCH_Q12;
+	else
+		E->pvq_prev_qpitch = cb[pi * NF + NF - 1];
+	for (int i = 0; i < NF; i++)
+		par[i].pitch = par[i].uv_flag ? (int16_t) UV_PITCH_Q7 : pow10_fxp(cb[pi * NF + i], 7);
+	E->qpar.pitch_index = pi;
+}
+
+MN void pitch_vq(EncState *E, MelpParam *par)
+{
+	PROF_SCOPE(10);
+	PvqWork w;
+	if (pvq_prelude(E, par, w) < 2)
+		return;
+	int size;
+	const int16_t *cb = g_tab + pvq_cb(w, &size);
+	int16_t il[PITCH_VQ_CAND];
+	Word32 dl[PITCH_VQ_CAND];
+	wvq1<NF>(w.tgt, w.wt, cb, size, il, dl, PITCH_VQ_CAND);
+	pvq_finish(E, par, w, il, dl);
 }
 
 /* gain_vq :368 -- 1024 x 6 full search with the reference's early skip */

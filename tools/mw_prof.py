@@ -18,7 +18,7 @@ import numpy as np  # noqa: E402
 LQ_SLOTS = 7
 PHASES = (["frame 0", "frame 1", "frame 2", "lsf prelude|bands2"]
           + [n % k for k in range(LQ_SLOTS) for n in ("lsf compute %d", "lsf scan %d")]
-          + ["sc_ana..", "find_harm", "pack"])
+          + ["sc_ana+pvq prelude", "pvq slices", "pvq finish..", "find_harm", "pack"])
 
 
 def main(C=32768, nsf=4):
