@@ -248,13 +248,16 @@ def w_over(oc, key, lo, hi):
 
 def pmc_traffic(kernel, channels):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
-    passes (profiles/pmc_latest.json, written by tools/prof_summary.py), if
-    they were taken at this channel count; else None."""
+    passes (profiles/pmc_latest.json, written by tools/prof_summary.py: one
+    set per channel count), if a set was taken at this channel count; else
+    None."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(p):
         return None, None
     d = json.load(open(p))
-    if d.get("channels") != channels:
+    sets = d.get("sets", [d])
+    d = next((x for x in sets if x.get("channels") == channels), None)
+    if d is None:
         return None, None
     k = d.get("kernels", {}).get(kernel)
     return (None if k is None else k["bytes_per_launch"]), d.get("source")

@@ -18,11 +18,11 @@
  * through the per-channel exchange block (LDS on the GPU), in a phase after
  * the one that produced them.  The tail (melp_ana.c:162-265) splits the
  * same way where the reference's order allows it:
- *   phase NF    v0 lsf_vq's prelude (it reads only the LSFs and voicing),
- *               v1..v3 frame NF-1's bands and classify, v2 gain_vq + the
- *               jitter quantiser
- *   NF+1 ..     lsf_vq's searches, each step scored by all four waves and
- *               replayed in order by v0 (lsfvq_mw.h)
+ *   phase NF    v0 lsf_vq's prelude (it reads only the LSFs and voicing)
+ *               and its first step alone, v1..v3 frame NF-1's bands and
+ *               classify, v2 gain_vq + the jitter quantiser
+ *   NF+1 ..     lsf_vq's other searches, each step scored by all four
+ *               waves and replayed in order by v0 (lsfvq_mw.h)
  *   MW_PH_SC    v0 sc_ana and pitch_vq's prelude, after gathering
  *               classify's and pitchAuto's tracks (through the HBM record)
  *               and the band voicings and gains (exchange block)
@@ -51,7 +51,9 @@ namespace mlp {
 /* frames, the lsf block's prelude, its (compute, scan) pairs, sc_ana &c.,
  * find_harm, packing */
 #define MW_PH_LQ (NF + 1)	/* first compute phase of the lsf block */
-#define MW_PH_SC (MW_PH_LQ + 2 * LQ_SLOTS)
+/* lsf_vq's first step runs on v0 in phase NF, the rest in the block */
+#define MW_LQ_PAIRS (LQ_SLOTS - 1)
+#define MW_PH_SC (MW_PH_LQ + 2 * MW_LQ_PAIRS)
 #define MW_PHASES (MW_PH_SC + 5)
 #define PV_CAP 128	/* kept entries a wave stores per pitch-VQ slice (lqbuf row) */
 static_assert(MW_NV * 2 * PV_CAP <= LQ_ROW, "pitch-VQ survivors exceed the score row");
@@ -341,6 +343,11 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, D &db, AnaMwTmp &tmp, in
 					par[i].lsf[k] = xc.get(XS_LSF + i * LPC_ORD + k);
 			lq_prelude(tmp.lq, E, par);
 			lq_publish(tmp.lq, E, par, xc, XS_LQ);
+			/* the first lspVQ stage (one candidate: 256 or 512 visits),
+			 * all four slices here -- v0 is otherwise idle in this phase */
+			for (int sl = 0; sl < LQ_NV; sl++)
+				lq_compute(xc, XS_LQ, db, sl);
+			lq_scan(tmp.lq, E, par, xc, XS_LQ, db);
 		} else if (v == 1) {
 			ana_mw_band(E, xc, NF - 1, 1);
 			ana_mw_band(E, xc, NF - 1, 2);

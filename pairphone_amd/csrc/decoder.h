@@ -690,6 +690,7 @@ MN Word16 low_rate_chn_read(DecState *D)
 #ifndef IDFT_BLK
 #define IDFT_BLK 12
 #endif
+static_assert(IDFT_BLK < PITCHMIN, "realIDFT's fast path reduces i + q mod len with one subtraction");
 
 /* realIDFT's cosine table entry i for period len (melpe/harm.c:70-80) */
 MD Word16 idft_cos_entry_w(Word16 w, int i)
@@ -765,6 +766,55 @@ MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 		mag[i] = mult(mag[i], w2);
 	else
 		mag[i] = mult(mag[i], w);
+#if !defined(MELPE_OPCOUNT)
+	/* No-clamp fast path.  Every partial sum of an output's chain is
+	 * mag[0] * 2^16 plus terms 2 mag[j] c[k] with |c| <= 2^15, so with
+	 * A = sum |mag[j]| (j = 0 .. len2-1) it stays within A * 2^16, and the
+	 * rounding adds 2^15: A <= 32766 proves neither L_mac nor r_ound can
+	 * clamp, the chain is an exact integer sum in any order, and each term
+	 * is one 24-bit multiply-add (|2 mag| < 2^17).  Decoded magnitudes are
+	 * scaled by 2/len, so this is the common case; a wave with any lane
+	 * outside it runs the saturating chain below for all of them. */
+	{
+		int A = 0;
+		for (int j = 0; j < len2; j++)
+			A += mag[j] < 0 ? -mag[j] : mag[j];
+		if (wave_all(A <= 32766)) {
+			const int m0 = (int) mag[0] * 65536 + 32768;
+			for (i = 0; i < len; i += IDFT_BLK) {
+				/* iq = (i + q) mod len (q < IDFT_BLK < PITCHMIN: one
+				 * subtraction), so every index stays in the row even for
+				 * the last block's unused outputs */
+				int Lq[IDFT_BLK], bq[IDFT_BLK], iq[IDFT_BLK];
+#pragma unroll
+				for (int q = 0; q < IDFT_BLK; q++) {
+					Lq[q] = m0;
+					bq[q] = 0;
+					iq[q] = i + q < len ? i + q : i + q - len;
+				}
+				for (int j = 1; j < len2; j++) {
+					const int m2 = 2 * (int) mag[j];
+					const int p = phm[j];
+#pragma unroll
+					for (int q = 0; q < IDFT_BLK; q++) {
+						bq[q] += iq[q];
+						if (bq[q] >= len)
+							bq[q] -= len;
+						int k = bq[q] + p;
+						if (k >= len)
+							k -= len;
+						Lq[q] += m2 * (int) c[k];
+					}
+				}
+#pragma unroll
+				for (int q = 0; q < IDFT_BLK; q++)
+					if (i + q < len)
+						sig[i + q] = (int16_t) (Lq[q] >> 16);
+			}
+			return;
+		}
+	}
+#endif
 	for (i = 0; i < len; i++) {
 		Word32 L = L_deposit_h(mag[0]);
 #if defined(MELPE_OPCOUNT)

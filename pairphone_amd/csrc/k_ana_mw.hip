@@ -20,7 +20,8 @@ MELPE_TU(anamw)
  */
 /* phase timers of the profiling build (tools/mw_prof.py): wave-cycles of
  * virtual wave v in phase p at slot 64 + 5p + v, the phase's wall time seen
- * by wave 0 (barrier included) at 64 + 5p + 4; copy-in / write-back after */
+ * by wave 0 (barrier included) at 64 + 5p + 4; copy-in / write-back / dc
+ * removal after */
 #define MW_SLOT(p, v) (64 + 5 * (p) + (v))
 #if defined(MELPE_PROF)
 #define MW_T0(t) unsigned long long t = __builtin_amdgcn_s_memtime()
@@ -34,7 +35,7 @@ MELPE_TU(anamw)
 #define MW_T0(t) (void) 0
 #define MW_T1(t, slot) (void) 0
 #endif
-static_assert(MW_SLOT(MW_PHASES, 1) < 256, "MW timer slots");
+static_assert(MW_SLOT(MW_PHASES, 2) < 256, "MW timer slots");
 
 struct LdsXch {
 	int16_t *w;
@@ -93,9 +94,12 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_MW_WAVES) void k_enc_ana_mw(EncSta
 	if (live) {
 		ana_mw_copy_in(&L.S, rec, w, NW);
 		lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
-		ana_mw_begin(&L.S, L.x);
 	}
 	MW_T1(tb, MW_SLOT(MW_PHASES, 0));
+	MW_T0(td);
+	if (live)
+		ana_mw_begin(&L.S, L.x);
+	MW_T1(td, MW_SLOT(MW_PHASES, 2));
 	for (int p = 0; p < MW_PHASES; p++) {
 		MW_T0(tp);
 		if (live)

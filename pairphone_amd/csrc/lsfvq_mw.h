@@ -13,11 +13,21 @@
  *   compute  every wave scores its contiguous slice of the visit sequence
  *            (c1-major, entry-minor): the rounded distortion after half the
  *            dimensions (WeightedMSE's early-exit test) and after all of
- *            them, into a per-channel scratch row in HBM;
+ *            them.  It runs the reference's M-best update on its slice
+ *            alone and stores, in order, only the visits that update kept,
+ *            with their (c1, entry) tag, in a per-channel row in HBM;
  *   scan     the leader (virtual wave 0) replays the reference's loop over
- *            the stored pairs in visit order -- SW_MAX when the half-way
- *            value reaches the current worst, then InsertCand's insert --
- *            which is exactly the sequential search, for any weights.
+ *            the stored visits of slices 0..3 in order -- SW_MAX when the
+ *            half-way value reaches the current worst, then InsertCand's
+ *            insert.
+ * Why skipping the other visits is exact: the M-best list holds the eight
+ * smallest distortions d seen so far (an insert drops the largest, an equal
+ * one is rejected), and with non-negative weights the half-way value is at
+ * most the full one f, so a visit enters iff f < worst.  The slice's list has
+ * seen a subset of the visits the reference's has at that point, so its
+ * worst is >= the reference's: a visit the slice rejected, the reference
+ * rejects.  A channel with a negative weight stores every visit (the scan is
+ * then the sequential search itself, for any weights).
  * The interpolation search is split by (candidate, pattern) pairs in the
  * reference's order, each wave keeping its first minimum, the leader the
  * first minimum over the waves.
@@ -44,6 +54,9 @@ namespace mlp {
 #define LQ_ROW 1024	/* dwords per channel of the score buffer (visits, pitch-VQ survivors) */
 #define LQ_NV 4	/* slices per step (the schedule's virtual waves) */
 #define LQ_BATCH 16	/* stored pairs read per batch by the leader's scan */
+#define LQ_SCAP (LQ_VISITS / LQ_NV)	/* stored visits per slice: every visit of the slice fits */
+static_assert(LQ_NV * 2 * LQ_SCAP <= LQ_ROW, "lsf slices exceed the score row");
+
 #define LQ_PAIRS (LSP_INP_CAND * 16)	/* interpolation (candidate, pattern) pairs */
 
 /* the lsf block's exchange words (offsets from its base in the block) */
@@ -54,7 +67,8 @@ enum {
 	XL_ROWS = XL_SIZES + LSP_VQ_STAGES,	/* [8][4] index rows of the candidates */
 	XL_TGT = XL_ROWS + LSP_VQ_CAND * LSP_VQ_STAGES,	/* [20] */
 	XL_WGT = XL_TGT + 2 * LPC_ORD,	/* [20] */
-	XL_PART = XL_WGT + 2 * LPC_ORD,	/* [LQ_NV][3] interpolation: err lo, hi, pair */
+	XL_NS = XL_WGT + 2 * LPC_ORD,	/* [LQ_NV] visits each slice stored */
+	XL_PART = XL_NS + LQ_NV,	/* [LQ_NV][3] interpolation: err lo, hi, pair */
 	XL_IP_LCAND = XL_PART + 3 * LQ_NV,	/* [5][10] frame 2's candidates */
 	XL_IP_QPLSP = XL_IP_LCAND + LSP_INP_CAND * LPC_ORD,	/* [10] */
 	XL_IP_LSP = XL_IP_QPLSP + LPC_ORD,	/* [3][10] the frames' LSFs */
@@ -73,6 +87,7 @@ struct LsfLead {
 	int16_t cand[LSP_VQ_CAND][2 * LPC_ORD];
 	int16_t lcand[LSP_INP_CAND][LPC_ORD], lidx[LSP_INP_CAND * LSP_VQ_STAGES];
 	int16_t best0[LPC_ORD], best1[LPC_ORD], tos2;
+	int16_t ns[LQ_NV];	/* the step's stored visits per slice */
 };
 
 /* the stored pair of one visit: rounded half-way and full distortion */
@@ -239,36 +254,37 @@ MD void lq_vq_scan(LsfLead &L, const D &db)
 	for (int k = 0; k < LSP_VQ_CAND; k++)
 		key[k] = SW_MAX_ * 65536 + (0x8000 | k);
 	Word16 maxd = SW_MAX_;
-	int c1 = 0, e = 0;
-	/* the stored pairs are read LQ_BATCH at a time, every load of a batch
-	 * issued before the first is used (one memory latency per batch instead
-	 * of one per visit); the visits themselves stay in order */
-	for (int u0 = 0; u0 < n; u0 += LQ_BATCH) {
-		uint32_t buf[LQ_BATCH];
+	/* each slice's stored visits in order, read LQ_BATCH at a time (every
+	 * load of a batch issued before the first is used) */
+	(void) n;
+	for (int v = 0; v < LQ_NV; v++) {
+		const int ns = L.ns[v];
+		for (int k0 = 0; k0 < ns; k0 += LQ_BATCH) {
+			uint32_t tb[LQ_BATCH], pb[LQ_BATCH];
 #pragma unroll
-		for (int b = 0; b < LQ_BATCH; b++)
-			buf[b] = (u0 + b < n) ? db.get(u0 + b) : 0u;
-#pragma unroll
-		for (int b = 0; b < LQ_BATCH; b++) {
-			if (u0 + b >= n)
-				break;
-			const int16_t h = (int16_t) (buf[b] & 0xffff), f = (int16_t) (buf[b] >> 16);
-			const Word16 d = (h >= maxd) ? (Word16) SW_MAX_ : f;
-			if (d < maxd) {
-				const int32_t dk = (int32_t) d * 65536;
-				const int32_t nk = dk + ((c1 << 9) | e);
-				bool kp[LSP_VQ_CAND];
-#pragma unroll
-				for (int k = 0; k < LSP_VQ_CAND; k++)
-					kp[k] = key[k] < dk;
-#pragma unroll
-				for (int k = LSP_VQ_CAND - 1; k >= 0; k--)
-					key[k] = kp[k] ? key[k] : ((k == 0 || kp[k > 0 ? k - 1 : 0]) ? nk : key[k > 0 ? k - 1 : 0]);
-				maxd = (Word16) (key[LSP_VQ_CAND - 1] >> 16);
+			for (int b = 0; b < LQ_BATCH; b++) {
+				const bool in = k0 + b < ns;
+				tb[b] = in ? db.get(v * 2 * LQ_SCAP + 2 * (k0 + b)) : 0u;
+				pb[b] = in ? db.get(v * 2 * LQ_SCAP + 2 * (k0 + b) + 1) : 0u;
 			}
-			if (++e == size) {
-				e = 0;
-				c1++;
+#pragma unroll
+			for (int b = 0; b < LQ_BATCH; b++) {
+				if (k0 + b >= ns)
+					break;
+				const int16_t h = (int16_t) (pb[b] & 0xffff), f = (int16_t) (pb[b] >> 16);
+				const Word16 d = (h >= maxd) ? (Word16) SW_MAX_ : f;
+				if (d < maxd) {
+					const int32_t dk = (int32_t) d * 65536;
+					const int32_t nk = dk + (int32_t) tb[b];	/* (c1 << 9) | entry */
+					bool kp[LSP_VQ_CAND];
+#pragma unroll
+					for (int k = 0; k < LSP_VQ_CAND; k++)
+						kp[k] = key[k] < dk;
+#pragma unroll
+					for (int k = LSP_VQ_CAND - 1; k >= 0; k--)
+						key[k] = kp[k] ? key[k] : ((k == 0 || kp[k > 0 ? k - 1 : 0]) ? nk : key[k > 0 ? k - 1 : 0]);
+					maxd = (Word16) (key[LSP_VQ_CAND - 1] >> 16);
+				}
 			}
 		}
 	}
@@ -363,6 +379,8 @@ MD void lq_scan(LsfLead &L, EncState *E, MelpParam *par, X &xc, int b, const D &
 		L.job = 2;
 		lq_vq_start(L, res, mwgt, 2 * LPC_ORD, LQ_CB_RES, res_sz, L.uvc == 1 ? 4 : 2, false);
 	} else {
+		for (int v = 0; v < LQ_NV; v++)
+			L.ns[v] = xc.get(b + XL_NS + v);
 		lq_vq_scan(L, db);
 		if (L.stage == L.tos) {
 			/* the lspVQ's outputs (lspVQ_t's last lines) */
@@ -408,6 +426,17 @@ MD void lq_vq_slice(X &xc, int b, D &db, int v, int cbs, int size, int nc, int s
 	}
 	const int cb0 = (int) (uint16_t) xc.get(b + XL_CB0LO) | ((int) xc.get(b + XL_CB0HI) << 16);
 	const int n = nc * size, lo = v * n / LQ_NV, hi = (v + 1) * n / LQ_NV;
+	bool all = false;	/* a negative weight: store every visit */
+#pragma unroll
+	for (int i = 0; i < DIM; i++)
+		all |= wr[i] < 0;
+	/* the slice's own M-best distortions, ascending (only their multiset
+	 * decides what the slice keeps) */
+	int16_t lk[LSP_VQ_CAND];
+#pragma unroll
+	for (int k = 0; k < LSP_VQ_CAND; k++)
+		lk[k] = SW_MAX_;
+	int ns = 0;
 	int c1 = -1;
 	for (int u = lo; u < hi; u++) {
 		const int c = u / size, e = u - c * size;
@@ -429,8 +458,25 @@ MD void lq_vq_slice(X &xc, int b, D &db, int v, int cbs, int size, int nc, int s
 			for (int i = 0; i < DIM; i++)
 				ct[i] = sub(tgt[i], cand[i]);
 		}
-		db.put(u, lq_wmse<DIM>(wr, g_tab + cbs + e * DIM, ct));
+		const uint32_t pr = lq_wmse<DIM>(wr, g_tab + cbs + e * DIM, ct);
+		const int16_t h = (int16_t) (pr & 0xffff), f = (int16_t) (pr >> 16);
+		const Word16 lmax = lk[LSP_VQ_CAND - 1];
+		const Word16 d = (h >= lmax) ? (Word16) SW_MAX_ : f;
+		const bool keep = d < lmax;
+		if (keep) {	/* sorted insert, the largest drops out */
+#pragma unroll
+			for (int k = LSP_VQ_CAND - 1; k >= 0; k--) {
+				const int16_t prev = k > 0 ? lk[k - 1] : (int16_t) -32768;
+				lk[k] = (prev > d) ? prev : ((lk[k] > d) ? d : lk[k]);
+			}
+		}
+		if (keep || all) {
+			db.put(v * 2 * LQ_SCAP + 2 * ns, (uint32_t) ((c << 9) | e));
+			db.put(v * 2 * LQ_SCAP + 2 * ns + 1, pr);
+			ns++;
+		}
 	}
+	xc.put(b + XL_NS + v, (int16_t) ns);
 }
 
 /* the interpolation search over pairs [20v, 20v + 20) (qnt12.c:1019-1063,

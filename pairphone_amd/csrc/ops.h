@@ -129,6 +129,17 @@ MD int wave_first(int v)
 #endif
 }
 
+/* whether p holds in every active lane (device); the host build's one
+ * channel */
+MD bool wave_all(bool p)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+	return __builtin_amdgcn_ballot_w64(!p) == 0;
+#else
+	return p;
+#endif
+}
+
 typedef int16_t Word16;
 typedef int32_t Word32;
 typedef int64_t Word40;

@@ -16,8 +16,8 @@ os.environ.setdefault("MELPE_AMD_LIB", os.path.join(ROOT, "pairphone_amd", "libm
 import numpy as np  # noqa: E402
 
 LQ_SLOTS = 7
-PHASES = (["frame 0", "frame 1", "frame 2", "lsf prelude|bands2"]
-          + [n % k for k in range(LQ_SLOTS) for n in ("lsf compute %d", "lsf scan %d")]
+PHASES = (["frame 0", "frame 1", "frame 2", "lsf prelude+step 0|bands2"]
+          + [n % k for k in range(1, LQ_SLOTS) for n in ("lsf compute %d", "lsf scan %d")]
           + ["sc_ana+pvq prelude", "pvq slices", "pvq finish..", "find_harm", "pack"])
 
 
@@ -54,8 +54,9 @@ def main(C=32768, nsf=4):
         tot += row[4]
         print("  %-16s %10.0f %10.0f %10.0f %10.0f %10.0f" % (name, row[4], *row[:4]))
     nwv = max(nw, 1)
-    print("  copy-in+dc_rmv per wave %.0f, write-back per wave %.0f, sum of phase walls %.0f"
-          % (v[64 + 5 * len(PHASES)] / wg / nwv, v[64 + 5 * len(PHASES) + 1] / wg / nwv, tot))
+    print("  copy-in per wave %.0f, dc_rmv per wave %.0f, write-back per wave %.0f, sum of phase "
+          "walls %.0f" % (v[64 + 5 * len(PHASES)] / wg / nwv, v[64 + 5 * len(PHASES) + 2] / wg / nwv,
+                          v[64 + 5 * len(PHASES) + 1] / wg / nwv, tot))
 
 
 if __name__ == "__main__":

@@ -7,8 +7,8 @@ Reads   <dir>/prof_kt/*_results.db        (--kernel-trace --stats pass)
         <dir>/pmc_*/*_results.db          (one --pmc pass each)
 Writes  profiles/<tag>_kernel_stats.txt   per-kernel calls / total / average
         profiles/<tag>_pmc.txt            per-kernel counter means per dispatch
-        profiles/pmc_latest.json          HBM bytes per k_encode / k_decode
-                                          launch (read by bench.py)
+        profiles/pmc_latest.json          HBM bytes per kernel launch, one set
+                                          per channel count (read by bench.py)
 
 FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters in KiB per dispatch
 (TCC_EA0_RDREQ / _WRREQ x request size).  MI355X_MICROARCH.md: on gfx950
@@ -114,7 +114,14 @@ def main():
                 out["kernels"][k] = {"fetch_bytes": d["FETCH_SIZE"] * 1024.0,
                                      "write_bytes": d["WRITE_SIZE"] * 1024.0,
                                      "bytes_per_launch": (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0}
-        json.dump(out, open(os.path.join(prof, "pmc_latest.json"), "w"), indent=1)
+        # one set per channel count: a pass at another size keeps the others
+        lp = os.path.join(prof, "pmc_latest.json")
+        sets = []
+        if os.path.exists(lp):
+            old = json.load(open(lp))
+            sets = old.get("sets", [old] if "kernels" in old else [])
+        sets = [x for x in sets if x.get("channels") != out["channels"]] + [out]
+        json.dump({"sets": sets}, open(lp, "w"), indent=1)
 
 
 if __name__ == "__main__":
