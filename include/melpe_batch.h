@@ -74,10 +74,11 @@ int melpe_engine_set_lane_order(melpe_engine *e, int on);
 
 /* Waves per 64 channels of the analysis kernel: 1 = one lane per channel;
  * 4 = each channel's independent analysis chains (bandpass-voicing bands,
- * LPC/LSF, pitch tracking, classification, the LSF codebook searches)
- * spread over four waves of one workgroup, for channel counts that would
- * leave SIMDs idle (up to 65,536 channels per GPU); 0 (default) = chosen
- * from the channel count.  Bits are the same either way. */
+ * LPC/LSF, global pitch, pitch tracking, classification, the LSF and pitch
+ * codebook searches) spread over four waves of one workgroup, for channel
+ * counts that would leave SIMDs idle; 0 (default) = chosen from the channel
+ * count (4 up to 32,768 channels per engine, where every workgroup is
+ * resident at once; 1 above).  Bits are the same either way. */
 int melpe_engine_set_ana_waves(melpe_engine *e, int waves);
 
 /* Per-channel state records, for checkpoint / resume and for moving channels

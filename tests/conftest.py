@@ -42,8 +42,20 @@ def _torch_hip_first(request):
     """GPU tests: bring up torch's HIP context before the engine library
     makes its first HIP call, so tests that mix the C ABI with torch device
     buffers see the same device set in any order."""
-    if request.node.get_closest_marker("gpu") is not None:
+    gpu = request.node.get_closest_marker("gpu") is not None
+    if gpu:
         import torch
         if torch.cuda.is_available():
             torch.cuda.init()
     yield
+    if gpu:
+        # hand the device memory this test's tensors held back to the device:
+        # the suite runs in one process, and later tests start other
+        # processes on the same GPU (tests/test_shard.py), whose kernels need
+        # their own scratch
+        import gc
+        import torch
+        gc.collect()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
