@@ -226,12 +226,14 @@ MD void pv_replay(const PvqWork &w, X &xc, const D &db, int16_t *il, Word32 *dl)
 
 /* the part of each physical wave's private copy that differs from the HBM
  * record before any phase: dc removal of the three frames (melp_ana.c:
- * 140-145; each wave filters its own copy, only wave 0 keeps the result) */
+ * 140-145; each wave filters its own copy, only wave 0 keeps the result),
+ * reading the superframe's PCM (4-byte aligned) where the caller holds it:
+ * the three frames are one run of the same biquads */
 MD void ana_mw_begin(EncState *E, const int16_t *sp_in)
 {
-	for (int i = 0; i < NF; i++)
-		dc_rmv(&sp_in[i * FRAME], &E->hpspeech[IN_BEG + i * FRAME], E->dcdelin, E->dcdelout_hi,
-		       E->dcdelout_lo, FRAME);
+	static_assert(BLOCK % 36 == 0, "dc removal batches");
+	iir3_d_batched(sp_in, &E->hpspeech[IN_BEG], TB(dc_den), TB(dc_num), E->dcdelin,
+		       E->dcdelout_hi, E->dcdelout_lo, BLOCK);
 }
 
 /* band k (1..4) of frame i on a non-driver wave */

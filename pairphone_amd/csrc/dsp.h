@@ -1410,6 +1410,49 @@ MD void iir3_d(const int16_t *in, int16_t *out, const int16_t *den, const int16_
 	}
 }
 
+/* iir3_d from a 4-byte aligned input of n samples (n a multiple of 36), read
+ * 18 dwords at a time with every load of a batch issued before the filter
+ * uses the first: the input is the caller's PCM in global memory, one
+ * channel per lane, where each load waits a full memory latency */
+MD void iir3_d_batched(const int16_t *in, int16_t *out, const int16_t *den, const int16_t *num,
+		       int16_t *din, int16_t *dhi, int16_t *dlo, int n)
+{
+	Biqd b[3];
+	for (int s = 0; s < 3; s++) {
+		b[s].n0 = num[3 * s];
+		b[s].n1 = num[3 * s + 1];
+		b[s].n2 = num[3 * s + 2];
+		b[s].d1 = den[3 * s + 1];
+		b[s].d2 = den[3 * s + 2];
+		b[s].i0 = din[2 * s];
+		b[s].i1 = din[2 * s + 1];
+		b[s].h0 = dhi[2 * s];
+		b[s].h1 = dhi[2 * s + 1];
+		b[s].l0 = dlo[2 * s];
+		b[s].l1 = dlo[2 * s + 1];
+	}
+	const u32_alias *p = (const u32_alias *) in;
+	for (int i = 0; i < n; i += 36) {
+		uint32_t v[18];
+#pragma unroll
+		for (int k = 0; k < 18; k++)
+			v[k] = p[i / 2 + k];
+#pragma unroll
+		for (int k = 0; k < 18; k++) {
+			out[i + 2 * k] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], (int16_t) (v[k] & 0xffff))));
+			out[i + 2 * k + 1] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], (int16_t) (v[k] >> 16))));
+		}
+	}
+	for (int s = 0; s < 3; s++) {
+		din[2 * s] = b[s].i0;
+		din[2 * s + 1] = b[s].i1;
+		dhi[2 * s] = b[s].h0;
+		dhi[2 * s + 1] = b[s].h1;
+		dlo[2 * s] = b[s].l0;
+		dlo[2 * s + 1] = b[s].l1;
+	}
+}
+
 MD void biqd_load(Biqd &b, const int16_t *den, const int16_t *num, const int16_t *din,
 		  const int16_t *dhi, const int16_t *dlo)
 {

@@ -56,7 +56,6 @@ struct GlbDb {
 struct AnaMwLane {
 	uint8_t guard[FLAT_GUARD_BYTES];
 	EncState S;	/* only the part after the NPP state is live */
-	int16_t x[BLOCK];
 	AnaMwTmp tmp;
 };
 
@@ -91,14 +90,12 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_MW_WAVES) void k_enc_ana_mw(EncSta
 	GlbDb db{lqbuf + blockIdx.x * WAVE + t, (size_t) gridDim.x * WAVE};
 	EncState *rec = &enc[c];
 	MW_T0(tb);
-	if (live) {
+	if (live)
 		ana_mw_copy_in(&L.S, rec, w, NW);
-		lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
-	}
 	MW_T1(tb, MW_SLOT(MW_PHASES, 0));
 	MW_T0(td);
 	if (live)
-		ana_mw_begin(&L.S, L.x);
+		ana_mw_begin(&L.S, sp + (size_t) c * BLOCK);
 	MW_T1(td, MW_SLOT(MW_PHASES, 2));
 	for (int p = 0; p < MW_PHASES; p++) {
 		MW_T0(tp);
