@@ -259,7 +259,10 @@ def pmc_traffic(kernel, channels):
     d = next((x for x in sets if x.get("channels") == channels), None)
     if d is None:
         return None, None
-    k = d.get("kernels", {}).get(kernel)
+    ks = d.get("kernels", {})
+    # at the channel counts the engine runs the multi-wave analysis kernel
+    # (k_enc_ana_mw<4>), that kernel is the analysis launch
+    k = ks.get(kernel) or next((v for n, v in ks.items() if n.startswith(kernel + "_mw")), None)
     return (None if k is None else k["bytes_per_launch"]), d.get("source")
 
 

@@ -25,11 +25,13 @@
  *               waves and replayed in order by v0 (lsfvq_mw.h)
  *   MW_PH_SC    v0 sc_ana and pitch_vq's prelude, after gathering
  *               classify's and pitchAuto's tracks (through the HBM record)
- *               and the band voicings and gains (exchange block)
+ *               and the band voicings and gains (exchange block); v1..v3
+ *               the residual spectrum of frame v-1 (find_harm's FFT needs
+ *               only the quantised LSFs)
  *   +1          pitch_vq's codebook search, a quarter per wave (pv_slice)
  *   +2          v0 the search's replay, pitch_vq's finish, quant_bp,
  *               quant_jitter
- *   +3          find_harm of frame i on v(i+1)
+ *   +3          find_harm's harmonic magnitudes of frame i on v(i+1)
  *   +4          v0 quant_fsmag, the channel write.
  * Phase 0 also runs the global-pitch chain of all three frames on v3 (it
  * depends on nothing else), so v0 takes frames 1 and 2's from the block.
@@ -136,6 +138,7 @@ struct AnaMwTmp {
 	int16_t peak[NF];
 	LsfLead lq;	/* lsf_vq's leader state (virtual wave 0) */
 	PvqWork pv;	/* pitch_vq's prelude, for its finish two phases on */
+	uint32_t hb[512];	/* v1..v3: the frame's residual spectrum (find_harm_fft) */
 };
 
 /*
@@ -384,11 +387,27 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, D &db, AnaMwTmp &tmp, in
 		}
 	} else if (p < MW_PH_SC) {
 		/* the lsf block: (compute on every wave, scan on the leader) */
-		if (((p - MW_PH_LQ) & 1) == 0)
+		if (((p - MW_PH_LQ) & 1) == 0) {
 			lq_compute(xc, XS_LQ, db, v);
-		else if (v == 0)
+		} else if (v == 0) {
 			lq_scan(tmp.lq, E, E->par, xc, XS_LQ, db);
+			if (p == MW_PH_SC - 1)	/* done: the quantised LSFs, for find_harm */
+				for (int i = 0; i < NF; i++)
+					for (int k = 0; k < LPC_ORD; k++)
+						xc.put(XS_LSF + i * LPC_ORD + k, E->par[i].lsf[k]);
+		}
 	} else if (p == MW_PH_SC) {
+		if (v >= 1 && v <= NF) {
+			/* find_harm's FFT of frame v-1 needs only the quantised LSFs:
+			 * it runs here, beside sc_ana, and its magnitudes, which need
+			 * the quantised pitch, three phases on */
+			const int i = v - 1;
+			MelpParam *par = &E->par[i];
+			for (int k = 0; k < LPC_ORD; k++)
+				par->lsf[k] = xc.get(XS_LSF + i * LPC_ORD + k);
+			ana_fsmag_fft(E, par, i, tmp.hb);
+			return;
+		}
 		if (v != 0)
 			return;
 		MelpParam *par = E->par;
@@ -434,21 +453,21 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, D &db, AnaMwTmp &tmp, in
 		quant_bp(E, par);
 		quant_jitter(E, par);
 		for (int i = 0; i < NF; i++) {
-			for (int k = 0; k < LPC_ORD; k++)
-				xc.put(XS_LSF + i * LPC_ORD + k, par[i].lsf[k]);
 			xc.put(XS_FHP + i, par[i].pitch);
 			xc.put(XS_FHUV + i, par[i].uv_flag);
 		}
 	} else if (p == MW_PH_SC + 3) {
-		if (v == 0)
+		if (v == 0 || v > NF)
 			return;
+		/* ana_fsmag_frame's second half (melp_ana.c:224-236) on the
+		 * spectrum of phase MW_PH_SC */
 		const int i = v - 1;
 		MelpParam *par = &E->par[i];
-		for (int k = 0; k < LPC_ORD; k++)
-			par->lsf[k] = xc.get(XS_LSF + i * LPC_ORD + k);
 		par->pitch = xc.get(XS_FHP + i);
 		par->uv_flag = xc.get(XS_FHUV + i);
-		ana_fsmag_frame(E, par, i);
+		v_set(par->fs_mag, 8192, NUM_HARM);
+		if (!par->uv_flag)
+			find_harm_mag(tmp.hb, par->fs_mag, par->pitch, NUM_HARM);
 		for (int k = 0; k < NUM_HARM; k++)
 			xc.put(XS_FSMAG + i * NUM_HARM + k, par->fs_mag[k]);
 	} else if (v == 0) {

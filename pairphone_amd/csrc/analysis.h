@@ -2023,11 +2023,10 @@ MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *
 /* ------------------------------------------------------------------ */
 /* find_harm, melpe/fs_lib.c:62 -- Fourier magnitudes of the residual */
 /* ------------------------------------------------------------------ */
-MN void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, int len)
+/* find_harm's pitch-independent half: the scaled residual's 512-point real
+ * FFT into hb (512 packed complex bins, re | im << 16) */
+MN void find_harm_fft(const int16_t *in, uint32_t *hb, int len)
 {
-	PROF_SCOPE(12);
-	uint32_t hb[512];	/* 512 packed complex bins (re | im << 16) */
-	Word32 Lm[NUM_HARM];
 	Word16 mx = 0;
 	for (int i = 0; i < len; i++) {
 		Word16 t = abs_s(in[i]);
@@ -2035,7 +2034,6 @@ MN void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, in
 			mx = t;
 	}
 	Word16 sh = norm_s(mx);
-	v_set(fsmag, 8192, nh);
 	/* the 512 real input points as 256 complex pairs, zero padded past len;
 	 * the scaled input's max |x| is the first guard test's block_max */
 	Word16 smx = 0;
@@ -2048,6 +2046,14 @@ MN void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, in
 	for (int k = 256; k < 512; k++)
 		hb[k] = 0;
 	rfft_pk(hb, 512, smx);
+}
+
+/* find_harm's second half: the peak magnitude around each pitch harmonic,
+ * normalised */
+MN void find_harm_mag(const uint32_t *hb, int16_t *fsmag, Word16 pitch, Word16 nh)
+{
+	Word32 Lm[NUM_HARM];
+	v_set(fsmag, 8192, nh);
 	Word16 fw = shr(divide_s(512, pitch), 2);
 	Word16 iw = shr(fw, 6);
 	Word16 i2 = shr(iw, 1);
@@ -2074,12 +2080,20 @@ MN void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, in
 	Word32 Lt = (Word32) L40_shl(avg, t1);
 	t1 = sub(31, t1);
 	Word16 t2 = divide_s(shl(nh, 10), extract_h(Lt));
-	sh = sub(30, t1);
+	Word16 sh = sub(30, t1);
 	for (int i = 0; i < nh; i++) {
 		t1 = extract_h(L_shl(Lm[i], sh));
 		t1 = extract_h(L_shl(L_mult(t1, t2), 2));
 		fsmag[i] = sqrt_Q15(t1);
 	}
+}
+
+MN void find_harm(const int16_t *in, int16_t *fsmag, Word16 pitch, Word16 nh, int len)
+{
+	PROF_SCOPE(12);
+	uint32_t hb[512];
+	find_harm_fft(in, hb, len);
+	find_harm_mag(hb, fsmag, pitch, nh);
 }
 
 }  // namespace mlp

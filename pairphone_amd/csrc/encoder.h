@@ -454,6 +454,20 @@ MN void ana_fsmag_frame(EncState *E, MelpParam *par, int i)
 	}
 }
 
+/* ana_fsmag_frame's pitch-independent half, run before the frame's pitch is
+ * quantised (ana_mw.h): the residual of the quantised LSFs, windowed, and
+ * its FFT (melp_ana.c:224-233) */
+MN void ana_fsmag_fft(EncState *E, MelpParam *par, int i, uint32_t *hb)
+{
+	int16_t lpc[LPC_ORD + 1];
+	lpc[0] = 4096;
+	lpc_lsp2pred(par->lsf, &lpc[1], LPC_ORD);
+	zerflt(&E->hpspeech[i * FRAME + FRAME_END - LPC_FRAME / 2], lpc, E->sigbuf, LPC_ORD,
+	       LPC_FRAME);
+	window(E->sigbuf, TB(win_cof), E->sigbuf, LPC_FRAME);
+	find_harm_fft(E->sigbuf, hb, LPC_FRAME);
+}
+
 /* quant_fsmag, the channel write and the history shift (melp_ana.c:238-265) */
 MN void ana_pack(EncState *E)
 {
@@ -482,6 +496,52 @@ MN void analysis_tail(EncState *E)
 	for (int i = 0; i < NF; i++)
 		ana_fsmag_frame(E, &par[i], i);
 	ana_pack(E);
+}
+
+/* analysis() in the split form of the lane-per-channel kernels (k_ana.hip
+ * k_enc_ana, k_harm.hip): analysis_a runs everything before the Fourier
+ * magnitudes, writes each voiced frame's windowed residual of the quantised
+ * LSFs to res[i * LPC_FRAME ..] (melp_ana.c:224-233, the input of
+ * find_harm; an unvoiced frame's row is not written) and does the history
+ * shift; the magnitudes go into par[i].fs_mag (k_enc_harm), then
+ * analysis_b packs the superframe.  The shift reads only hpspeech, which
+ * nothing after it reads, so moving it ahead of the packing changes no
+ * value. */
+MN void analysis_a(EncState *E, const int16_t *sp_in, int16_t *res)
+{
+	for (int i = 0; i < NF; i++)
+		analysis_frame(E, sp_in, i);
+	MelpParam *par = E->par;
+	sc_ana(E, par);
+	lsf_vq(E, par);
+	pitch_vq(E, par);
+	gain_vq(E, par);
+	for (int i = 0; i < NF; i++)
+		quant_u(&par[i].jitter, &E->qpar.jit_index[i], 0, MAX_JITTER_Q15, 2, SW_MAX_,
+			true, 7);
+	quant_bp(E, par);
+	quant_jitter(E, par);
+	for (int i = 0; i < NF; i++) {
+		if (par[i].uv_flag)
+			continue;
+		int16_t lpc[LPC_ORD + 1];
+		lpc[0] = 4096;
+		lpc_lsp2pred(par[i].lsf, &lpc[1], LPC_ORD);
+		zerflt(&E->hpspeech[i * FRAME + FRAME_END - LPC_FRAME / 2], lpc, E->sigbuf, LPC_ORD,
+		       LPC_FRAME);
+		window(E->sigbuf, TB(win_cof), E->sigbuf, LPC_FRAME);
+		v_copy(&res[i * LPC_FRAME], E->sigbuf, LPC_FRAME);
+	}
+	v_copy(E->hpspeech, &E->hpspeech[NF * FRAME], IN_BEG);
+}
+
+MN void analysis_b(EncState *E)
+{
+	MelpParam *par = E->par;
+	quant_fsmag(E, par);
+	for (int i = 0; i < NF; i++)
+		E->qpar.uv_flag[i] = par[i].uv_flag;
+	low_rate_chn_write(E);
 }
 
 MN void analysis(EncState *E, const int16_t *sp_in)

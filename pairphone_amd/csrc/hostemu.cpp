@@ -157,7 +157,7 @@ int emu_encode_ana_mw(emu_engine *e, unsigned char *bits, const int16_t *sp, int
 		for (int p = 0; p < MW_PHASES; p++)
 			for (int w = 0; w < nw; w++)
 				for (int v = w; v < MW_NV; v += nw)
-					ana_mw_phase(&W[w], &rec, xc, db, tmp[w], v, p);
+					ana_mw_phase(&W[w], &rec, xc, db, tmp[v], v, p);
 		for (int w = 0; w < nw; w++)
 			for (int v = w; v < MW_NV; v += nw) {
 				size_t off[2], len[2];
