@@ -16,14 +16,17 @@ The decode leg (melpe_s of the bits just produced), the TX front end (VAD
 gate + melpe_a on ragged streams, config 5), the voice-frame crypt and the
 VAD alone are timed the same way and reported beside the headline.
 
-A step is two kernels on one stream: k_enc_npp (noise pre-processor, one
-wavefront per channel) then k_enc_ana (analysis + packing); each launch is
-bracketed by HIP events on that stream.
+A step is two launches on one stream: k_enc_npp (noise pre-processor, one
+wavefront per channel) then the analysis (k_enc_ana, lane per channel, up to
+the Fourier magnitudes; k_enc_harm, their FFTs with a wavefront per channel;
+k_enc_tail, the packing -- or k_enc_ana_mw at up to 32,768 channels); each
+launch is bracketed by HIP events on that stream.
 
 Roofline: the codec is bit-exact saturating int16/int32 arithmetic with
 serial recursions per channel, so it is bounded by INT VALU issue, not HBM
-and not MFMA.  For the dominant kernel (k_enc_ana) achieved =
-W_ana x channels / its average launch duration, W_ana = the reference's basic
+and not MFMA.  For the dominant launch (the analysis, reported as
+"k_enc_ana") achieved = W_ana x channels / its average duration, W_ana = the
+reference's basic
 ops per channel-superframe of the analysis averaged over exactly the
 superframes this run times (profiles/opcount.json W_enc_ana_by_sf, counted by
 tools/opcount.py on this same input); peak = 256 CUs x 4 SIMDs x 32
@@ -67,6 +70,11 @@ PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12     # INT32 lane-ops/s, T
 # 24 rot, chi 75 (not, and, xor per lane), iota 1 = 155 64-bit ops; x 24 rounds
 VC_OPS_PER_PACKET = 2 * 155 * 24
 REF_TOOL = os.path.join(ROOT, "oracle", "_ref", "ref_tool")
+# the kernels of one analysis launch (encode_ana_dev): the lane-per-channel
+# analysis split around the wave-per-channel Fourier magnitudes (k_harm.hip),
+# or the multi-wave kernel at the channel counts the engine runs it
+ANALYSIS_KERNELS = ("k_enc_ana", "k_enc_ana<true>", "k_enc_ana<false>", "k_enc_harm", "k_enc_tail",
+                    "k_enc_ana_mw<4>")
 
 
 def parse(argv=None):
@@ -260,10 +268,9 @@ def pmc_traffic(kernel, channels):
     if d is None:
         return None, None
     ks = d.get("kernels", {})
-    # at the channel counts the engine runs the multi-wave analysis kernel
-    # (k_enc_ana_mw<4>), that kernel is the analysis launch
-    k = ks.get(kernel) or next((v for n, v in ks.items() if n.startswith(kernel + "_mw")), None)
-    return (None if k is None else k["bytes_per_launch"]), d.get("source")
+    names = ANALYSIS_KERNELS if kernel == "k_enc_ana" else (kernel,)
+    got = [ks[n]["bytes_per_launch"] for n in names if n in ks]
+    return (sum(got) if got else None), d.get("source")
 
 
 def kroof(kernel, W_sf, C, kms, in_b, out_b, traffic_key=None):
@@ -490,6 +497,8 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
                 "unit": "T basic-ops/s (INT32 VALU lane-ops)", "frac": ana["frac"],
                 "traffic": ana["traffic"], "traffic_source": ana["traffic_source"],
                 "kernel": "k_enc_ana", "kernel_ms": ana_kms,
+                "kernel_note": "the analysis launch: k_enc_ana + k_enc_harm + k_enc_tail (lane / "
+                               "wave / lane per channel), or k_enc_ana_mw up to 32,768 channels",
                 "W_per_channel_superframe": w_ana, "W_source": w_src,
                 "algorithmic_hbm_bytes_per_launch": ana["algorithmic_hbm_bytes_per_launch"],
                 "kernels": [ana, npp],

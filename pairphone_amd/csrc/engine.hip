@@ -57,19 +57,24 @@ extern "C" {
 int melpe_tu_npp_upload(const void *blob, size_t bytes);
 int melpe_tu_ana_upload(const void *blob, size_t bytes);
 int melpe_tu_anamw_upload(const void *blob, size_t bytes);
+int melpe_tu_harm_upload(const void *blob, size_t bytes);
 int melpe_tu_dec_upload(const void *blob, size_t bytes);
 int melpe_tu_r24_upload(const void *blob, size_t bytes);
 int melpe_tu_r24_prof(uint64_t *acc);
 int melpe_tu_npp_prof(uint64_t *acc);
 int melpe_tu_ana_prof(uint64_t *acc);
 int melpe_tu_anamw_prof(uint64_t *acc);
+int melpe_tu_harm_prof(uint64_t *acc);
 int melpe_tu_dec_prof(uint64_t *acc);
 int kl_npp(EncState *enc, int16_t *sp, int frames, int stride, const uint8_t *active, int n,
 	   int rate1200, hipStream_t s);
 int kl_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active, int n, hipStream_t s);
 int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
-	       const int *perm, const int *nlive,
-	       hipStream_t s);
+	       const int *perm, const int *nlive, int16_t *res, hipStream_t s);
+int kl_enc_harm(EncState *enc, const int16_t *res, const uint8_t *active, int n, const int *perm,
+		const int *nlive, hipStream_t s);
+int kl_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active, int n, const int *perm,
+		const int *nlive, hipStream_t s);
 int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
 		  const int *perm, const int *nlive, int nw, uint32_t *lqbuf, hipStream_t s);
 size_t kl_enc_ana_mw_lq_words(int n);
@@ -614,6 +619,7 @@ struct melpe_engine {
 	int lane_order = -1;	/* 1 on, 0 off, -1 the MELPE_BIN default */
 	int ana_waves = 0;	/* waves per 64 channels in k_enc_ana(_mw); 0: by channel count */
 	uint32_t *d_lq = nullptr;	/* k_enc_ana_mw's lsf_vq score rows, allocated on first use */
+	int16_t *d_res = nullptr;	/* the split lane analysis' windowed residuals (C x NF x LPC_FRAME) */
 	/* one event per stream this engine's *_dev calls have used, recorded
 	 * after each call: the host-side calls wait on these (engine_wait)
 	 * instead of the whole device */
@@ -645,6 +651,18 @@ static int ana_waves_for(melpe_engine *e)
 	return groups <= 512 ? 4 : 1;
 }
 
+/* the split lane analysis (k_harm.hip); MELPE_HARM=0 (diagnostics) runs the
+ * whole analysis in k_enc_ana */
+static bool harm_split(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("MELPE_HARM");
+		v = !(e && e[0] == '0');
+	}
+	return v != 0;
+}
+
 static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, const uint8_t *d_act,
 		      hipStream_t s)
 {
@@ -667,9 +685,27 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 			return (int) er;
 		}
 	}
-	int rc = nw == 1 ? kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, s)
-			 : kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nw,
-					 e->d_lq, s);
+	int rc;
+	if (nw == 1 && harm_split()) {
+		/* lane-per-channel analysis up to the Fourier magnitudes, the
+		 * magnitudes with a wave per channel, then the packing (k_harm.hip) */
+		if (!e->d_res) {
+			er = hipMalloc(&e->d_res, sizeof(int16_t) * NF * LPC_FRAME * (size_t) e->channels);
+			if (er != hipSuccess) {
+				e->d_res = nullptr;
+				return (int) er;
+			}
+		}
+		rc = kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, e->d_res, s);
+		if (rc == 0)
+			rc = kl_enc_harm(e->d_enc, e->d_res, d_act, e->channels, perm, nlive, s);
+		if (rc == 0)
+			rc = kl_enc_tail(e->d_enc, d_bits, d_act, e->channels, perm, nlive, s);
+	} else {
+		rc = nw == 1 ? kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nullptr, s)
+			     : kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nw,
+					     e->d_lq, s);
+	}
 	if (rc == 0 && on)
 		rc = (int) bin_release(b, s);
 	return rc;
@@ -708,7 +744,8 @@ static int ensure_device_tables(int dev)
 		return fail_msg("embedded table blob has the wrong size");
 	DEVGUARD(dev);
 	int (*up[])(const void *, size_t) = {melpe_tu_eng_upload, melpe_tu_npp_upload,
-					     melpe_tu_ana_upload, melpe_tu_anamw_upload, melpe_tu_dec_upload,
+					     melpe_tu_ana_upload, melpe_tu_anamw_upload, melpe_tu_harm_upload,
+					     melpe_tu_dec_upload,
 					     melpe_tu_r24_upload};
 	for (auto f : up)
 		if (int rc = f(melpe_tables_blob, bytes))
@@ -846,6 +883,7 @@ int melpe_engine_destroy(melpe_engine *e)
 	hipFree(e->bin_enc.perm);
 	hipFree(e->bin_dec.perm);
 	hipFree(e->d_lq);
+	hipFree(e->d_res);
 	for (auto &m : e->marks)
 		hipEventDestroy(m.second);
 	if (e->bin_enc.done)
@@ -1265,6 +1303,7 @@ int melpe_prof_read(uint64_t *out, int n)
 {
 	uint64_t acc[MELPE_PROF_SLOTS_ABI] = {0};
 	int (*rd[])(uint64_t *) = {melpe_tu_eng_prof, melpe_tu_npp_prof, melpe_tu_ana_prof, melpe_tu_anamw_prof,
+				   melpe_tu_harm_prof,
 				   melpe_tu_dec_prof, melpe_tu_r24_prof};
 	for (auto f : rd)
 		if (f(acc))

@@ -109,6 +109,30 @@ int emu_encode_npp(emu_engine *e, int16_t *sp)
 	return 0;
 }
 
+/* the split lane analysis as k_enc_ana / k_enc_harm / k_enc_tail run it,
+ * with the Fourier magnitudes from the scalar find_harm on the written
+ * residuals (the wave kernel's own arithmetic is checked on the GPU) */
+int emu_encode_ana_split(emu_engine *e, unsigned char *bits, const int16_t *sp)
+{
+	static int16_t res[NF * LPC_FRAME];
+	for (int c = 0; c < e->channels; c++) {
+		EncState *E = &e->enc[c];
+		for (int k = 0; k < NF * LPC_FRAME; k++)
+			res[k] = (int16_t) 0x5a5a;	/* unvoiced rows stay unread */
+		analysis_a(E, sp + (size_t) c * BLOCK, res);
+		for (int i = 0; i < NF; i++) {
+			MelpParam *par = &E->par[i];
+			v_set(par->fs_mag, 8192, NUM_HARM);
+			if (!par->uv_flag)
+				find_harm(&res[i * LPC_FRAME], par->fs_mag, par->pitch, NUM_HARM, LPC_FRAME);
+		}
+		analysis_b(E);
+		for (int k = 0; k < 11; k++)
+			bits[c * 11 + k] = E->chbuf[k];
+	}
+	return 0;
+}
+
 int emu_encode_ana(emu_engine *e, unsigned char *bits, const int16_t *sp)
 {
 	for (int c = 0; c < e->channels; c++) {

@@ -15,9 +15,13 @@ struct AnaLane {
 	int16_t x[BLOCK];
 };
 
+/* SPLIT: the split form (encoder.h analysis_a): the windowed residuals to
+ * res (NF x LPC_FRAME per channel), the Fourier magnitudes and the packing
+ * in k_harm.hip; else the whole analysis and the bits here (MELPE_HARM=0) */
+template <bool SPLIT>
 __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits,
 						  const uint8_t *active, int n, const int *perm,
-						  const int *nlive)
+						  const int *nlive, int16_t *res)
 {
 	/* lane g runs channel perm[g] when the engine ordered the live channels
 	 * by pitch class (engine.hip, MELPE_BIN), else channel g under the mask */
@@ -33,6 +37,11 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 	PIN_FRAME(L);
 	lane_copy((char *) &L.S + ENC_ANA_OFF, (const char *) &enc[c] + ENC_ANA_OFF, ENC_ANA_BYTES);
 	lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
+	if (SPLIT) {
+		analysis_a(&L.S, L.x, res + (size_t) c * NF * LPC_FRAME);
+		lane_copy((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, ENC_ANA_BYTES);
+		return;
+	}
 	analysis(&L.S, L.x);
 	lane_copy((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, ENC_ANA_BYTES);
 	for (int k = 0; k < 11; k++)
@@ -67,9 +76,12 @@ static unsigned ana_lds_bytes(void)
 }
 
 extern "C" int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
-			  int n, const int *perm, const int *nlive, hipStream_t s)
+			  int n, const int *perm, const int *nlive, int16_t *res, hipStream_t s)
 {
-	k_enc_ana<<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive);
+	if (res)
+		k_enc_ana<true><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res);
+	else
+		k_enc_ana<false><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res);
 	return (int) hipGetLastError();
 }
 

@@ -54,6 +54,9 @@ namespace mlp {
 #define LQ_ROW 1024	/* dwords per channel of the score buffer (visits, pitch-VQ survivors) */
 #define LQ_NV 4	/* slices per step (the schedule's virtual waves) */
 #define LQ_BATCH 16	/* stored pairs read per batch by the leader's scan */
+#ifndef MELPE_LQ_GATHER
+#define MELPE_LQ_GATHER 0
+#endif
 #define LQ_SCAP (LQ_VISITS / LQ_NV)	/* stored visits per slice: every visit of the slice fits */
 static_assert(LQ_NV * 2 * LQ_SCAP <= LQ_ROW, "lsf slices exceed the score row");
 
@@ -479,6 +482,86 @@ MD void lq_vq_slice(X &xc, int b, D &db, int v, int cbs, int size, int nc, int s
 	xc.put(b + XL_NS + v, (int16_t) ns);
 }
 
+#if MELPE_LQ_GATHER
+/* lq_vq_slice with the stage, size, candidates and codebook per lane: the
+ * codebook rows are gathered through the vector memory path (dword loads,
+ * the lsf codebooks' rows are 4-byte aligned) instead of one scalar-cache
+ * pass per distinct stage among the wave's channels (experiment) */
+template <int DIM, class X, class D>
+MD void lq_vq_slice_g(X &xc, int b, D &db, int v, int cbs, int size, int nc, int s)
+{
+	int16_t wr[DIM], tgt[DIM], ct[DIM];
+#pragma unroll
+	for (int i = 0; i < DIM; i++) {
+		wr[i] = xc.get(b + XL_WGT + i);
+		tgt[i] = xc.get(b + XL_TGT + i);
+	}
+	const int cb0 = (int) (uint16_t) xc.get(b + XL_CB0LO) | ((int) xc.get(b + XL_CB0HI) << 16);
+	const int n = nc * size, lo = v * n / LQ_NV, hi = (v + 1) * n / LQ_NV;
+	bool all = false;
+#pragma unroll
+	for (int i = 0; i < DIM; i++)
+		all |= wr[i] < 0;
+	int16_t lk[LSP_VQ_CAND];
+#pragma unroll
+	for (int k = 0; k < LSP_VQ_CAND; k++)
+		lk[k] = SW_MAX_;
+	int ns = 0;
+	int c = lo / size, e = lo - c * size;
+	bool fresh = true;
+	for (int u = lo; u < hi; u++) {
+		if (fresh) {
+			fresh = false;
+			int16_t cand[DIM];
+#pragma unroll
+			for (int i = 0; i < DIM; i++)
+				cand[i] = 0;
+			const int16_t *p2 = g_tab + cb0;
+			for (int i = 0; i < s; i++) {
+				const int16_t r = xc.get(b + XL_ROWS + c * LSP_VQ_STAGES + i);
+				Word16 o = extract_l(L_shr(L_mult(r, (Word16) DIM), 1));
+				v_add(cand, p2 + o, DIM);
+				p2 += extract_l(L_shr(L_mult(xc.get(b + XL_SIZES + i), (Word16) DIM), 1));
+			}
+#pragma unroll
+			for (int i = 0; i < DIM; i++)
+				ct[i] = sub(tgt[i], cand[i]);
+		}
+		int16_t x[DIM];
+		const u32_alias *row = (const u32_alias *) (g_tab + cbs + e * DIM);
+#pragma unroll
+		for (int i = 0; i < DIM / 2; i++) {
+			const uint32_t w2 = row[i];
+			x[2 * i] = (int16_t) (w2 & 0xffff);
+			x[2 * i + 1] = (int16_t) (w2 >> 16);
+		}
+		const uint32_t pr = lq_wmse<DIM>(wr, x, ct);
+		const int16_t h = (int16_t) (pr & 0xffff), f = (int16_t) (pr >> 16);
+		const Word16 lmax = lk[LSP_VQ_CAND - 1];
+		const Word16 d = (h >= lmax) ? (Word16) SW_MAX_ : f;
+		const bool keep = d < lmax;
+		if (keep) {
+#pragma unroll
+			for (int k = LSP_VQ_CAND - 1; k >= 0; k--) {
+				const int16_t prev = k > 0 ? lk[k - 1] : (int16_t) -32768;
+				lk[k] = (prev > d) ? prev : ((lk[k] > d) ? d : lk[k]);
+			}
+		}
+		if (keep || all) {
+			db.put(v * 2 * LQ_SCAP + 2 * ns, (uint32_t) ((c << 9) | e));
+			db.put(v * 2 * LQ_SCAP + 2 * ns + 1, pr);
+			ns++;
+		}
+		if (++e == size) {
+			e = 0;
+			c++;
+			fresh = true;
+		}
+	}
+	xc.put(b + XL_NS + v, (int16_t) ns);
+}
+#endif
+
 /* the interpolation search over pairs [20v, 20v + 20) (qnt12.c:1019-1063,
  * the general chain: any weights) */
 template <class X>
@@ -535,6 +618,19 @@ MD void lq_compute(X &xc, int b, D &db, int v)
 	for (int i = 0; i < s; i++)
 		cbs += xc.get(b + XL_SIZES + i) * dim;
 	const int size = xc.get(b + XL_SIZES + s);
+#if MELPE_LQ_GATHER
+	for (;;) {	/* one pass per dimension */
+		const int udim = wave_first(dim);
+		if (dim != udim)
+			continue;
+		if (udim == 2 * LPC_ORD)
+			lq_vq_slice_g<2 * LPC_ORD>(xc, b, db, v, cbs, size, nc, s);
+		else
+			lq_vq_slice_g<LPC_ORD>(xc, b, db, v, cbs, size, nc, s);
+		break;
+	}
+	return;
+#endif
 	/* one pass per distinct (codebook stage, size, dim, candidates) among
 	 * the wave's channels, with those values wave-uniform inside: the
 	 * codebook rows come through the scalar cache (as lspVQ_t's scan) */
