@@ -55,7 +55,7 @@ namespace mlp {
 #define LQ_NV 4	/* slices per step (the schedule's virtual waves) */
 #define LQ_BATCH 16	/* stored pairs read per batch by the leader's scan */
 #ifndef MELPE_LQ_GATHER
-#define MELPE_LQ_GATHER 0
+#define MELPE_LQ_GATHER 1
 #endif
 #define LQ_SCAP (LQ_VISITS / LQ_NV)	/* stored visits per slice: every visit of the slice fits */
 static_assert(LQ_NV * 2 * LQ_SCAP <= LQ_ROW, "lsf slices exceed the score row");
@@ -486,7 +486,8 @@ MD void lq_vq_slice(X &xc, int b, D &db, int v, int cbs, int size, int nc, int s
 /* lq_vq_slice with the stage, size, candidates and codebook per lane: the
  * codebook rows are gathered through the vector memory path (dword loads,
  * the lsf codebooks' rows are 4-byte aligned) instead of one scalar-cache
- * pass per distinct stage among the wave's channels (experiment) */
+ * pass per distinct stage among the wave's channels (32,768 channels:
+ * 9.83 vs 9.95 ms per k_enc_ana_mw launch, profiles/r03_m_*) */
 template <int DIM, class X, class D>
 MD void lq_vq_slice_g(X &xc, int b, D &db, int v, int cbs, int size, int nc, int s)
 {
