@@ -89,50 +89,6 @@ enum {
 };
 static_assert(XP_END <= XS_WORDS, "pitch-VQ words overflow the lsf block");
 
-typedef int16_t __attribute__((__may_alias__)) i16_alias;
-
-/* int16 copy of a record field (no alignment beyond 2 assumed) */
-MD void lane_copy16(void *dst, const void *src, size_t bytes)
-{
-	i16_alias *d = (i16_alias *) dst;
-	const i16_alias *s = (const i16_alias *) src;
-	const int n = (int) (bytes / 2);
-	int i = 0;
-	for (; i + 32 <= n; i += 32) {	/* 32 loads in flight, as lane_copy32 */
-		int16_t v[32];
-#pragma unroll
-		for (int k = 0; k < 32; k++)
-			v[k] = s[i + k];
-#pragma unroll
-		for (int k = 0; k < 32; k++)
-			d[i + k] = v[k];
-	}
-	for (; i < n; i++)
-		d[i] = s[i];
-}
-
-/* dword copy (offsets and sizes multiples of 4), 32 loads in flight: the
- * record reads are one channel per lane, each its own cache line, so the
- * copy is latency-bound */
-MD void lane_copy32(void *dst, const void *src, size_t bytes)
-{
-	u32_alias *d = (u32_alias *) dst;
-	const u32_alias *s = (const u32_alias *) src;
-	const int n = (int) (bytes / 4);
-	int i = 0;
-	for (; i + 32 <= n; i += 32) {
-		uint32_t v[32];
-#pragma unroll
-		for (int k = 0; k < 32; k++)
-			v[k] = s[i + k];
-#pragma unroll
-		for (int k = 0; k < 32; k++)
-			d[i + k] = v[k];
-	}
-	for (; i < n; i++)
-		d[i] = s[i];
-}
-
 /* what v0 keeps from a frame's first phase for its second and the tail */
 struct AnaMwTmp {
 	int16_t peak[NF];

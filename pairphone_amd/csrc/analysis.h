@@ -1089,13 +1089,13 @@ MN void bpvc_band0(EncState *E, const int16_t *speech, const int16_t *fpitch, in
 
 /* band i = 1..4 of bpvc_ana (melp_sub.c:137-189): the band's window and
  * its envelope, each correlated at band 0's pitch; only band i's memories
- * and bpvc[i] are touched, so the four bands are independent chains */
-MN void bpvc_band(EncState *E, const int16_t *speech, int i, Word16 pitch, int16_t *bpvci)
+ * B and bpvc[i] are touched, so the four bands are independent chains.
+ * sp[0..FRAME) are the frame's new samples (`speech` + PITCH_FR - FRAME -
+ * PITCHMAX for bpvc_ana's `speech`). */
+MN void bpvc_band_s(BandState *B, const int16_t *sp, int i, Word16 pitch, int16_t *bpvci)
 {
 	int16_t sb[BPF_ORD + PITCH_FR];
 	Word16 pcorr, t, sc;
-	BandState *B = &E->band[i];
-	const int16_t *sp = &speech[PITCH_FR - FRAME - PITCHMAX];
 	int16_t *w = &sb[BPF_ORD];
 	const int fi = i * (BPF_ORD / 2) * 3;
 	bool ex;
@@ -1115,6 +1115,11 @@ MN void bpvc_band(EncState *E, const int16_t *speech, int i, Word16 pitch, int16
 	pcorr = sub(pcorr, 1638);
 	if (pcorr > *bpvci)
 		*bpvci = pcorr;
+}
+
+MN void bpvc_band(EncState *E, const int16_t *speech, int i, Word16 pitch, int16_t *bpvci)
+{
+	bpvc_band_s(&E->band[i], &speech[PITCH_FR - FRAME - PITCHMAX], i, pitch, bpvci);
 }
 
 /* bpvc_ana, melpe/melp_sub.c:77 */

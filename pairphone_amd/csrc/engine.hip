@@ -58,6 +58,8 @@ int melpe_tu_npp_upload(const void *blob, size_t bytes);
 int melpe_tu_ana_upload(const void *blob, size_t bytes);
 int melpe_tu_anamw_upload(const void *blob, size_t bytes);
 int melpe_tu_harm_upload(const void *blob, size_t bytes);
+int melpe_tu_band_upload(const void *blob, size_t bytes);
+int melpe_tu_lsf_upload(const void *blob, size_t bytes);
 int melpe_tu_dec_upload(const void *blob, size_t bytes);
 int melpe_tu_r24_upload(const void *blob, size_t bytes);
 int melpe_tu_r24_prof(uint64_t *acc);
@@ -65,6 +67,8 @@ int melpe_tu_npp_prof(uint64_t *acc);
 int melpe_tu_ana_prof(uint64_t *acc);
 int melpe_tu_anamw_prof(uint64_t *acc);
 int melpe_tu_harm_prof(uint64_t *acc);
+int melpe_tu_band_prof(uint64_t *acc);
+int melpe_tu_lsf_prof(uint64_t *acc);
 int melpe_tu_dec_prof(uint64_t *acc);
 int kl_npp(EncState *enc, int16_t *sp, int frames, int stride, const uint8_t *active, int n,
 	   int rate1200, hipStream_t s);
@@ -74,6 +78,12 @@ int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *a
 int kl_enc_harm(EncState *enc, const int16_t *res, const uint8_t *active, int n, const int *perm,
 		const int *nlive, hipStream_t s);
 int kl_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active, int n, const int *perm,
+		const int *nlive, int shift, hipStream_t s);
+int kl_enc_lsf(EncState *enc, const int16_t *aux, const uint8_t *active, int n, const int *perm,
+	       const int *nlive, hipStream_t s);
+int kl_enc_ana_part(EncState *enc, const int16_t *sp, int16_t *bw, int16_t *res, const uint8_t *active,
+		    int n, const int *perm, const int *nlive, int part, hipStream_t s);
+int kl_enc_band(EncState *enc, const int16_t *bw, const uint8_t *active, int n, const int *perm,
 		const int *nlive, hipStream_t s);
 int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
 		  const int *perm, const int *nlive, int nw, uint32_t *lqbuf, hipStream_t s);
@@ -620,6 +630,8 @@ struct melpe_engine {
 	int ana_waves = 0;	/* waves per 64 channels in k_enc_ana(_mw); 0: by channel count */
 	uint32_t *d_lq = nullptr;	/* k_enc_ana_mw's lsf_vq score rows, allocated on first use */
 	int16_t *d_res = nullptr;	/* the split lane analysis' windowed residuals (C x NF x LPC_FRAME) */
+	int16_t *d_bw = nullptr;	/* band 0's pitch and the peakiness flag per frame (C x NF x 2) */
+	int16_t *d_lw = nullptr;	/* lsf_vq's pattern and weights (C x LSF_AUX), k_lsf.hip */
 	/* one event per stream this engine's *_dev calls have used, recorded
 	 * after each call: the host-side calls wait on these (engine_wait)
 	 * instead of the whole device */
@@ -663,6 +675,33 @@ static bool harm_split(void)
 	return v != 0;
 }
 
+/* MELPE_BANDS=1: bands 1..4 of the voicing analysis in their own kernel
+ * (k_band.hip).  Bit-exact, but at 262,144 channels the three launches
+ * took 40.5 ms against 37.2 for k_enc_ana with the bands inside
+ * (profiles/r03_p_*), so it is off by default. */
+static bool band_split(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("MELPE_BANDS");
+		v = e && e[0] == '1';
+	}
+	return v != 0;
+}
+
+/* lsf_vq with a wave per channel (k_lsf.hip), the residuals formed in
+ * k_enc_harm; MELPE_LSFW=0 (diagnostics) keeps lsf_vq in k_enc_ana (and
+ * MELPE_BANDS=1 then applies) */
+static bool lsf_wave(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("MELPE_LSFW");
+		v = !(e && e[0] == '0');
+	}
+	return v != 0;
+}
+
 static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, const uint8_t *d_act,
 		      hipStream_t s)
 {
@@ -686,7 +725,26 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 		}
 	}
 	int rc;
-	if (nw == 1 && harm_split()) {
+	if (nw == 1 && harm_split() && lsf_wave()) {
+		/* frames and quantisers but lsf_vq (its pattern and weights into
+		 * d_lw), lsf_vq with a wave per channel (k_lsf.hip), the magnitudes
+		 * from residuals formed in k_enc_harm, then the history shift and
+		 * the packing */
+		if (!e->d_lw) {
+			er = hipMalloc(&e->d_lw, sizeof(int16_t) * LSF_AUX * (size_t) e->channels);
+			if (er != hipSuccess) {
+				e->d_lw = nullptr;
+				return (int) er;
+			}
+		}
+		rc = kl_enc_ana_part(e->d_enc, d_sp, e->d_lw, nullptr, d_act, e->channels, perm, nlive, 3, s);
+		if (rc == 0)
+			rc = kl_enc_lsf(e->d_enc, e->d_lw, d_act, e->channels, perm, nlive, s);
+		if (rc == 0)
+			rc = kl_enc_harm(e->d_enc, nullptr, d_act, e->channels, perm, nlive, s);
+		if (rc == 0)
+			rc = kl_enc_tail(e->d_enc, d_bits, d_act, e->channels, perm, nlive, 1, s);
+	} else if (nw == 1 && harm_split()) {
 		/* lane-per-channel analysis up to the Fourier magnitudes, the
 		 * magnitudes with a wave per channel, then the packing (k_harm.hip) */
 		if (!e->d_res) {
@@ -696,11 +754,29 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 				return (int) er;
 			}
 		}
-		rc = kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, e->d_res, s);
+		if (band_split()) {
+			/* the frames with band 0, bands 1..4 with four lanes per
+			 * channel, then the superframe (k_band.hip) */
+			if (!e->d_bw) {
+				er = hipMalloc(&e->d_bw, sizeof(int16_t) * 2 * NF * (size_t) e->channels);
+				if (er != hipSuccess) {
+					e->d_bw = nullptr;
+					return (int) er;
+				}
+			}
+			rc = kl_enc_ana_part(e->d_enc, d_sp, e->d_bw, nullptr, d_act, e->channels, perm, nlive, 1, s);
+			if (rc == 0)
+				rc = kl_enc_band(e->d_enc, e->d_bw, d_act, e->channels, perm, nlive, s);
+			if (rc == 0)
+				rc = kl_enc_ana_part(e->d_enc, nullptr, nullptr, e->d_res, d_act, e->channels, perm,
+						     nlive, 2, s);
+		} else {
+			rc = kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, e->d_res, s);
+		}
 		if (rc == 0)
 			rc = kl_enc_harm(e->d_enc, e->d_res, d_act, e->channels, perm, nlive, s);
 		if (rc == 0)
-			rc = kl_enc_tail(e->d_enc, d_bits, d_act, e->channels, perm, nlive, s);
+			rc = kl_enc_tail(e->d_enc, d_bits, d_act, e->channels, perm, nlive, 0, s);
 	} else {
 		rc = nw == 1 ? kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nullptr, s)
 			     : kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nw,
@@ -745,6 +821,7 @@ static int ensure_device_tables(int dev)
 	DEVGUARD(dev);
 	int (*up[])(const void *, size_t) = {melpe_tu_eng_upload, melpe_tu_npp_upload,
 					     melpe_tu_ana_upload, melpe_tu_anamw_upload, melpe_tu_harm_upload,
+					     melpe_tu_band_upload, melpe_tu_lsf_upload,
 					     melpe_tu_dec_upload,
 					     melpe_tu_r24_upload};
 	for (auto f : up)
@@ -884,6 +961,8 @@ int melpe_engine_destroy(melpe_engine *e)
 	hipFree(e->bin_dec.perm);
 	hipFree(e->d_lq);
 	hipFree(e->d_res);
+	hipFree(e->d_bw);
+	hipFree(e->d_lw);
 	for (auto &m : e->marks)
 		hipEventDestroy(m.second);
 	if (e->bin_enc.done)
@@ -1303,7 +1382,7 @@ int melpe_prof_read(uint64_t *out, int n)
 {
 	uint64_t acc[MELPE_PROF_SLOTS_ABI] = {0};
 	int (*rd[])(uint64_t *) = {melpe_tu_eng_prof, melpe_tu_npp_prof, melpe_tu_ana_prof, melpe_tu_anamw_prof,
-				   melpe_tu_harm_prof,
+				   melpe_tu_harm_prof, melpe_tu_band_prof, melpe_tu_lsf_prof,
 				   melpe_tu_dec_prof, melpe_tu_r24_prof};
 	for (auto f : rd)
 		if (f(acc))

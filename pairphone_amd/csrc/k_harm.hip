@@ -22,20 +22,17 @@ MELPE_TU(harm)
 using namespace mlp::wv;
 
 /* find_harm_fft + find_harm_mag (analysis.h) of one frame, the windowed
- * residual w[0..LPC_FRAME) in global memory, the result into fsmag[0..10) */
-MD void wv_find_harm(const int16_t *w, int16_t *fsmag, Word16 pitch, uint32_t *x, const WvConst *kc,
+ * residual's samples lane + 64 t in v[t] (0 past LPC_FRAME), the result
+ * into fsmag[0..10) */
+MD void wv_find_harm(const int16_t v[4], int16_t *fsmag, Word16 pitch, uint32_t *x, const WvConst *kc,
 		     int lane)
 {
 	int16_t *d0 = (int16_t *) x;	/* 256 complex points, re / im interleaved */
 	/* the input's max |x|, its scale, the packed points zero padded */
 	int mx = 0;
-	int16_t v[4];
 #pragma unroll
-	for (int t = 0; t < 4; t++) {
-		const int i = lane + WV * t;
-		v[t] = i < LPC_FRAME ? w[i] : (int16_t) 0;
+	for (int t = 0; t < 4; t++)
 		mx = max(mx, (int) abs_s(v[t]));
-	}
 	const Word16 sh = norm_s((Word16) wmax(mx));
 #pragma unroll
 	for (int t = 0; t < 8; t++) {
@@ -140,8 +137,18 @@ MD void wv_find_harm(const int16_t *w, int16_t *fsmag, Word16 pitch, uint32_t *x
 	wsync();
 }
 
+/* RESID: the windowed residuals formed here, from the record's hpspeech
+ * and quantised LSFs (encoder.h ana_resid_sample, one sample per lane and
+ * step), the last voiced frame's left in sigbuf as analysis_a leaves it;
+ * else read from res (k_enc_ana mode 1). */
+struct HarmLane {
+	uint8_t guard[FLAT_GUARD_BYTES];
+	int16_t lpc[LPC_ORD + 1];
+};
+
 /* one wave per live channel: slot g runs channel perm[g] (the engine's
  * lane order) or channel g under the mask; the three frames in order */
+template <bool RESID>
 __global__ __launch_bounds__(WAVE) void k_enc_harm(EncState *enc, const int16_t *res,
 						   const uint8_t *active, int n, const int *perm,
 						   const int *nlive)
@@ -166,14 +173,43 @@ __global__ __launch_bounds__(WAVE) void k_enc_harm(EncState *enc, const int16_t 
 				par->fs_mag[lane] = 8192;
 			continue;
 		}
-		wv_find_harm(res + ((size_t) c * NF + i) * LPC_FRAME, par->fs_mag, pitch, x, &kc, lane);
+		int16_t v[4];
+		if (RESID) {
+			HarmLane L;
+			PIN_FRAME(L);
+			L.lpc[0] = 4096;
+			lpc_lsp2pred(par->lsf, &L.lpc[1], LPC_ORD);
+			int16_t lc[LPC_ORD + 1];
+#pragma unroll
+			for (int j = 0; j <= LPC_ORD; j++)
+				lc[j] = L.lpc[j];
+#pragma unroll
+			for (int t = 0; t < 4; t++) {
+				const int k = lane + WV * t;
+				v[t] = k < LPC_FRAME ? ana_resid_sample(enc[c].hpspeech, lc, i, k) : (int16_t) 0;
+				if (k < LPC_FRAME)
+					enc[c].sigbuf[k] = v[t];
+			}
+		} else {
+			const int16_t *w = res + ((size_t) c * NF + i) * LPC_FRAME;
+#pragma unroll
+			for (int t = 0; t < 4; t++) {
+				const int k = lane + WV * t;
+				v[t] = k < LPC_FRAME ? w[k] : (int16_t) 0;
+			}
+		}
+		wv_find_harm(v, par->fs_mag, pitch, x, &kc, lane);
 	}
 }
 
+/* res == nullptr: the residuals formed in the kernel (RESID) */
 extern "C" int kl_enc_harm(EncState *enc, const int16_t *res, const uint8_t *active, int n,
 			   const int *perm, const int *nlive, hipStream_t s)
 {
-	k_enc_harm<<<n, WAVE, 0, s>>>(enc, res, active, n, perm, nlive);
+	if (res)
+		k_enc_harm<false><<<n, WAVE, 0, s>>>(enc, res, active, n, perm, nlive);
+	else
+		k_enc_harm<true><<<n, WAVE, 0, s>>>(enc, res, active, n, perm, nlive);
 	return (int) hipGetLastError();
 }
 
@@ -185,7 +221,7 @@ struct TailLane {
 };
 
 __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active,
-						   int n, const int *perm, const int *nlive)
+						   int n, const int *perm, const int *nlive, int shift)
 {
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (perm) {
@@ -205,6 +241,8 @@ __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bi
 	static_assert(o % 4 == 0 && e % 4 == 0, "the tail's record ranges are dword copies");
 	lane_copy((char *) &L.S + o, (const char *) &enc[c] + o, e - o);
 	lane_copy((char *) &L.S + o2, (const char *) &enc[c] + o2, e2 - o2);
+	if (shift)	/* ana_shift on the record (the residuals are formed) */
+		lane_copy16(enc[c].hpspeech, &enc[c].hpspeech[NF * FRAME], sizeof(int16_t) * IN_BEG);
 	analysis_b(&L.S);
 	lane_copy((char *) &enc[c] + o, (const char *) &L.S + o, e - o);
 	lane_copy((char *) &enc[c] + o2, (const char *) &L.S + o2, e2 - o2);
@@ -213,8 +251,8 @@ __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bi
 }
 
 extern "C" int kl_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active, int n,
-			   const int *perm, const int *nlive, hipStream_t s)
+			   const int *perm, const int *nlive, int shift, hipStream_t s)
 {
-	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(enc, bits, active, n, perm, nlive);
+	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(enc, bits, active, n, perm, nlive, shift);
 	return (int) hipGetLastError();
 }

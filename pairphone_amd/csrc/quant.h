@@ -561,8 +561,17 @@ MD Word32 lsf_werr(Word32 acc, Word16 w)
 	return L_shl(r, sub(t1, 3));
 }
 
-/* lsf_vq :895 */
-MN void lsf_vq(EncState *E, MelpParam *par)
+/* the voicing pattern lsf_vq branches on (qnt12.c:934-941): frame 0 in bit 2 */
+MD Word16 lsf_uvc(const MelpParam *par)
+{
+	Word16 uvc = 0;
+	for (int i = 0; i < NF; i++)
+		uvc = (Word16) ((uvc << 1) | (par[i].uv_flag ? 1 : 0));
+	return uvc;
+}
+
+/* lsf_vq :895, on the voicing pattern uvc (lsf_uvc of the flags it sees) */
+MN void lsf_vq_u(EncState *E, MelpParam *par, Word16 uvc)
 {
 	PROF_SCOPE(9);
 	QuantParam *q = &E->qpar;
@@ -593,17 +602,10 @@ MN void lsf_vq(EncState *E, MelpParam *par)
 		vq_lspw(wgt[i], lsp(i), lpc, LPC_ORD);
 	}
 	}
-	Word16 uvc = 0;
-	for (int i = 0; i < NF; i++) {
-		uvc = shl(uvc, 1);
-		if (par[i].uv_flag) {
-			uvc |= 1;
-			if (i == 0)
-				v_scale(wgt[0], 6554, LPC_ORD);
-			else if (i == 1)
-				v_scale(wgt[1], 6554, LPC_ORD);
-		}
-	}
+	if (uvc & 4)
+		v_scale(wgt[0], 6554, LPC_ORD);
+	if (uvc & 2)
+		v_scale(wgt[1], 6554, LPC_ORD);
 	/* One call site per quantisation, its codebook chosen per lane: the
 	 * lanes of a wave carry different voicing patterns, and a call site per
 	 * (branch, codebook) ran each scan once per site the wave's lanes
@@ -747,6 +749,11 @@ MN void lsf_vq(EncState *E, MelpParam *par)
 		lspSort(lsp(2), LPC_ORD);
 	v_copy(E->qplsp, lsp(2), LPC_ORD);
 #undef lsp
+}
+
+MN void lsf_vq(EncState *E, MelpParam *par)
+{
+	lsf_vq_u(E, par, lsf_uvc(par));
 }
 
 /* quant_jitter :1198 */

@@ -199,39 +199,46 @@ def test_single_stream_dropin_matches_golden():
     assert np.concatenate(out).tobytes() == bytes.fromhex(g["bits_hex"][0])[:nsf * 11]
 
 
-def emu_encode_split(x, nsf):
+def emu_encode_split(x, nsf, fn="emu_encode_ana_split"):
     """the split lane analysis (encoder.h analysis_a / analysis_b, as
-    k_enc_ana / k_enc_harm / k_enc_tail run it), NPP first"""
+    k_enc_ana / k_enc_harm / k_enc_tail run it; fn="emu_encode_ana_split3":
+    with the voicing bands 1..4 in k_enc_band's chains), NPP first"""
     lib = emu()
     lib.emu_encode_npp.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    lib.emu_encode_ana_split.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    f = getattr(lib, fn)
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     e = lib.emu_create(x.shape[0])
 
     def enc(sp):
         b = np.zeros((x.shape[0], 11), np.uint8)
         lib.emu_encode_npp(e, sp.ctypes.data)
-        assert lib.emu_encode_ana_split(e, b.ctypes.data, sp.ctypes.data) == 0
+        assert f(e, b.ctypes.data, sp.ctypes.data) == 0
         return b
     out = run_superframes(enc, x, nsf)
     lib.emu_destroy(e)
     return out
 
 
-def test_split_analysis_hostemu_matches_golden():
-    """8 golden channels x 10 s through analysis_a, find_harm on the written
-    residuals, analysis_b: the goldens' bits and NPP samples"""
+@pytest.mark.parametrize("fn", ["emu_encode_ana_split", "emu_encode_ana_split3",
+                                "emu_encode_ana_split4"])
+def test_split_analysis_hostemu_matches_golden(fn):
+    """8 golden channels x 10 s through analysis_a (or analysis_a1, the band
+    chains, analysis_a2), find_harm on the written residuals, analysis_b:
+    the goldens' bits and NPP samples"""
     g = golden()
     ch, nsf = 8, g["superframes"]
-    bits, npp = emu_encode_split(signals(g["seed"], ch, nsf), nsf)
+    bits, npp = emu_encode_split(signals(g["seed"], ch, nsf), nsf, fn)
     for c in range(ch):
         assert sha(bits[c]) == g["bits_sha256"][c], "channel %d bits" % c
         assert sha(npp[c]) == g["npp_sha256"][c], "channel %d npp" % c
 
 
-def test_split_analysis_hostemu_edge_signals_match_serial():
+@pytest.mark.parametrize("fn", ["emu_encode_ana_split", "emu_encode_ana_split3",
+                                "emu_encode_ana_split4"])
+def test_split_analysis_hostemu_edge_signals_match_serial(fn):
     nsf = 16
     sig = edge_signals(nsf * 540)
     x = np.stack([sig[k] for k in sorted(sig)])
     want, _ = emu_encode_all(x.copy(), nsf)
-    got, _ = emu_encode_split(x.copy(), nsf)
+    got, _ = emu_encode_split(x.copy(), nsf, fn)
     np.testing.assert_array_equal(got, want)
