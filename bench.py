@@ -73,7 +73,9 @@ REF_TOOL = os.path.join(ROOT, "oracle", "_ref", "ref_tool")
 # the kernels of one analysis launch (encode_ana_dev): the lane-per-channel
 # analysis split around the wave-per-channel Fourier magnitudes (k_harm.hip),
 # or the multi-wave kernel at the channel counts the engine runs it
-ANALYSIS_KERNELS = ("k_enc_ana", "k_enc_ana<true>", "k_enc_ana<false>", "k_enc_harm", "k_enc_tail",
+ANALYSIS_KERNELS = ("k_enc_ana", "k_enc_ana<true>", "k_enc_ana<false>", "k_enc_ana<0>", "k_enc_ana<1>",
+                    "k_enc_ana<2>", "k_enc_ana<3>", "k_enc_ana<4>", "k_enc_lsf", "k_enc_band",
+                    "k_enc_harm", "k_enc_harm<true>", "k_enc_harm<false>", "k_enc_tail",
                     "k_enc_ana_mw<4>")
 
 

@@ -1898,6 +1898,51 @@ MN void lpc_lsp2pred(int16_t *lsf, int16_t *lpc, int order)
 	}
 }
 
+/* lpc_lsp2pred for order 10 on registers: lsf[] is lpc_clmp(lsf, 0, 10)'s
+ * result on entry -- with delta 0 the clamp is its bubble sort alone (the
+ * separation pass finds no gap below 0), done here as nine branch-free
+ * passes -- and the recursion is lpc_lsp2pred's, unrolled */
+MD void lsf_sort10(int16_t *l)
+{
+#pragma unroll
+	for (int p = 0; p < 9; p++)
+#pragma unroll
+		for (int i = 0; i < 9; i++) {
+			const int16_t a = l[i], b = l[i + 1];
+			l[i] = a > b ? b : a;
+			l[i + 1] = a > b ? a : b;
+		}
+}
+
+MD void lsp2pred10(const int16_t *lsf, int16_t *lpc)
+{
+	Word32 f0[6], f1[6];
+	f0[0] = f1[0] = 33554431L;
+	f0[1] = L_shr(L_deposit_h(negate(cos_fxp(lsf[0]))), 5);
+	f1[1] = L_shr(L_deposit_h(negate(cos_fxp(lsf[1]))), 5);
+#pragma unroll
+	for (int i = 2; i <= 5; i++) {
+		const Word16 c0 = negate(cos_fxp(lsf[2 * i - 2]));
+		const Word16 c1 = negate(cos_fxp(lsf[2 * i - 1]));
+		f0[i] = f0[i - 2];
+		f1[i] = f1[i - 2];
+#pragma unroll
+		for (int j = i; j >= 2; j--) {
+			f0[j] = L_add(f0[j], L_add(L_shl(L_mpy_ls(f0[j - 1], c0), 1), f0[j - 2]));
+			f1[j] = L_add(f1[j], L_add(L_shl(L_mpy_ls(f1[j - 1], c1), 1), f1[j - 2]));
+		}
+		f0[1] = L_add(f0[1], L_shl(L_mpy_ls(f0[0], c0), 1));
+		f1[1] = L_add(f1[1], L_shl(L_mpy_ls(f1[0], c1), 1));
+	}
+#pragma unroll
+	for (int i = 4; i >= 0; i--) {
+		f0[i + 1] = L_add(f0[i + 1], f0[i]);
+		f1[i + 1] = L_sub(f1[i + 1], f1[i]);
+		lpc[i] = extract_h(L_shl(L_add(f0[i + 1], f1[i + 1]), 2));
+		lpc[9 - i] = extract_h(L_shl(L_sub(f0[i + 1], f1[i + 1]), 2));
+	}
+}
+
 /* lpc_syn :922 -- all-pole synthesis, y[-order..-1] is the memory; the
  * order-10 case keeps coefficients and the output history in registers */
 MD void lpc_syn(const int16_t *x, int16_t *y, const int16_t *a, int order, int n)

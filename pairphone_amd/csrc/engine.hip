@@ -689,15 +689,15 @@ static bool band_split(void)
 	return v != 0;
 }
 
-/* lsf_vq with a wave per channel (k_lsf.hip), the residuals formed in
- * k_enc_harm; MELPE_LSFW=0 (diagnostics) keeps lsf_vq in k_enc_ana (and
- * MELPE_BANDS=1 then applies) */
+/* MELPE_LSFW=1: lsf_vq with a wave per channel (k_lsf.hip), the residuals
+ * formed in k_enc_harm; else lsf_vq stays in k_enc_ana (and MELPE_BANDS=1
+ * applies) */
 static bool lsf_wave(void)
 {
 	static int v = -1;
 	if (v < 0) {
 		const char *e = getenv("MELPE_LSFW");
-		v = !(e && e[0] == '0');
+		v = e && e[0] == '1';
 	}
 	return v != 0;
 }

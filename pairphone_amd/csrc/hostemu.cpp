@@ -188,7 +188,8 @@ int emu_encode_ana_split4(emu_engine *e, unsigned char *bits, const int16_t *sp)
 				continue;
 			int16_t lpc[LPC_ORD + 1];
 			lpc[0] = 4096;
-			lpc_lsp2pred(par->lsf, &lpc[1], LPC_ORD);
+			lsf_sort10(par->lsf);	/* as k_enc_harm: lpc_lsp2pred's clamp */
+			lsp2pred10(par->lsf, &lpc[1]);
 			for (int n = 0; n < LPC_FRAME; n++)
 				w[n] = ana_resid_sample(E->hpspeech, lpc, i, n);
 			v_copy(E->sigbuf, w, LPC_FRAME);

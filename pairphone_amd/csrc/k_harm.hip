@@ -141,11 +141,6 @@ MD void wv_find_harm(const int16_t v[4], int16_t *fsmag, Word16 pitch, uint32_t 
  * and quantised LSFs (encoder.h ana_resid_sample, one sample per lane and
  * step), the last voiced frame's left in sigbuf as analysis_a leaves it;
  * else read from res (k_enc_ana mode 1). */
-struct HarmLane {
-	uint8_t guard[FLAT_GUARD_BYTES];
-	int16_t lpc[LPC_ORD + 1];
-};
-
 /* one wave per live channel: slot g runs channel perm[g] (the engine's
  * lane order) or channel g under the mask; the three frames in order */
 template <bool RESID>
@@ -175,14 +170,22 @@ __global__ __launch_bounds__(WAVE) void k_enc_harm(EncState *enc, const int16_t 
 		}
 		int16_t v[4];
 		if (RESID) {
-			HarmLane L;
-			PIN_FRAME(L);
-			L.lpc[0] = 4096;
-			lpc_lsp2pred(par->lsf, &L.lpc[1], LPC_ORD);
-			int16_t lc[LPC_ORD + 1];
+			/* lpc_lsp2pred on registers (dsp.h lsp2pred10), its clamp
+			 * written back as the reference's writes it */
+			int16_t l[LPC_ORD], lc[LPC_ORD + 1];
 #pragma unroll
-			for (int j = 0; j <= LPC_ORD; j++)
-				lc[j] = L.lpc[j];
+			for (int j = 0; j < LPC_ORD; j++)
+				l[j] = par->lsf[j];
+			lsf_sort10(l);
+			if (lane < LPC_ORD) {
+				int16_t v = 0;
+#pragma unroll
+				for (int j = 0; j < LPC_ORD; j++)
+					v = lane == j ? l[j] : v;
+				par->lsf[lane] = v;
+			}
+			lc[0] = 4096;
+			lsp2pred10(l, &lc[1]);
 #pragma unroll
 			for (int t = 0; t < 4; t++) {
 				const int k = lane + WV * t;
