@@ -15,6 +15,7 @@ import hashlib
 import json
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -112,6 +113,33 @@ def test_encode_gpu_1024_channels_match_golden():
     badn = [c for c in range(C) if sha(npp[c]) != g["npp_sha256"][c]]
     assert not bad, "bitstream mismatch on %d channels, first %s" % (len(bad), bad[:8])
     assert not badn, "NPP output mismatch on %d channels, first %s" % (len(badn), badn[:8])
+
+
+_OPT_IN_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[1] + "/tests")
+import test_encode as t
+from pairphone_amd import MelpeEngine
+g = t.golden()
+C, nsf = g["channels"], g["superframes"]
+bits, npp = t.run_superframes(MelpeEngine(C).encode, t.signals(g["seed"], C, nsf), nsf)
+bad = [c for c in range(C) if t.sha(bits[c]) != g["bits_sha256"][c] or t.sha(npp[c]) != g["npp_sha256"][c]]
+print("mismatch", len(bad), bad[:8])
+sys.exit(1 if bad else 0)
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", ["MELPE_LSFW", "MELPE_BANDS"])
+def test_encode_gpu_opt_in_analysis_splits_match_golden(env):
+    """the opt-in launch orders of the lane analysis (lsf_vq on a wave per
+    channel, k_lsf.hip; the voicing bands on four lanes per channel,
+    k_band.hip), read once per process: a child process per order runs the
+    1024-channel goldens"""
+    r = subprocess.run([sys.executable, "-c", _OPT_IN_CHILD, ROOT], env=dict(os.environ, **{env: "1"}),
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
 def edge_signals(n):
