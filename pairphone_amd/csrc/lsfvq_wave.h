@@ -42,8 +42,6 @@ struct LsfShared {
 	int16_t lcand[LSP_INP_CAND][LPC_ORD], lidx[LSP_INP_CAND * LSP_VQ_STAGES];
 	int16_t lsf_index[NF][MAX_LSF_STAGE];
 	int16_t cand[LSP_VQ_CAND][2 * LPC_ORD];
-	int16_t index[LSP_VQ_CAND][LSP_VQ_STAGES], nextIndex[LSP_VQ_CAND][LSP_VQ_STAGES];
-	int16_t rows[LSP_VQ_CAND][LSP_VQ_STAGES];
 };
 
 /* lspVQ of one channel across the wave; cand: LDS, LSP_VQ_CAND rows */
@@ -52,17 +50,26 @@ MD void lspVQ_wv(const int16_t *target, const int16_t *weight, int16_t *qout, co
 		 const int16_t *cb_size, int16_t *cb_index, bool flag, LsfShared *W, int lane)
 {
 	int16_t (*cand)[2 * LPC_ORD] = W->cand;
-	int16_t (*index)[LSP_VQ_STAGES] = W->index, (*nextIndex)[LSP_VQ_STAGES] = W->nextIndex;
-	int16_t (*rows)[LSP_VQ_STAGES] = W->rows;
+	/* the candidates' stage indices, row k's stage s in bits 16 s of
+	 * ix[k] (index[][]) and nx[k] (nextIndex[][]): wave-uniform registers */
+	uint64_t ix[LSP_VQ_CAND], nx[LSP_VQ_CAND];
+	auto pick = [](const uint64_t *a, int k) {
+		uint64_t v = a[0];
+#pragma unroll
+		for (int q = 1; q < LSP_VQ_CAND; q++)
+			v = k == q ? a[q] : v;
+		return v;
+	};
+	auto fld = [](uint64_t r, int st) { return (int16_t) (r >> (16 * st)); };
 	int16_t wr[DIM], tg[DIM];
 #pragma unroll
 	for (int i = 0; i < DIM; i++) {
 		wr[i] = weight[i];
 		tg[i] = target[i];
 	}
+#pragma unroll
 	for (int k = 0; k < LSP_VQ_CAND; k++)
-		for (int i = 0; i < LSP_VQ_STAGES; i++)
-			index[k][i] = nextIndex[k][i] = 0;
+		ix[k] = nx[k] = 0;
 	for (int t = lane; t < LSP_VQ_CAND * 2 * LPC_ORD; t += WV)
 		cand[t / (2 * LPC_ORD)][t % (2 * LPC_ORD)] = 0;
 	wsync();
@@ -120,21 +127,18 @@ MD void lspVQ_wv(const int16_t *target, const int16_t *weight, int16_t *qout, co
 			}
 		}
 		{
+			/* InsertCand's rows (:735-788) from the keys' tags */
+			uint64_t rw[LSP_VQ_CAND];
+			const uint64_t lo = (1ull << (16 * s1)) - 1;
+#pragma unroll
 			for (int k = 0; k < LSP_VQ_CAND; k++) {
 				const int t = key[k] & 0xffff;
-				if (!(t & 0x8000)) {
-					const int c1 = t >> 9;
-					for (int i = 0; i < s1; i++)
-						rows[k][i] = index[c1][i];
-					rows[k][s1] = (int16_t) (t & 511);
-				} else {
-					for (int i = 0; i <= s1; i++)
-						rows[k][i] = nextIndex[t & 0x7fff][i];
-				}
+				rw[k] = (t & 0x8000) ? pick(nx, t & 7)
+						     : ((pick(ix, t >> 9) & lo) | ((uint64_t) (t & 511) << (16 * s1)));
 			}
+#pragma unroll
 			for (int k = 0; k < LSP_VQ_CAND; k++)
-				for (int i = 0; i <= s1; i++)
-					nextIndex[k][i] = rows[k][i];
+				nx[k] = rw[k];
 		}
 		if (!flag && s1 == tos - 1) {
 			ncPrev = 1;
@@ -143,9 +147,10 @@ MD void lspVQ_wv(const int16_t *target, const int16_t *weight, int16_t *qout, co
 			Word16 t2 = (s1 == tos - 1) ? LSP_INP_CAND : LSP_VQ_CAND;
 			ncPrev = t1 < t2 ? t1 : t2;
 		}
-		for (int c1 = 0; c1 < ncPrev; c1++)
-			for (int i = 0; i <= s1; i++)
-				index[c1][i] = nextIndex[c1][i];
+#pragma unroll
+		for (int c1 = 0; c1 < LSP_VQ_CAND; c1++)
+			if (c1 < ncPrev)
+				ix[c1] = nx[c1];
 		/* the new candidates, one element per lane: the stages' rows added
 		 * in stage order (v_add) from zero */
 		wsync();
@@ -154,7 +159,7 @@ MD void lspVQ_wv(const int16_t *target, const int16_t *weight, int16_t *qout, co
 			const int16_t *p2 = cb;
 			Word16 v = 0;
 			for (int st = 0; st <= s1; st++) {
-				Word16 o = extract_l(L_shr(L_mult(index[c1][st], (Word16) DIM), 1));
+				Word16 o = extract_l(L_shr(L_mult(fld(pick(ix, c1), st), (Word16) DIM), 1));
 				v = add(v, p2[o + i]);
 				p2 += extract_l(L_shr(L_mult(cb_size[st], (Word16) DIM), 1));
 			}
@@ -163,12 +168,11 @@ MD void lspVQ_wv(const int16_t *target, const int16_t *weight, int16_t *qout, co
 		wsync();
 		cbo += size * DIM;
 	}
-	for (int i = 0; i < ncPrev; i++) {
-		for (int k = 0; k < tos; k++)
-			cb_index[i * tos + k] = index[i][k];
-		for (int j = 0; j < DIM; j++)
-			qout[i * DIM + j] = cand[i][j];
-	}
+	/* one lane per element */
+	for (int t = lane; t < ncPrev * tos; t += WV)
+		cb_index[t] = fld(pick(ix, t / tos), t % tos);
+	for (int t = lane; t < ncPrev * DIM; t += WV)
+		qout[t] = cand[t / DIM][t % DIM];
 	wsync();
 }
 
@@ -209,7 +213,8 @@ MD void lsf_interp_wv(const LsfShared *W, int *cand, int16_t *inp, int16_t *best
 	const int pr = (int) (bk & 127);
 	*cand = pr >> 4;
 	*inp = (int16_t) (pr & 15);
-	for (int j = 0; j < LPC_ORD; j++) {
+	if (lane < LPC_ORD) {	/* one lane per element */
+		const int j = lane;
 		Word16 f = ic[*inp * 20 + j];
 		Word32 acc = L_mac(L_mult(f, W->qplsp[j]), sub(16384, f), W->lcand[*cand][j]);
 		best0[j] = extract_h(L_shl(acc, 1));
@@ -265,21 +270,23 @@ MD void lsf_vq_wv(EncState *E, const int16_t *aux, LsfShared *W, int lane)
 		int16_t inp;
 		lsf_interp_wv(W, &cnd, &inp, W->best0, W->best1, lane);
 		wsync();
-		for (int i = 0; i < LPC_ORD; i++)
+		if (lane < LPC_ORD) {	/* one lane per element */
+			const int i = lane;
 			lsp(2)[i] = W->lcand[cnd][i];
-		for (int k = 0; k < tos; k++)
-			W->lsf_index[0][k] = W->lidx[cnd * tos + k];
-		W->lsf_index[1][0] = inp;
-		for (int i = 0; i < LPC_ORD; i++) {
 			W->res[i] = shl(sub(lsp(0)[i], W->best0[i]), 2);
 			W->res[i + LPC_ORD] = shl(sub(lsp(1)[i], W->best1[i]), 2);
 			W->mwgt[i] = W->wgt[0][i];
 			W->mwgt[i + LPC_ORD] = W->wgt[1][i];
+			if (i < tos)
+				W->lsf_index[0][i] = W->lidx[cnd * tos + i];
+			if (i == 0)
+				W->lsf_index[1][0] = inp;
 		}
 		wsync();
 		lspVQ_wv<2 * LPC_ORD>(W->res, W->mwgt, W->res, TB(res256x64x64x64), uvc == 1 ? 4 : 2,
 				      res_cb_size, W->lsf_index[2], false, W, lane);
-		for (int i = 0; i < LPC_ORD; i++) {
+		if (lane < LPC_ORD) {
+			const int i = lane;
 			lsp(0)[i] = add(shr(W->res[i], 2), W->best0[i]);
 			lsp(1)[i] = add(shr(W->res[i + LPC_ORD], 2), W->best1[i]);
 		}
