@@ -1,0 +1,10 @@
+# round-3 final set, part 4 (end of round): the whole GPU suite,
+# the default bench line with its CPU baseline curve, a kernel trace of the
+# default command, and PMC passes at 262,144 channels
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/$1 && export TMPDIR=/tmp &&
+timeout -k 10 900 python -u -m pytest -s tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/$1/full_tests.log 2>&1 &&
+timeout -k 10 900 python bench.py > gpurun_out/$1/bench.json 2> gpurun_out/$1/bench.err &&
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/$1/prof_kt -o kt -- python3 bench.py --no-cpu-baseline > gpurun_out/$1/kt_bench.json 2> gpurun_out/$1/kt_bench.err &&
+python3 tools/prof_summary.py gpurun_out/$1 r03_$1 > gpurun_out/$1/summary.log 2>&1 &&
+mkdir -p gpurun_out/$1/profiles && cp profiles/r03_$1_* gpurun_out/$1/profiles/ &&
+bash tools/gpu_r03_pmc.sh ${1}pmc 262144
