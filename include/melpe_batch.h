@@ -35,6 +35,11 @@
  * (the engine records an event on each stream it is given), and for nothing
  * else on the device.  To reset channels in stream order (no host sync), use
  * melpe_engine_reset_dev on the stream that carries the encode/decode work.
+ * One engine may be called from several host threads: its calls take a
+ * per-engine lock while they enqueue (the host side of a call is short; the
+ * device work is not serialised by it).  A call that fails after enqueueing
+ * part of its work still records its stream's event, so later host-side
+ * waits cover that work too.
  * Entry points restore the calling thread's current HIP device on return.
  */
 #ifndef MELPE_AMD_BATCH_H
@@ -80,6 +85,15 @@ int melpe_engine_set_lane_order(melpe_engine *e, int on);
  * count (4 up to 32,768 channels per engine, where every workgroup is
  * resident at once; 1 above).  Bits are the same either way. */
 int melpe_engine_set_ana_waves(melpe_engine *e, int waves);
+
+/* The live-count mapping of the automatic choice above 32,768 channels: a
+ * superframe with at most live_max live channels (ragged streams, paused
+ * channels) runs the four-wave analysis, more run one lane per channel.
+ * The count comes from the lane-order sort on the device, so it needs the
+ * lane order on (the default); the host never waits for it.  live_max is
+ * 0 .. 32,768 (default 32,768; 0 = by channel count only).  Bits are the
+ * same either way. */
+int melpe_engine_set_mw_live_max(melpe_engine *e, int live_max);
 
 /* Per-channel state records, for checkpoint / resume and for moving channels
  * between engines or GPUs (e.g. re-balancing ragged streams).  which: 1 =

@@ -55,12 +55,12 @@ def build_oracle():
 PROF_LIB = os.path.join(ROOT, "pairphone_amd", "libmelpe_amd_prof.so")
 
 
-TUS = ("engine", "k_npp", "k_ana", "k_ana_mw", "k_harm", "k_band", "k_lsf", "k_dec", "k_r24")
+TUS = ("engine", "k_npp", "k_ana", "k_ana_mw", "k_harm", "k_dec", "k_r24")
 # the codec TUs compile their whole call tree inline, so every access to a
 # lane's private state is a scratch_/global_ instruction with counted waits
 # instead of a generic FLAT access; this is what costs compile
 # time, hence one TU per kernel, compiled in parallel
-HOT_TUS = ("k_npp", "k_ana", "k_ana_mw", "k_harm", "k_band", "k_lsf", "k_dec", "k_r24")
+HOT_TUS = ("k_npp", "k_ana", "k_ana_mw", "k_harm", "k_dec", "k_r24")
 
 
 def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=HOT_TUS, only=None):
@@ -130,7 +130,7 @@ def device_disassembly(obj):
 # codec kernels that must not contain generic (FLAT) accesses: a FLAT access
 # to the private segment is aperture-checked before its offset is added,
 # which faulted on gfx950 (kern.h FLAT_GUARD_BYTES)
-NO_FLAT = ("k_enc_ana", "k_enc_harm", "k_enc_tail", "k_enc_band", "k_enc_lsf", "k_decode", "k_vad", "k_enc_npp", "k_npp",
+NO_FLAT = ("k_enc_ana", "k_enc_harm", "k_enc_tail", "k_decode", "k_vad", "k_enc_npp", "k_npp",
            "k_demodulate", "k_enc24",
            "k_dec24", "k_helpers_eval")
 

@@ -40,6 +40,7 @@ def load_library(path=None):
         "melpe_engine_reset_dev": (i32, [vp, vp, i32, vp]),
         "melpe_engine_set_lane_order": (i32, [vp, i32]),
         "melpe_engine_set_ana_waves": (i32, [vp, i32]),
+        "melpe_engine_set_mw_live_max": (i32, [vp, i32]),
         "melpe_engine_state_bytes": (ctypes.c_long, [i32]),
         "melpe_engine_export": (i32, [vp, i32, i32, i32, vp]),
         "melpe_engine_import": (i32, [vp, i32, i32, i32, vp]),
@@ -226,6 +227,12 @@ class MelpeEngine:
         4 waves per channel group (ana_mw.h), 0 = by channel count (results
         are the same either way)"""
         _check(self.lib.melpe_engine_set_ana_waves(self.h, int(waves)))
+
+    def set_mw_live_max(self, live_max):
+        """above 32,768 channels, superframes with at most live_max live
+        channels run the four-wave analysis (0 = off; results are the same
+        either way)"""
+        _check(self.lib.melpe_engine_set_mw_live_max(self.h, int(live_max)))
 
     def reset_dev(self, d_mask=None, which=3, stream=None):
         """reset enqueued on `stream` (ordered with the *_dev calls on it)"""

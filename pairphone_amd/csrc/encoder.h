@@ -58,7 +58,9 @@ MN Word16 global_pitch(const int16_t *speech, int16_t *sb, int16_t *delin, int16
 
 MN void ana_global_pitch(EncState *E, const int16_t *speech)
 {
+#if !defined(MELPE_KO_GPITCH)
 	E->fpitch[1] = global_pitch(speech, E->sigbuf, E->lpfsp_delin, E->lpfsp_delout);
+#endif
 }
 
 /* LPC analysis (melp_ana.c:366-393): ac[17] (the autocorrelation classify
@@ -147,14 +149,8 @@ MN void ana_pitch_gain(EncState *E, const int16_t *speech, MelpParam *par, Word1
 	E->fpitch[0] = E->fpitch[1];
 }
 
-/* bw != nullptr: the deferred-band form (analysis_a1): only band 0 of
- * bpvc_ana runs; bands 1..4 are left to ana_band_frames, which needs band
- * 0's pitch (bw[0]) and whether the peakiness forces bands 1-2 (bw[1]).
- * Nothing else in melp_ana reads bpvc[1..4] (ana_peaky only writes them),
- * so their values are the reference's once ana_band_frames has run. */
 template <bool R24>
-MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum,
-		 int16_t *bw = nullptr)
+MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
 {
 	PROF_SCOPE(1);
 	int16_t ac[17], lpc[LPC_ORD + 1];
@@ -164,13 +160,6 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum,
 #if defined(MELPE_KO_BPVC)
 	sub_pitch = E->fpitch[0];
 	v_set(par->bpvc, 0, NUM_BANDS);
-#elif !defined(MELPE_OPCOUNT)
-	if (bw) {
-		bpvc_init(E);
-		bpvc_band0(E, &speech[FRAME_END], E->fpitch, &par->bpvc[0], &sub_pitch);
-	} else {
-		bpvc_ana(E, &speech[FRAME_END], E->fpitch, par->bpvc, &sub_pitch);
-	}
 #else
 	bpvc_ana(E, &speech[FRAME_END], E->fpitch, par->bpvc, &sub_pitch);
 #endif
@@ -178,10 +167,6 @@ MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum,
 	ana_lpc<R24>(E, speech, ac, lpc, par->lsf);
 	const Word16 peak = ana_resid(E, speech, lpc);
 	ana_peaky(par->bpvc, peak, 0, 2);
-	if (bw) {
-		bw[0] = sub_pitch;
-		bw[1] = peak > 6553;
-	}
 	if (!R24) {
 		for (int i = 0; i < PIT_SUBNUM; i++) {
 			ana_track_pa(E, speech, subnum, i);
@@ -447,11 +432,11 @@ MN void sc_ana(EncState *E, MelpParam *par)
 /* analysis() in the two parts the GPU runs as separate kernels:
  * analysis_frame: dc removal and melp_ana of frame i (melp_ana.c:140-160);
  * analysis_tail: sc_ana, the quantisers and channel packing (:162-265) */
-MD void analysis_frame(EncState *E, const int16_t *sp_in, int i, int16_t *bw = nullptr)
+MD void analysis_frame(EncState *E, const int16_t *sp_in, int i)
 {
 	dc_rmv(&sp_in[i * FRAME], &E->hpspeech[IN_BEG + i * FRAME], E->dcdelin,
 	       E->dcdelout_hi, E->dcdelout_lo, FRAME);
-	melp_ana<false>(E, &E->hpspeech[i * FRAME], &E->par[i], i, bw);
+	melp_ana<false>(E, &E->hpspeech[i * FRAME], &E->par[i], i);
 }
 
 /* the Fourier magnitudes of frame i (melp_ana.c:224-236): the LPC residual
@@ -555,103 +540,12 @@ MN void analysis_a2(EncState *E, int16_t *res)
 
 MN void analysis_a(EncState *E, const int16_t *sp_in, int16_t *res)
 {
+#if defined(MELPE_KO_ANALYSIS)
+	return;
+#endif
 	for (int i = 0; i < NF; i++)
 		analysis_frame(E, sp_in, i);
 	analysis_a2(E, res);
-}
-
-/* analysis_a with bands 1..4 of bpvc_ana taken out (k_ana.hip k_enc_ana
- * mode 2 -> k_band.hip -> mode 3): analysis_a1 runs the frames with band 0
- * only and leaves bw[2 i .. 2 i + 1] per frame (melp_ana); ana_band_frames
- * then runs band j's chain over the three frames -- bands are independent
- * chains, each touching only its memories and bpvc[j] -- and analysis_a2
- * the superframe.  hpspeech is shifted only at the end of analysis_a2, so
- * the bands read the samples melp_ana's bpvc_ana would have. */
-MN void analysis_a1(EncState *E, const int16_t *sp_in, int16_t *bw)
-{
-	for (int i = 0; i < NF; i++)
-		analysis_frame(E, sp_in, i, bw + 2 * i);
-}
-
-/* band j = 1..4 of the superframe's three frames: B its memories, hp the
- * record's hpspeech (read only), par the record's (only bpvc[j] written) */
-MN void ana_band_frames(BandState *B, const int16_t *hp, int j, const int16_t *bw, MelpParam *par)
-{
-	for (int i = 0; i < NF; i++) {
-		int16_t x[FRAME], v;
-		lane_copy16(x, &hp[i * FRAME + FRAME_END + PITCH_FR - FRAME - PITCHMAX],
-			    sizeof(int16_t) * FRAME);
-		bpvc_band_s(B, x, j, bw[2 * i], &v);
-		if (j <= 2 && bw[2 * i + 1])	/* ana_peaky's forcing (melp_ana.c:404-409) */
-			v = 16384;
-		par[i].bpvc[j] = v;
-	}
-}
-
-/* analysis() as the four launches of the lane analysis (k_ana.hip mode 4,
- * k_lsf.hip, k_harm.hip, k_enc_tail):
- *   analysis_c  the frames, sc_ana and the quantisers other than lsf_vq;
- *               *uvc = the voicing pattern lsf_vq sees (after sc_ana, before
- *               quant_bp rewrites the flags);
- *   lsf_vq_u    on that pattern (a wave per channel on the GPU);
- *   the Fourier magnitudes of the voiced frames, each frame's windowed
- *   residual (ana_resid_sample) formed from the record's hpspeech and
- *   quantised LSFs, the last voiced frame's left in sigbuf;
- *   ana_shift + analysis_b.
- * lsf_vq reads only the LSFs, the pattern and its own memories (qplsp,
- * lsf_started), which pitch_vq, gain_vq and the jitter / bandpass
- * quantisers neither read nor write, so running it after them changes no
- * value. */
-MN void analysis_c(EncState *E, const int16_t *sp_in, Word16 *uvc)
-{
-	for (int i = 0; i < NF; i++)
-		analysis_frame(E, sp_in, i);
-	MelpParam *par = E->par;
-	sc_ana(E, par);
-	*uvc = lsf_uvc(par);
-	pitch_vq(E, par);
-	gain_vq(E, par);
-	for (int i = 0; i < NF; i++)
-		quant_u(&par[i].jitter, &E->qpar.jit_index[i], 0, MAX_JITTER_Q15, 2, SW_MAX_,
-			true, 7);
-	quant_bp(E, par);
-	quant_jitter(E, par);
-}
-
-/* words per channel of the lane kernel's hand-over to k_enc_lsf (k_ana.hip
- * mode 4): the voicing pattern, then lsf_vq's weights after its voicing
- * scaling (qnt12.c:925-941, the lane-serial part of its prelude) */
-#define LSF_AUX 32
-#define LSF_AUX_WGT 2
-static_assert(LSF_AUX_WGT + NF * LPC_ORD <= LSF_AUX, "lsf hand-over row");
-
-/* lsf_vq's prelude as the lane kernel runs it: aux[0] = uvc, the weights */
-MD void lsf_aux(MelpParam *par, Word16 uvc, int16_t *aux)
-{
-	int16_t lpc[LPC_ORD], w[LPC_ORD];
-	aux[0] = uvc;
-	aux[1] = 0;
-	for (int i = 0; i < NF; i++) {
-		lpc_lsp2pred(par[i].lsf, lpc, LPC_ORD);
-		vq_lspw(w, par[i].lsf, lpc, LPC_ORD);
-		if (((uvc >> (NF - 1 - i)) & 1) && i < NF - 1)
-			v_scale(w, 6554, LPC_ORD);
-		for (int j = 0; j < LPC_ORD; j++)
-			aux[LSF_AUX_WGT + i * LPC_ORD + j] = w[j];
-	}
-}
-
-/* sample n of frame i's windowed residual (melp_ana.c:224-233: zerflt of
- * the quantised-LSF predictor over hpspeech, then window): hp the record's
- * hpspeech, lpc[0..LPC_ORD] with lpc[0] = 4096 */
-MD int16_t ana_resid_sample(const int16_t *hp, const int16_t *lpc, int i, int n)
-{
-	const int16_t *x = &hp[i * FRAME + FRAME_END - LPC_FRAME / 2 + n];
-	Word32 a = 0;
-#pragma unroll
-	for (int j = 0; j <= LPC_ORD; j++)
-		a = L_mac(a, x[-j], lpc[j]);
-	return mult(TB(win_cof)[n], r_ound(L_shl(a, 3)));
 }
 
 /* the history shift at the end of analysis (melp_ana.c:262) */

@@ -58,8 +58,6 @@ int melpe_tu_npp_upload(const void *blob, size_t bytes);
 int melpe_tu_ana_upload(const void *blob, size_t bytes);
 int melpe_tu_anamw_upload(const void *blob, size_t bytes);
 int melpe_tu_harm_upload(const void *blob, size_t bytes);
-int melpe_tu_band_upload(const void *blob, size_t bytes);
-int melpe_tu_lsf_upload(const void *blob, size_t bytes);
 int melpe_tu_dec_upload(const void *blob, size_t bytes);
 int melpe_tu_r24_upload(const void *blob, size_t bytes);
 int melpe_tu_r24_prof(uint64_t *acc);
@@ -67,28 +65,25 @@ int melpe_tu_npp_prof(uint64_t *acc);
 int melpe_tu_ana_prof(uint64_t *acc);
 int melpe_tu_anamw_prof(uint64_t *acc);
 int melpe_tu_harm_prof(uint64_t *acc);
-int melpe_tu_band_prof(uint64_t *acc);
-int melpe_tu_lsf_prof(uint64_t *acc);
 int melpe_tu_dec_prof(uint64_t *acc);
 int kl_npp(EncState *enc, int16_t *sp, int frames, int stride, const uint8_t *active, int n,
 	   int rate1200, hipStream_t s);
 int kl_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active, int n, hipStream_t s);
 int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
-	       const int *perm, const int *nlive, int16_t *res, hipStream_t s);
+	       const int *perm, const int *nlive, int16_t *res, int cut, hipStream_t s);
 int kl_enc_harm(EncState *enc, const int16_t *res, const uint8_t *active, int n, const int *perm,
-		const int *nlive, hipStream_t s);
+		const int *nlive, int cut, hipStream_t s);
 int kl_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active, int n, const int *perm,
-		const int *nlive, int shift, hipStream_t s);
-int kl_enc_lsf(EncState *enc, const int16_t *aux, const uint8_t *active, int n, const int *perm,
-	       const int *nlive, hipStream_t s);
-int kl_enc_ana_part(EncState *enc, const int16_t *sp, int16_t *bw, int16_t *res, const uint8_t *active,
-		    int n, const int *perm, const int *nlive, int part, hipStream_t s);
-int kl_enc_band(EncState *enc, const int16_t *bw, const uint8_t *active, int n, const int *perm,
-		const int *nlive, hipStream_t s);
+		const int *nlive, int cut, hipStream_t s);
 int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
-		  const int *perm, const int *nlive, int nw, uint32_t *lqbuf, hipStream_t s);
+		  const int *perm, const int *nlive, int nw, uint32_t *lqbuf, int cut, hipStream_t s);
 size_t kl_enc_ana_mw_lq_words(int n);
 int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto, hipStream_t s);
+int kl_npp_warm(hipStream_t s);
+int kl_ana_warm(hipStream_t s);
+int kl_harm_warm(hipStream_t s);
+int kl_ana_mw_warm(hipStream_t s);
+int kl_dec_warm(hipStream_t s);
 int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
 	      const int *perm, const int *nlive,
 	      hipStream_t s);
@@ -613,6 +608,10 @@ static hipError_t bin_release(BinBuf &b, hipStream_t s)
 	return hipEventRecord(b.done, s);
 }
 
+/* k_enc_ana_mw holds two workgroups (of 4 waves, 64 channels) per CU, so it
+ * keeps every workgroup resident up to 512 of them */
+#define MW_MAX_CHANNELS (512 * WAVE)
+
 struct melpe_engine {
 	int device = 0;
 	int channels = 0;
@@ -628,14 +627,17 @@ struct melpe_engine {
 	BinBuf bin_enc, bin_dec;	/* pitch-class lane order of k_enc_ana / k_decode */
 	int lane_order = -1;	/* 1 on, 0 off, -1 the MELPE_BIN default */
 	int ana_waves = 0;	/* waves per 64 channels in k_enc_ana(_mw); 0: by channel count */
-	uint32_t *d_lq = nullptr;	/* k_enc_ana_mw's lsf_vq score rows, allocated on first use */
+	uint32_t *d_lq = nullptr;	/* k_enc_ana_mw's lsf_vq score rows (engine_reserve) */
+	int lq_channels = 0;	/* channels d_lq has rows for */
+	/* the live-count mapping (ana_launch): a superframe with at most this
+	 * many live channels runs the multi-wave kernel (0: off) */
+	int mw_live_max = MW_MAX_CHANNELS;
 	int16_t *d_res = nullptr;	/* the split lane analysis' windowed residuals (C x NF x LPC_FRAME) */
-	int16_t *d_bw = nullptr;	/* band 0's pitch and the peakiness flag per frame (C x NF x 2) */
-	int16_t *d_lw = nullptr;	/* lsf_vq's pattern and weights (C x LSF_AUX), k_lsf.hip */
 	/* one event per stream this engine's *_dev calls have used, recorded
 	 * after each call: the host-side calls wait on these (engine_wait)
 	 * instead of the whole device */
 	std::vector<std::pair<hipStream_t, hipEvent_t>> marks;
+	std::recursive_mutex mu;	/* guards marks and the BinBuf bookkeeping */
 	size_t npp_bytes = 0;
 	float last_ms = 0.f;
 };
@@ -645,16 +647,24 @@ struct melpe_engine {
  * about four waves per SIMD to hide its scratch latency; below that the
  * channel count leaves SIMDs idle or alone, and the multi-wave kernel
  * (k_enc_ana_mw, ana_mw.h) spreads each channel's independent chains over
- * 2 or 4 waves instead.  MELPE_ANA_NW overrides (diagnostics).
+ * 2 or 4 waves instead.  MELPE_ANA_NW overrides the automatic choice
+ * (diagnostics), not an explicit melpe_engine_set_ana_waves(1 or 4).
  */
-static int ana_waves_for(melpe_engine *e)
+static int ana_nw_env(void)
 {
 	static int env = -2;
 	if (env == -2) {
 		const char *v = getenv("MELPE_ANA_NW");
 		env = v ? atoi(v) : -1;
 	}
-	int nw = env >= 0 ? env : e->ana_waves;
+	return env;
+}
+
+static int ana_waves_for(melpe_engine *e)
+{
+	const int env = ana_nw_env();
+	/* an explicit melpe_engine_set_ana_waves() wins over the environment */
+	int nw = e->ana_waves ? e->ana_waves : env;
 	if (nw == 1 || nw == 4)
 		return nw;
 	/* k_enc_ana_mw holds two workgroups (of 4 waves) per CU, so it keeps
@@ -675,33 +685,6 @@ static bool harm_split(void)
 	return v != 0;
 }
 
-/* MELPE_BANDS=1: bands 1..4 of the voicing analysis in their own kernel
- * (k_band.hip).  Bit-exact, but at 262,144 channels the three launches
- * took 40.5 ms against 37.2 for k_enc_ana with the bands inside
- * (profiles/r03_p_*), so it is off by default. */
-static bool band_split(void)
-{
-	static int v = -1;
-	if (v < 0) {
-		const char *e = getenv("MELPE_BANDS");
-		v = e && e[0] == '1';
-	}
-	return v != 0;
-}
-
-/* MELPE_LSFW=1: lsf_vq with a wave per channel (k_lsf.hip), the residuals
- * formed in k_enc_harm; else lsf_vq stays in k_enc_ana (and MELPE_BANDS=1
- * applies) */
-static bool lsf_wave(void)
-{
-	static int v = -1;
-	if (v < 0) {
-		const char *e = getenv("MELPE_LSFW");
-		v = e && e[0] == '1';
-	}
-	return v != 0;
-}
-
 static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, const uint8_t *d_act,
 		      hipStream_t s)
 {
@@ -716,71 +699,43 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 	const int *perm = on ? b.perm : nullptr;
 	const int *nlive = on ? (const int *) (b.ctl + 2 * NBIN) : nullptr;
 	int nw = ana_waves_for(e);
-	if (nw > 1 && !e->d_lq) {
-		/* ordered after any work still reading the engine: a fresh buffer */
-		er = hipMalloc(&e->d_lq, sizeof(uint32_t) * kl_enc_ana_mw_lq_words(e->channels));
-		if (er != hipSuccess) {
-			e->d_lq = nullptr;
+	if (nw > 1 && e->lq_channels < e->channels) {
+		/* an explicit 4-wave mapping above MW_MAX_CHANNELS: score rows for
+		 * every channel (ordered after any work still reading the old
+		 * buffer: a fresh one) */
+		uint32_t *q;
+		er = hipMalloc(&q, sizeof(uint32_t) * kl_enc_ana_mw_lq_words(e->channels));
+		if (er != hipSuccess)
 			return (int) er;
-		}
+		hipFree(e->d_lq);
+		e->d_lq = q;
+		e->lq_channels = e->channels;
 	}
+	/* Above MW_MAX_CHANNELS the engine runs the lane kernels -- unless the
+	 * superframe has few live channels (ragged streams, BASELINE config 5):
+	 * with the lane order on, the live count is on the device (the bin sort
+	 * counted it), so both mappings are enqueued, each guarded by that count
+	 * (the lane kernels exit when at most mw_live_max channels are live, the
+	 * multi-wave kernel when more are), and the host never waits for it. */
+	const bool live_pick = nw == 1 && on && e->ana_waves == 0 && ana_nw_env() < 0 &&
+			       e->mw_live_max > 0 && harm_split();
+	const int cut = live_pick ? e->mw_live_max : -1;
 	int rc;
-	if (nw == 1 && harm_split() && lsf_wave()) {
-		/* frames and quantisers but lsf_vq (its pattern and weights into
-		 * d_lw), lsf_vq with a wave per channel (k_lsf.hip), the magnitudes
-		 * from residuals formed in k_enc_harm, then the history shift and
-		 * the packing */
-		if (!e->d_lw) {
-			er = hipMalloc(&e->d_lw, sizeof(int16_t) * LSF_AUX * (size_t) e->channels);
-			if (er != hipSuccess) {
-				e->d_lw = nullptr;
-				return (int) er;
-			}
-		}
-		rc = kl_enc_ana_part(e->d_enc, d_sp, e->d_lw, nullptr, d_act, e->channels, perm, nlive, 3, s);
-		if (rc == 0)
-			rc = kl_enc_lsf(e->d_enc, e->d_lw, d_act, e->channels, perm, nlive, s);
-		if (rc == 0)
-			rc = kl_enc_harm(e->d_enc, nullptr, d_act, e->channels, perm, nlive, s);
-		if (rc == 0)
-			rc = kl_enc_tail(e->d_enc, d_bits, d_act, e->channels, perm, nlive, 1, s);
-	} else if (nw == 1 && harm_split()) {
+	if (nw == 1 && harm_split()) {
 		/* lane-per-channel analysis up to the Fourier magnitudes, the
 		 * magnitudes with a wave per channel, then the packing (k_harm.hip) */
-		if (!e->d_res) {
-			er = hipMalloc(&e->d_res, sizeof(int16_t) * NF * LPC_FRAME * (size_t) e->channels);
-			if (er != hipSuccess) {
-				e->d_res = nullptr;
-				return (int) er;
-			}
-		}
-		if (band_split()) {
-			/* the frames with band 0, bands 1..4 with four lanes per
-			 * channel, then the superframe (k_band.hip) */
-			if (!e->d_bw) {
-				er = hipMalloc(&e->d_bw, sizeof(int16_t) * 2 * NF * (size_t) e->channels);
-				if (er != hipSuccess) {
-					e->d_bw = nullptr;
-					return (int) er;
-				}
-			}
-			rc = kl_enc_ana_part(e->d_enc, d_sp, e->d_bw, nullptr, d_act, e->channels, perm, nlive, 1, s);
-			if (rc == 0)
-				rc = kl_enc_band(e->d_enc, e->d_bw, d_act, e->channels, perm, nlive, s);
-			if (rc == 0)
-				rc = kl_enc_ana_part(e->d_enc, nullptr, nullptr, e->d_res, d_act, e->channels, perm,
-						     nlive, 2, s);
-		} else {
-			rc = kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, e->d_res, s);
-		}
+		rc = kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, e->d_res, cut, s);
 		if (rc == 0)
-			rc = kl_enc_harm(e->d_enc, e->d_res, d_act, e->channels, perm, nlive, s);
+			rc = kl_enc_harm(e->d_enc, e->d_res, d_act, e->channels, perm, nlive, cut, s);
 		if (rc == 0)
-			rc = kl_enc_tail(e->d_enc, d_bits, d_act, e->channels, perm, nlive, 0, s);
+			rc = kl_enc_tail(e->d_enc, d_bits, d_act, e->channels, perm, nlive, cut, s);
+		if (rc == 0 && live_pick)
+			rc = kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->mw_live_max, perm, nlive, 4, e->d_lq,
+					   cut, s);
 	} else {
-		rc = nw == 1 ? kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nullptr, s)
+		rc = nw == 1 ? kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nullptr, -1, s)
 			     : kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nw,
-					     e->d_lq, s);
+					     e->d_lq, INT32_MAX, s);
 	}
 	if (rc == 0 && on)
 		rc = (int) bin_release(b, s);
@@ -821,9 +776,7 @@ static int ensure_device_tables(int dev)
 	DEVGUARD(dev);
 	int (*up[])(const void *, size_t) = {melpe_tu_eng_upload, melpe_tu_npp_upload,
 					     melpe_tu_ana_upload, melpe_tu_anamw_upload, melpe_tu_harm_upload,
-					     melpe_tu_band_upload, melpe_tu_lsf_upload,
-					     melpe_tu_dec_upload,
-					     melpe_tu_r24_upload};
+					     melpe_tu_dec_upload, melpe_tu_r24_upload};
 	for (auto f : up)
 		if (int rc = f(melpe_tables_blob, bytes))
 			return fail("table upload", (hipError_t) rc);
@@ -847,7 +800,12 @@ static void ev_end(melpe_engine *e, hipStream_t s, bool sync)
 	}
 }
 
-/* after enqueueing this engine's work on stream s */
+/* after enqueueing this engine's work on stream s (EngineCall records it on
+ * every exit of a call once the call has started enqueueing, error paths
+ * included, so a later host-side wait also covers the work a failed call
+ * left in flight).  A stream's event is reused; at most MAX_MARKS streams
+ * are tracked, beyond that the oldest mark is waited for and recycled. */
+#define MAX_MARKS 16
 static int engine_mark(melpe_engine *e, hipStream_t s)
 {
 	for (auto &m : e->marks)
@@ -855,6 +813,12 @@ static int engine_mark(melpe_engine *e, hipStream_t s)
 			HIPCHK(hipEventRecord(m.second, s));
 			return 0;
 		}
+	if (e->marks.size() >= MAX_MARKS) {
+		auto m = e->marks.front();
+		e->marks.erase(e->marks.begin());
+		HIPCHK(hipEventSynchronize(m.second));
+		HIPCHK(hipEventDestroy(m.second));
+	}
 	hipEvent_t ev;
 	HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
 	e->marks.emplace_back(s, ev);
@@ -866,19 +830,66 @@ static int engine_mark(melpe_engine *e, hipStream_t s)
  * stream (not for other engines or unrelated work on the device) */
 static int engine_wait(melpe_engine *e)
 {
+	std::lock_guard<std::recursive_mutex> lk(e->mu);
 	for (auto &m : e->marks)
 		HIPCHK(hipEventSynchronize(m.second));
 	HIPCHK(hipStreamSynchronize(e->stream));
 	return 0;
 }
 #define ENGINE_WAIT(e) do { if (int _r = engine_wait(e)) return _r; } while (0)
-#define ENGINE_MARK(e, s) do { if (int _r = engine_mark(e, s)) return _r; } while (0)
+/* one *_dev call of an engine: holds the engine's lock (the host-side
+ * bookkeeping -- marks, the lane-order buffers -- is shared by the calls of
+ * every thread) and records the stream's mark when it ends */
+struct EngineCall {
+	melpe_engine *e;
+	hipStream_t s;
+	std::lock_guard<std::recursive_mutex> lk;
+	EngineCall(melpe_engine *e_, hipStream_t s_) : e(e_), s(s_), lk(e_->mu) {}
+	~EngineCall() { engine_mark(e, s); }
+};
+#define ENGINE_CALL(e, s) EngineCall _call(e, s)
 
 extern "C" {
 
 const char *melpe_last_error(void)
 {
 	return g_err.c_str();
+}
+
+/*
+ * What the engine's launches need beyond its records, had at create so a
+ * shortage fails here and not mid-stream:
+ * - the analysis hand-over buffers (the split lane analysis' residuals; the
+ *   multi-wave kernel's score rows up to its 512 resident workgroups);
+ * - the private-segment scratch of every codec kernel (the lane kernels
+ *   hold ~27 KB per lane): the runtime reserves a queue's scratch at the
+ *   first dispatch that needs it, so one empty workgroup of each kernel is
+ *   dispatched on the engine's stream and waited for.  (Scratch is held per
+ *   hardware queue: a caller's own stream may map to another queue, whose
+ *   first dispatch reserves it again.)
+ */
+static int engine_reserve(melpe_engine *e)
+{
+	DEVGUARD(e->device);
+	hipError_t er;
+	if (harm_split() && (er = hipMalloc(&e->d_res, sizeof(int16_t) * NF * LPC_FRAME *
+						     (size_t) e->channels)) != hipSuccess) {
+		e->d_res = nullptr;
+		return fail("melpe_engine_create: analysis residual buffer", er);
+	}
+	const int mw = e->channels < MW_MAX_CHANNELS ? e->channels : MW_MAX_CHANNELS;
+	if ((er = hipMalloc(&e->d_lq, sizeof(uint32_t) * kl_enc_ana_mw_lq_words(mw))) != hipSuccess) {
+		e->d_lq = nullptr;
+		return fail("melpe_engine_create: multi-wave score rows", er);
+	}
+	e->lq_channels = mw;
+	int (*warm[])(hipStream_t) = {kl_npp_warm, kl_ana_warm, kl_harm_warm, kl_ana_mw_warm, kl_dec_warm};
+	for (auto f : warm)
+		if ((er = (hipError_t) f(e->stream)) != hipSuccess)
+			return fail("melpe_engine_create: codec kernel scratch could not be reserved", er);
+	if ((er = hipStreamSynchronize(e->stream)) != hipSuccess)
+		return fail("melpe_engine_create: codec kernel scratch could not be reserved", er);
+	return 0;
 }
 
 int melpe_engine_create(melpe_engine **out, int device, int channels)
@@ -917,6 +928,8 @@ int melpe_engine_create(melpe_engine **out, int device, int channels)
 		return r;
 	}
 	int r = melpe_engine_reset(e, nullptr, 3);
+	if (r == 0)
+		r = engine_reserve(e);
 	if (r) {
 		std::string m = g_err;
 		melpe_engine_destroy(e);
@@ -932,6 +945,15 @@ int melpe_engine_set_lane_order(melpe_engine *e, int on)
 	if (!e)
 		return fail_msg("melpe_engine_set_lane_order: null engine");
 	e->lane_order = on ? 1 : 0;
+	return 0;
+}
+
+int melpe_engine_set_mw_live_max(melpe_engine *e, int live_max)
+{
+	if (!e || live_max < 0 || live_max > MW_MAX_CHANNELS)
+		return fail_msg("melpe_engine_set_mw_live_max: 0 .. 32768 live channels");
+	std::lock_guard<std::recursive_mutex> lk(e->mu);
+	e->mw_live_max = live_max;
 	return 0;
 }
 
@@ -961,8 +983,6 @@ int melpe_engine_destroy(melpe_engine *e)
 	hipFree(e->bin_dec.perm);
 	hipFree(e->d_lq);
 	hipFree(e->d_res);
-	hipFree(e->d_bw);
-	hipFree(e->d_lw);
 	for (auto &m : e->marks)
 		hipEventDestroy(m.second);
 	if (e->bin_enc.done)
@@ -1001,10 +1021,10 @@ int melpe_engine_reset_dev(melpe_engine *e, const void *d_mask, int which, void 
 	if (!e || which < 1 || which > 3)
 		return fail_msg("melpe_engine_reset_dev: bad arguments");
 	DEVGUARD(e->device);
+	ENGINE_CALL(e, (hipStream_t) hip_stream);
 	k_reset<<<grid_for(e->channels), WAVE, 0, (hipStream_t) hip_stream>>>(
 		e->d_enc, e->d_dec, (const uint8_t *) d_mask, e->channels, which);
 	HIPCHK(hipGetLastError());
-	ENGINE_MARK(e, (hipStream_t) hip_stream);
 	return 0;
 }
 
@@ -1033,10 +1053,10 @@ static int npp_launch(melpe_engine *e, int16_t *d_sp, int frames, int stride,
 	if (frames <= 0 || stride < frames * MELPE_FRAME_SAMPLES)
 		return fail_msg("melpe_npp: bad frames/stride");
 	DEVGUARD(e->device);
+	ENGINE_CALL(e, s);
 	ev_begin(e, s);
 	HIPCHK((hipError_t) kl_npp(e->d_enc, d_sp, frames, stride, d_act, e->channels, rate1200, s));
 	ev_end(e, s, sync);
-	ENGINE_MARK(e, s);
 	return 0;
 }
 
@@ -1084,11 +1104,11 @@ static int encode_launch(melpe_engine *e, unsigned char *d_bits, int16_t *d_sp,
 			 const uint8_t *d_act, hipStream_t s, bool sync)
 {
 	DEVGUARD(e->device);
+	ENGINE_CALL(e, s);
 	ev_begin(e, s);
 	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, d_sp, d_act, e->channels, s));
 	HIPCHK((hipError_t) ana_launch(e, d_sp, d_bits, d_act, s));
 	ev_end(e, s, sync);
-	ENGINE_MARK(e, s);
 	return 0;
 }
 
@@ -1106,9 +1126,9 @@ int melpe_encode_npp_dev(melpe_engine *e, void *d_sp, const void *d_active, void
 	if (!e || !d_sp)
 		return fail_msg("melpe_encode_npp_dev: null argument");
 	DEVGUARD(e->device);
+	ENGINE_CALL(e, (hipStream_t) hip_stream);
 	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, (int16_t *) d_sp, (const uint8_t *) d_active,
 				       e->channels, (hipStream_t) hip_stream));
-	ENGINE_MARK(e, (hipStream_t) hip_stream);
 	return 0;
 }
 
@@ -1118,9 +1138,9 @@ int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const 
 	if (!e || !d_bits || !d_sp)
 		return fail_msg("melpe_encode_ana_dev: null argument");
 	DEVGUARD(e->device);
+	ENGINE_CALL(e, (hipStream_t) hip_stream);
 	HIPCHK((hipError_t) ana_launch(e, (const int16_t *) d_sp, (uint8_t *) d_bits,
 				       (const uint8_t *) d_active, (hipStream_t) hip_stream));
-	ENGINE_MARK(e, (hipStream_t) hip_stream);
 	return 0;
 }
 
@@ -1152,10 +1172,10 @@ static int decode_launch(melpe_engine *e, int16_t *d_sp, const unsigned char *d_
 			 const uint8_t *d_act, hipStream_t s, bool sync)
 {
 	DEVGUARD(e->device);
+	ENGINE_CALL(e, s);
 	ev_begin(e, s);
 	HIPCHK((hipError_t) dec_launch(e, d_sp, d_bits, d_act, s));
 	ev_end(e, s, sync);
-	ENGINE_MARK(e, s);
 	return 0;
 }
 
@@ -1199,11 +1219,11 @@ static int encode24_launch(melpe_engine *e, unsigned char *d_bits, int16_t *d_sp
 			   const uint8_t *d_act, hipStream_t s, bool sync)
 {
 	DEVGUARD(e->device);
+	ENGINE_CALL(e, s);
 	ev_begin(e, s);
 	HIPCHK((hipError_t) kl_npp(e->d_enc, d_sp, 1, MELPE_FRAME_SAMPLES, d_act, e->channels, 0, s));
 	HIPCHK((hipError_t) kl_enc24(e->d_enc, d_sp, d_bits, d_act, e->channels, s));
 	ev_end(e, s, sync);
-	ENGINE_MARK(e, s);
 	return 0;
 }
 
@@ -1223,11 +1243,11 @@ int melpe_decode2400_dev(melpe_engine *e, void *d_sp, const void *d_bits, const 
 		return fail_msg("melpe_decode2400_dev: null argument");
 	DEVGUARD(e->device);
 	hipStream_t s = (hipStream_t) hip_stream;
+	ENGINE_CALL(e, s);
 	ev_begin(e, s);
 	HIPCHK((hipError_t) kl_dec24(e->d_dec, (int16_t *) d_sp, (const uint8_t *) d_bits,
 				     (const uint8_t *) d_active, e->channels, s));
 	ev_end(e, s, false);
-	ENGINE_MARK(e, s);
 	return 0;
 }
 
@@ -1348,10 +1368,10 @@ int melpe_synth_dev(melpe_engine *e, void *d_sp, int samples, void *hip_stream)
 	if (!e || !d_sp || samples <= 0)
 		return fail_msg("melpe_synth_dev: bad arguments");
 	DEVGUARD(e->device);
+	ENGINE_CALL(e, (hipStream_t) hip_stream);
 	k_synth<<<grid_for(e->channels), WAVE, 0, (hipStream_t) hip_stream>>>(
 		e->d_syn, (int16_t *) d_sp, samples, e->channels);
 	HIPCHK(hipGetLastError());
-	ENGINE_MARK(e, (hipStream_t) hip_stream);
 	return 0;
 }
 
@@ -1382,7 +1402,7 @@ int melpe_prof_read(uint64_t *out, int n)
 {
 	uint64_t acc[MELPE_PROF_SLOTS_ABI] = {0};
 	int (*rd[])(uint64_t *) = {melpe_tu_eng_prof, melpe_tu_npp_prof, melpe_tu_ana_prof, melpe_tu_anamw_prof,
-				   melpe_tu_harm_prof, melpe_tu_band_prof, melpe_tu_lsf_prof,
+				   melpe_tu_harm_prof,
 				   melpe_tu_dec_prof, melpe_tu_r24_prof};
 	for (auto f : rd)
 		if (f(acc))

@@ -133,76 +133,6 @@ int emu_encode_ana_split(emu_engine *e, unsigned char *bits, const int16_t *sp)
 	return 0;
 }
 
-/* the split with the voicing bands 1..4 taken out as well (k_enc_ana mode 2,
- * k_enc_band, mode 3, k_enc_harm, k_enc_tail): every channel's frames
- * first, then the bands of every channel, then the rest */
-int emu_encode_ana_split3(emu_engine *e, unsigned char *bits, const int16_t *sp)
-{
-	static int16_t res[NF * LPC_FRAME];
-	std::vector<int16_t> bw((size_t) e->channels * 2 * NF, (int16_t) 0x5a5a);
-	for (int c = 0; c < e->channels; c++)
-		analysis_a1(&e->enc[c], sp + (size_t) c * BLOCK, &bw[(size_t) c * 2 * NF]);
-	for (int c = 0; c < e->channels; c++) {
-		EncState *E = &e->enc[c];
-		for (int j = 1; j < NUM_BANDS; j++) {
-			BandState B = E->band[j];
-			ana_band_frames(&B, E->hpspeech, j, &bw[(size_t) c * 2 * NF], E->par);
-			E->band[j] = B;
-		}
-	}
-	for (int c = 0; c < e->channels; c++) {
-		EncState *E = &e->enc[c];
-		for (int k = 0; k < NF * LPC_FRAME; k++)
-			res[k] = (int16_t) 0x5a5a;
-		analysis_a2(E, res);
-		for (int i = 0; i < NF; i++) {
-			MelpParam *par = &E->par[i];
-			v_set(par->fs_mag, 8192, NUM_HARM);
-			if (!par->uv_flag)
-				find_harm(&res[i * LPC_FRAME], par->fs_mag, par->pitch, NUM_HARM, LPC_FRAME);
-		}
-		analysis_b(E);
-		for (int k = 0; k < 11; k++)
-			bits[c * 11 + k] = E->chbuf[k];
-	}
-	return 0;
-}
-
-/* the four-launch form (encoder.h analysis_c): frames and quantisers, then
- * lsf_vq on the saved pattern, then the magnitudes from per-sample
- * residuals, then the shift and the packing */
-int emu_encode_ana_split4(emu_engine *e, unsigned char *bits, const int16_t *sp)
-{
-	std::vector<int16_t> uvc(e->channels);
-	for (int c = 0; c < e->channels; c++)
-		analysis_c(&e->enc[c], sp + (size_t) c * BLOCK, &uvc[c]);
-	for (int c = 0; c < e->channels; c++)
-		lsf_vq_u(&e->enc[c], e->enc[c].par, uvc[c]);
-	for (int c = 0; c < e->channels; c++) {
-		EncState *E = &e->enc[c];
-		int16_t w[LPC_FRAME];
-		for (int i = 0; i < NF; i++) {
-			MelpParam *par = &E->par[i];
-			v_set(par->fs_mag, 8192, NUM_HARM);
-			if (par->uv_flag)
-				continue;
-			int16_t lpc[LPC_ORD + 1];
-			lpc[0] = 4096;
-			lsf_sort10(par->lsf);	/* as k_enc_harm: lpc_lsp2pred's clamp */
-			lsp2pred10(par->lsf, &lpc[1]);
-			for (int n = 0; n < LPC_FRAME; n++)
-				w[n] = ana_resid_sample(E->hpspeech, lpc, i, n);
-			v_copy(E->sigbuf, w, LPC_FRAME);
-			find_harm(w, par->fs_mag, par->pitch, NUM_HARM, LPC_FRAME);
-		}
-		ana_shift(E);
-		analysis_b(E);
-		for (int k = 0; k < 11; k++)
-			bits[c * 11 + k] = E->chbuf[k];
-	}
-	return 0;
-}
-
 int emu_encode_ana(emu_engine *e, unsigned char *bits, const int16_t *sp)
 {
 	for (int c = 0; c < e->channels; c++) {

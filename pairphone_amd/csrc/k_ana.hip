@@ -18,25 +18,19 @@ struct AnaLane {
 /* MODE 0: the whole analysis and the bits here (MELPE_HARM=0).
  * MODE 1: the split form (encoder.h analysis_a): the windowed residuals to
  *         res (NF x LPC_FRAME per channel), the Fourier magnitudes and the
- *         packing in k_harm.hip.
- * MODE 2: analysis_a1, the frames with band 0 of bpvc_ana only, bw (2 x NF
- *         per channel) for k_band.hip, which runs bands 1..4;
- * MODE 3: analysis_a2, the superframe up to the residuals (as MODE 1's
- *         second half).  It neither reads nor writes the band memories.
- * MODE 4: analysis_c, everything before lsf_vq's turn but lsf_vq, the
- *         voicing pattern it sees and its weights into bw (LSF_AUX words
- *         per channel, encoder.h lsf_aux; k_lsf.hip, then k_enc_harm
- *         forms the residuals and k_enc_tail shifts the history). */
+ *         packing in k_harm.hip. */
 template <int MODE>
 __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits,
 						  const uint8_t *active, int n, const int *perm,
-						  const int *nlive, int16_t *res, int16_t *bw)
+						  const int *nlive, int16_t *res, int cut)
 {
 	/* lane g runs channel perm[g] when the engine ordered the live channels
-	 * by pitch class (engine.hip, MELPE_BIN), else channel g under the mask */
+	 * by pitch class (engine.hip, MELPE_BIN), else channel g under the mask;
+	 * with at most `cut` live channels the multi-wave kernel takes the
+	 * superframe (engine.hip ana_launch) */
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (perm) {
-		if (c >= *nlive)
+		if (c >= *nlive || *nlive <= cut)
 			return;
 		c = perm[c];
 	} else if (c >= n || (active && !active[c])) {
@@ -44,30 +38,14 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 	}
 	AnaLane L;
 	PIN_FRAME(L);
-	constexpr size_t nb = MODE == 3 ? offsetof(EncState, band) - ENC_ANA_OFF : ENC_ANA_BYTES;
+	constexpr size_t nb = ENC_ANA_BYTES;
 	static_assert(nb % 4 == 0, "the record copy is in dwords");
 	lane_copy((char *) &L.S + ENC_ANA_OFF, (const char *) &enc[c] + ENC_ANA_OFF, nb);
-	if (MODE != 3)
-		lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
+	lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
 	if (MODE == 0)
 		analysis(&L.S, L.x);
-	else if (MODE == 1)
+	else
 		analysis_a(&L.S, L.x, res + (size_t) c * NF * LPC_FRAME);
-	else if (MODE == 2) {
-		int16_t w[2 * NF];
-		analysis_a1(&L.S, L.x, w);
-		for (int k = 0; k < 2 * NF; k++)
-			bw[(size_t) c * 2 * NF + k] = w[k];
-	} else if (MODE == 3) {
-		analysis_a2(&L.S, res + (size_t) c * NF * LPC_FRAME);
-	} else {
-		Word16 u;
-		analysis_c(&L.S, L.x, &u);
-		int16_t aux[LSF_AUX];
-		lsf_aux(L.S.par, u, aux);
-		for (int k = 0; k < LSF_AUX; k++)
-			bw[(size_t) c * LSF_AUX + k] = aux[k];
-	}
 	lane_copy((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, nb);
 	if (MODE == 0)
 		for (int k = 0; k < 11; k++)
@@ -101,37 +79,28 @@ static unsigned ana_lds_bytes(void)
 }
 
 extern "C" int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
-			  int n, const int *perm, const int *nlive, int16_t *res, hipStream_t s)
+			  int n, const int *perm, const int *nlive, int16_t *res, int cut, hipStream_t s)
 {
 	if (res)
 		k_enc_ana<1><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res,
-									  nullptr);
+									  cut);
 	else
 		k_enc_ana<0><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res,
-									  nullptr);
-	return (int) hipGetLastError();
-}
-
-/* part 1: analysis_a1 (bw out), part 2: analysis_a2 (res out), part 3:
- * analysis_c (the voicing pattern per channel into bw) */
-extern "C" int kl_enc_ana_part(EncState *enc, const int16_t *sp, int16_t *bw, int16_t *res,
-			       const uint8_t *active, int n, const int *perm, const int *nlive, int part,
-			       hipStream_t s)
-{
-	if (part == 3)
-		k_enc_ana<4><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, nullptr, active, n, perm, nlive,
-									  nullptr, bw);
-	else if (part == 1)
-		k_enc_ana<2><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, nullptr, active, n, perm, nlive,
-									  nullptr, bw);
-	else
-		k_enc_ana<3><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, nullptr, nullptr, active, n, perm,
-									  nlive, res, nullptr);
+									  cut);
 	return (int) hipGetLastError();
 }
 
 extern "C" int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto, hipStream_t s)
 {
 	k_enc_ana_dbg<<<grid_for(n), WAVE, 0, s>>>(enc, sp, n, upto);
+	return (int) hipGetLastError();
+}
+
+/* one workgroup with no live channel (every lane exits at once): the launch
+ * still makes the runtime reserve the kernel's private-segment scratch
+ * (engine.hip melpe_engine_create) */
+extern "C" int kl_ana_warm(hipStream_t s)
+{
+	k_enc_ana<1><<<1, WAVE, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, -1);
 	return (int) hipGetLastError();
 }

@@ -72,8 +72,13 @@ template <int NW>
 __global__ __launch_bounds__(WAVE * NW, MELPE_MW_WAVES) void k_enc_ana_mw(EncState *enc, const int16_t *sp,
 									    uint8_t *bits, const uint8_t *active,
 									    int n, const int *perm, const int *nlive,
-									    uint32_t *lqbuf)
+									    uint32_t *lqbuf, int cut)
 {
+	/* a launch guarded by the live count (engine.hip ana_launch): the lane
+	 * kernels take the superframe when more than `cut` channels are live
+	 * (uniform in the workgroup, before any barrier) */
+	if (perm && *nlive > cut)
+		return;
 	__shared__ int16_t xs[XS_WORDS * WAVE];
 	const int w = threadIdx.x / WAVE, t = threadIdx.x % WAVE;
 	int c = blockIdx.x * WAVE + t;
@@ -139,14 +144,21 @@ extern "C" size_t kl_enc_ana_mw_lq_words(int n)
 }
 
 extern "C" int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
-			     int n, const int *perm, const int *nlive, int nw, uint32_t *lqbuf,
+			     int n, const int *perm, const int *nlive, int nw, uint32_t *lqbuf, int cut,
 			     hipStream_t s)
 {
 	/* 4 waves per 64 channels (2 measured no better at any channel count
 	 * and cost a third more compile time; ana_mw.h supports any count) */
 	if (nw == 4)
-		k_enc_ana_mw<4><<<grid_for(n), WAVE * 4, 0, s>>>(enc, sp, bits, active, n, perm, nlive, lqbuf);
+		k_enc_ana_mw<4><<<grid_for(n), WAVE * 4, 0, s>>>(enc, sp, bits, active, n, perm, nlive, lqbuf, cut);
 	else
 		return (int) hipErrorInvalidValue;
+	return (int) hipGetLastError();
+}
+
+extern "C" int kl_ana_mw_warm(hipStream_t s)
+{
+	k_enc_ana_mw<4><<<1, WAVE * 4, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr,
+					       nullptr, INT32_MAX);
 	return (int) hipGetLastError();
 }

@@ -54,3 +54,10 @@ extern "C" int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const 
 	k_decode<<<(n + b - 1) / b, b, IDFT_LDS_WORDS * sizeof(int16_t), s>>>(dec, sp, bits, active, n, perm, nlive);
 	return (int) hipGetLastError();
 }
+
+extern "C" int kl_dec_warm(hipStream_t s)
+{
+	k_decode<<<1, WAVE, IDFT_LDS_WORDS * sizeof(int16_t), s>>>(nullptr, nullptr, nullptr, nullptr, 0,
+								      nullptr, nullptr);
+	return (int) hipGetLastError();
+}

@@ -137,20 +137,16 @@ MD void wv_find_harm(const int16_t v[4], int16_t *fsmag, Word16 pitch, uint32_t 
 	wsync();
 }
 
-/* RESID: the windowed residuals formed here, from the record's hpspeech
- * and quantised LSFs (encoder.h ana_resid_sample, one sample per lane and
- * step), the last voiced frame's left in sigbuf as analysis_a leaves it;
- * else read from res (k_enc_ana mode 1). */
+/* the windowed residuals k_enc_ana (mode 1) left in res */
 /* one wave per live channel: slot g runs channel perm[g] (the engine's
  * lane order) or channel g under the mask; the three frames in order */
-template <bool RESID>
 __global__ __launch_bounds__(WAVE) void k_enc_harm(EncState *enc, const int16_t *res,
 						   const uint8_t *active, int n, const int *perm,
-						   const int *nlive)
+						   const int *nlive, int cut)
 {
 	int c = blockIdx.x;
 	if (perm) {
-		if (c >= *nlive)
+		if (c >= *nlive || *nlive <= cut)
 			return;
 		c = perm[c];
 	} else if (c >= n || (active && !active[c])) {
@@ -169,50 +165,20 @@ __global__ __launch_bounds__(WAVE) void k_enc_harm(EncState *enc, const int16_t 
 			continue;
 		}
 		int16_t v[4];
-		if (RESID) {
-			/* lpc_lsp2pred on registers (dsp.h lsp2pred10), its clamp
-			 * written back as the reference's writes it */
-			int16_t l[LPC_ORD], lc[LPC_ORD + 1];
+		const int16_t *w = res + ((size_t) c * NF + i) * LPC_FRAME;
 #pragma unroll
-			for (int j = 0; j < LPC_ORD; j++)
-				l[j] = par->lsf[j];
-			lsf_sort10(l);
-			if (lane < LPC_ORD) {
-				int16_t v = 0;
-#pragma unroll
-				for (int j = 0; j < LPC_ORD; j++)
-					v = lane == j ? l[j] : v;
-				par->lsf[lane] = v;
-			}
-			lc[0] = 4096;
-			lsp2pred10(l, &lc[1]);
-#pragma unroll
-			for (int t = 0; t < 4; t++) {
-				const int k = lane + WV * t;
-				v[t] = k < LPC_FRAME ? ana_resid_sample(enc[c].hpspeech, lc, i, k) : (int16_t) 0;
-				if (k < LPC_FRAME)
-					enc[c].sigbuf[k] = v[t];
-			}
-		} else {
-			const int16_t *w = res + ((size_t) c * NF + i) * LPC_FRAME;
-#pragma unroll
-			for (int t = 0; t < 4; t++) {
-				const int k = lane + WV * t;
-				v[t] = k < LPC_FRAME ? w[k] : (int16_t) 0;
-			}
+		for (int t = 0; t < 4; t++) {
+			const int k = lane + WV * t;
+			v[t] = k < LPC_FRAME ? w[k] : (int16_t) 0;
 		}
 		wv_find_harm(v, par->fs_mag, pitch, x, &kc, lane);
 	}
 }
 
-/* res == nullptr: the residuals formed in the kernel (RESID) */
 extern "C" int kl_enc_harm(EncState *enc, const int16_t *res, const uint8_t *active, int n,
-			   const int *perm, const int *nlive, hipStream_t s)
+			   const int *perm, const int *nlive, int cut, hipStream_t s)
 {
-	if (res)
-		k_enc_harm<false><<<n, WAVE, 0, s>>>(enc, res, active, n, perm, nlive);
-	else
-		k_enc_harm<true><<<n, WAVE, 0, s>>>(enc, res, active, n, perm, nlive);
+	k_enc_harm<<<n, WAVE, 0, s>>>(enc, res, active, n, perm, nlive, cut);
 	return (int) hipGetLastError();
 }
 
@@ -224,11 +190,11 @@ struct TailLane {
 };
 
 __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active,
-						   int n, const int *perm, const int *nlive, int shift)
+						   int n, const int *perm, const int *nlive, int cut)
 {
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (perm) {
-		if (c >= *nlive)
+		if (c >= *nlive || *nlive <= cut)
 			return;
 		c = perm[c];
 	} else if (c >= n || (active && !active[c])) {
@@ -244,8 +210,6 @@ __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bi
 	static_assert(o % 4 == 0 && e % 4 == 0, "the tail's record ranges are dword copies");
 	lane_copy((char *) &L.S + o, (const char *) &enc[c] + o, e - o);
 	lane_copy((char *) &L.S + o2, (const char *) &enc[c] + o2, e2 - o2);
-	if (shift)	/* ana_shift on the record (the residuals are formed) */
-		lane_copy16(enc[c].hpspeech, &enc[c].hpspeech[NF * FRAME], sizeof(int16_t) * IN_BEG);
 	analysis_b(&L.S);
 	lane_copy((char *) &enc[c] + o, (const char *) &L.S + o, e - o);
 	lane_copy((char *) &enc[c] + o2, (const char *) &L.S + o2, e2 - o2);
@@ -254,8 +218,15 @@ __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bi
 }
 
 extern "C" int kl_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active, int n,
-			   const int *perm, const int *nlive, int shift, hipStream_t s)
+			   const int *perm, const int *nlive, int cut, hipStream_t s)
 {
-	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(enc, bits, active, n, perm, nlive, shift);
+	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(enc, bits, active, n, perm, nlive, cut);
+	return (int) hipGetLastError();
+}
+
+extern "C" int kl_harm_warm(hipStream_t s)
+{
+	k_enc_harm<<<1, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr, -1);
+	k_enc_tail<<<1, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr, -1);
 	return (int) hipGetLastError();
 }

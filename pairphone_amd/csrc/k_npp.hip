@@ -71,3 +71,9 @@ extern "C" int kl_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active, int
 	k_enc_npp<<<n, WAVE, 0, s>>>(enc, sp, active, n);
 	return (int) hipGetLastError();
 }
+
+extern "C" int kl_npp_warm(hipStream_t s)
+{
+	k_enc_npp<<<1, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0);
+	return (int) hipGetLastError();
+}

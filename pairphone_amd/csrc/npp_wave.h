@@ -18,9 +18,10 @@
  *    where it is defined (npp_spec_term, npp_bias_scalars, wv_enh_init), so
  *    the reduction order cannot change the result;
  *  - the two cross-bin scans whose order matters (the gain average with its
- *    running block-floating-point rescale, npp.c:1336-1360, and the
- *    cmp_shift arg-max, :1362-1366) run in reference order on every lane
- *    (uniform, no divergence).
+ *    running block-floating-point rescale, npp.c:1361-1389, and the
+ *    comp_data_shift arg-max, :1391-1399): the average as an exact
+ *    fixed-point sum over a prefix max of the exponents, the arg-max as a
+ *    scan in reference order over the few bins that can win (wv_gain_scan).
  * Scalars of the state are computed redundantly by all lanes and written by
  * all lanes with identical values.  wsync() (a one-wave workgroup barrier)
  * separates phases whose LDS data crosses lanes.
@@ -39,6 +40,29 @@ namespace wv {
  * only the owning lane reads back can live in registers indexed by t */
 #define BIN_LOOP(t, i) \
 	_Pragma("unroll") for (int t = 0, i = lane; t < 3; t++, i += WV) if (i < NPP_NB)
+
+/* bins 0..127 as two full passes of the wave, then bin 128 (NPP_NB - 1)
+ * in wave-uniform control flow.  A third pass would issue every vector
+ * instruction of the body for lane 0 alone; with the bin index a constant
+ * the body's values are uniform, so the compiler keeps them in scalar
+ * registers and on the scalar unit, beside the other waves' vector work.
+ * Every lane runs bin 128: its stores write one value from all lanes, and a
+ * body that adds bin terms into a per-lane partial sum counts bin 128 on
+ * lane 0 only (ON_LANE0(t)). */
+#if !defined(MELPE_NPP_LANE128)
+#define BIN_PASSES(t, i, ...) \
+	_Pragma("unroll") for (int t = 0; t < 3; t++) { \
+		const int i = t < 2 ? lane + WV * t : NPP_NB - 1; \
+		__VA_ARGS__ \
+	}
+#define ON_LANE0(t) ((t) < 2 || lane == 0)
+#else	/* A/B diagnostics: bin 128 as a third vector pass on lane 0 */
+#define BIN_PASSES(t, i, ...) \
+	_Pragma("unroll") for (int t = 0, i = lane; t < 3; t++, i += WV) if (i < NPP_NB) { \
+		__VA_ARGS__ \
+	}
+#define ON_LANE0(t) true
+#endif
 
 __device__ __forceinline__ void wsync()
 {
@@ -77,6 +101,44 @@ __device__ __forceinline__ int wsum(int v)
 	v += dppmov<DPP_ROW_MIRROR>(v);
 	return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
 	       __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+}
+
+/* inclusive prefix max over the lanes (lane l gets the max of lanes 0..l):
+ * row_shr 1, 2, 4, 8 inside each row of 16 lanes (max is idempotent, so
+ * the overlapping windows are harmless), then row_bcast:15 (the end of rows
+ * 0 and 2 into rows 1 and 3) and row_bcast:31 (the end of row 1 into rows 2
+ * and 3).  Lanes without a source keep `old` = the identity. */
+#define DPP_ROW_SHR(n) (0x110 + (n))
+#define DPP_ROW_BCAST15 0x142
+#define DPP_ROW_BCAST31 0x143
+template <int CTRL, int RM> __device__ __forceinline__ int dpp_or(int old, int v)
+{
+	return __builtin_amdgcn_update_dpp(old, v, CTRL, RM, 0xF, false);
+}
+
+__device__ __forceinline__ int wscan_max(int v)
+{
+	v = max(v, dpp_or<DPP_ROW_SHR(1), 0xF>(INT32_MIN, v));
+	v = max(v, dpp_or<DPP_ROW_SHR(2), 0xF>(INT32_MIN, v));
+	v = max(v, dpp_or<DPP_ROW_SHR(4), 0xF>(INT32_MIN, v));
+	v = max(v, dpp_or<DPP_ROW_SHR(8), 0xF>(INT32_MIN, v));
+	v = max(v, dpp_or<DPP_ROW_BCAST15, 0xA>(INT32_MIN, v));
+	v = max(v, dpp_or<DPP_ROW_BCAST31, 0xC>(INT32_MIN, v));
+	return v;
+}
+
+/* the same for floats (as bit patterns; -inf is the identity) */
+__device__ __forceinline__ float wscan_maxf(float f)
+{
+	const int ni = (int) 0xff800000u;
+	int v = __float_as_int(f);
+	v = __float_as_int(fmaxf(__int_as_float(v), __int_as_float(dpp_or<DPP_ROW_SHR(1), 0xF>(ni, v))));
+	v = __float_as_int(fmaxf(__int_as_float(v), __int_as_float(dpp_or<DPP_ROW_SHR(2), 0xF>(ni, v))));
+	v = __float_as_int(fmaxf(__int_as_float(v), __int_as_float(dpp_or<DPP_ROW_SHR(4), 0xF>(ni, v))));
+	v = __float_as_int(fmaxf(__int_as_float(v), __int_as_float(dpp_or<DPP_ROW_SHR(8), 0xF>(ni, v))));
+	v = __float_as_int(fmaxf(__int_as_float(v), __int_as_float(dpp_or<DPP_ROW_BCAST15, 0xA>(ni, v))));
+	v = __float_as_int(fmaxf(__int_as_float(v), __int_as_float(dpp_or<DPP_ROW_BCAST31, 0xC>(ni, v))));
+	return __int_as_float(v);
 }
 
 /* value of bin i (0..128) held one bin per lane in r0 (bins 0..63), r1
@@ -416,6 +478,171 @@ MD void wv_enh_init(NppWave *W, int16_t *noise, const WvConst *kc, int lane, Npp
 	wsync();
 }
 
+/* The gamma average with its running rescale and the gamma arg-max
+ * (npp.c:1361-1399) over gk / gks (129 bins, LDS).  gk = divide_s(..) is in
+ * [0, 32767] and the shifts are small, so the reference's saturating ops
+ * reduce to plain integer ones: the running sum is at most 129 * 2^22 <
+ * 2^31, a left-shifted term at most 2^22 (shift <= 7), sub() of two shifts
+ * cannot saturate.
+ *
+ * The average in parallel.  Let a_j be bin j's exponent as the sum sees it
+ * (gks, one lower for bins 0 and 128) and M_j = max(a_0..a_j) the running
+ * shift.  Bin j adds term_j = gk_j << (7 - t) or >> (t - 7), t = M_j - a_j,
+ * and each rise of the running shift by D floors the sum to sum >> D.
+ * Since floor(floor(x / 2^p) + y) / 2^q) = floor((x + y 2^p) / 2^(p+q)) for
+ * an integer y, the reference's sum is exactly
+ *     floor( sum_j term_j / 2^(M_128 - M_j) ),
+ * the terms taken relative to the final shift.  With every M_128 - M_j <=
+ * 32 that is an exact fixed-point sum with 32 fraction bits: integer parts
+ * (< 2^30 in all) and the 32-bit fractions as two 16-bit halves.  M_j is a
+ * prefix max across the lanes (wscan_max); a wave whose exponents spread
+ * wider runs the reference's serial scan (wv_gain_scan_serial).
+ *
+ * The arg-max stays a scan in reference order (its comparison truncates
+ * the smaller-exponent mantissa, which makes it order-dependent), but only
+ * over the bins that can be taken.  In values v = gk 2^gks: a bin is taken
+ * only if v exceeds the current champion c; the champion only rises; and
+ * every earlier bin i left behind satisfied v_i < v_c + 2^max(e_i, e_c).
+ * So bin j can be taken only if v_j > max(v_0..v_(j-1)) - 2^E_j, E_j the
+ * largest exponent up to j.  The test runs in floats (gk has 15 bits, so
+ * v is exact; the threshold's rounding error is below 2^(E_j - 9), and the
+ * float test uses 2^(E_j + 1), so it keeps a superset); a wave whose
+ * exponents leave the float range scans every bin. */
+MD void wv_gain_scan_serial(const int16_t *gk, const int16_t *gks, int lane, int *acc_out, int *sh_out,
+			    int *mn_out, int *ms_out, bool sum)
+{
+	int gk0 = gk[lane], gk1 = gk[lane + 64], gk2 = gk[NPP_NB - 1];
+	int gs0 = gks[lane], gs1 = gks[lane + 64], gs2 = gks[NPP_NB - 1];
+	int acc, sh2;		/* L, sh of the reference */
+	int mn, ms;		/* gmax, gmaxs */
+	{
+		int g = __builtin_amdgcn_readlane(gk0, 0), e = __builtin_amdgcn_readlane(gs0, 0);
+		acc = g << 7;
+		sh2 = e - 1;
+		mn = g;
+		ms = e;
+	}
+	/* one bin: branch-free (selects), shift counts clamped to 31 where the
+	 * reference's saturating shift would give 0 (operands are >= 0) */
+	auto shc = [](int k) { return k < 0 ? 0 : (k > 31 ? 31 : k); };
+	auto step = [&](int g, int e, int ee) {
+		/* cmp_shift(gmax, gmaxs, g, e) < 0 for non-negative mantissas:
+		 * the value with the smaller exponent truncated to the larger */
+		int d = ms - e;
+		int a1 = d > 0 ? mn : mn >> shc(-d);
+		int b1 = d > 0 ? g >> shc(d) : g;
+		bool take = a1 < b1;
+		mn = take ? g : mn;
+		ms = take ? e : ms;
+		if (sum) {
+			int t = sh2 - ee;
+			int n = t - 7;	/* L_shr(gk, t - 7), no saturation for t >= 1 */
+			int term = n >= 0 ? g >> shc(n) : g << shc(-n);
+			int accb = (acc >> shc(-t)) + (g << 7);
+			acc = t > 0 ? acc + term : accb;
+			sh2 = t > 0 ? sh2 : ee;
+		}
+	};
+	#pragma unroll 2
+	for (int i = 1; i < 64; i++) {
+		int e = __builtin_amdgcn_readlane(gs0, i);
+		step(__builtin_amdgcn_readlane(gk0, i), e, e);
+	}
+	#pragma unroll 2
+	for (int i = 0; i < 64; i++) {
+		int e = __builtin_amdgcn_readlane(gs1, i);
+		step(__builtin_amdgcn_readlane(gk1, i), e, e);
+	}
+	step(gk2, gs2, gs2 - 1);
+	*acc_out = acc;
+	*sh_out = sh2;
+	*mn_out = mn;
+	*ms_out = ms;
+}
+
+MD void wv_gain_scan(const int16_t *gk, const int16_t *gks, int lane, Word16 *gav, Word16 *gavs,
+		     Word16 *gmax, Word16 *gmaxs)
+{
+	const int g0 = gk[lane], g1 = gk[lane + 64], g2 = gk[NPP_NB - 1];
+	const int e0 = gks[lane], e1 = gks[lane + 64], e2 = gks[NPP_NB - 1];
+	/* ---- the average ---- */
+	const int a0 = lane == 0 ? e0 - 1 : e0, a2 = e2 - 1;
+	const int M0 = wscan_max(a0);
+	const int M1 = max(__builtin_amdgcn_readlane(M0, 63), wscan_max(e1));
+	const int M2 = max(__builtin_amdgcn_readlane(M1, 63), a2);	/* the final shift */
+	const int dmax = M2 - __builtin_amdgcn_readlane(a0, 0);
+	int acc, sh2, mn, ms;
+	bool serial_sum = dmax > 32;
+	if (!serial_sum) {
+		auto term = [](int g, int t) { return t >= 7 ? g >> (t - 7 > 31 ? 31 : t - 7) : g << (7 - t); };
+		const int t0 = term(g0, M0 - a0), t1 = term(g1, M1 - e1), t2 = term(g2, M2 - a2);
+		const int d0 = M2 - M0, d1 = M2 - M1;	/* 0 .. 32 */
+		auto ip = [](int t, int d) { return d >= 32 ? 0 : t >> d; };
+		auto fp = [](int t, int d) {
+			return d == 0 ? 0u : (uint32_t) ((uint64_t) (uint32_t) t << (32 - d));
+		};
+		const uint32_t f0 = fp(t0, d0), f1 = fp(t1, d1);
+		const int si = wsum(ip(t0, d0) + ip(t1, d1)) + t2;
+		const int slo = wsum((int) ((f0 & 0xffffu) + (f1 & 0xffffu)));
+		const int shi = wsum((int) ((f0 >> 16) + (f1 >> 16)));
+		acc = si + ((shi + (slo >> 16)) >> 16);
+		sh2 = M2;
+	}
+	/* ---- the arg-max over the bins that can be taken ---- */
+	const int emx = max(wmax(max(e0, e1)), e2), emn = min(-wmax(-min(e0, e1)), e2);
+	if (serial_sum || emx > 100 || emn < -100) {
+		int a, s2;
+		wv_gain_scan_serial(gk, gks, lane, &a, &s2, &mn, &ms, serial_sum);
+		if (serial_sum) {
+			acc = a;
+			sh2 = s2;
+		}
+	} else {
+		const float v0 = ldexpf((float) g0, e0), v1 = ldexpf((float) g1, e1), v2 = ldexpf((float) g2, e2);
+		const int E0 = wscan_max(e0);
+		const int E1 = max(__builtin_amdgcn_readlane(E0, 63), wscan_max(e1));
+		const int E2 = max(__builtin_amdgcn_readlane(E1, 63), e2);
+		const float I0 = wscan_maxf(v0);
+		const float I1 = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(I0), 63)), wscan_maxf(v1));
+		const float I2 = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(I1), 63)), v2);
+		const bool c0 = v0 > I0 - ldexpf(1.0f, E0 + 1) && lane != 0;
+		const bool c1 = v1 > I1 - ldexpf(1.0f, E1 + 1);
+		const bool c2 = v2 > I2 - ldexpf(1.0f, E2 + 1);
+		uint64_t m0 = __ballot(c0), m1 = __ballot(c1);
+		mn = __builtin_amdgcn_readlane(g0, 0);
+		ms = __builtin_amdgcn_readlane(e0, 0);
+		auto shc = [](int k) { return k < 0 ? 0 : (k > 31 ? 31 : k); };
+		auto step = [&](int g, int e) {
+			int d = ms - e;
+			int x = d > 0 ? mn : mn >> shc(-d);
+			int y = d > 0 ? g >> shc(d) : g;
+			bool take = x < y;
+			mn = take ? g : mn;
+			ms = take ? e : ms;
+		};
+		while (m0) {
+			const int k = __builtin_ctzll(m0);
+			m0 &= m0 - 1;
+			step(__builtin_amdgcn_readlane(g0, k), __builtin_amdgcn_readlane(e0, k));
+		}
+		while (m1) {
+			const int k = __builtin_ctzll(m1);
+			m1 &= m1 - 1;
+			step(__builtin_amdgcn_readlane(g1, k), __builtin_amdgcn_readlane(e1, k));
+		}
+		if (c2)
+			step(g2, e2);
+	}
+	Word32 L = acc;
+	if (L == 0)
+		L = 1;
+	Word16 t1 = norm_l(L);
+	*gav = extract_h(L_shl(L, t1));
+	*gavs = add(sub((Word16) sh2, t1), 2);
+	*gmax = (Word16) mn;
+	*gmaxs = (Word16) ms;
+}
+
 /* process_frame :1212 -- one 256-sample analysis/synthesis frame; in and
  * out are 256-sample LDS buffers */
 MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *out, const WvConst *kc,
@@ -468,7 +695,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	Word16 Ysh = add(ash, g);
 	Word16 YYavs = shl(Ysh, 1);
 	int maxs = SW_MIN_;
-	LANE_LOOP(i, NPP_NB) {
+	BIN_PASSES(t, i, {
 		Word32 v;
 		if (i == 0)
 			v = L_mult(yb[0], yb[0]);
@@ -482,13 +709,13 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 		w->YY[i] = extract_h(L_shl(v, n));
 		w->YY_shift[i] = sub(YYavs, n);
 		maxs = max(maxs, (int) w->YY_shift[i]);
-	}
+	})
 	maxs = wmax(maxs);
 	int part = 0;
 	/* |Y| of the lane's bins lane + 64 t: read back only by the same lane,
 	 * so it stays in registers (BIN_LOOP) */
 	int16_t ymag[3] = {0, 0, 0}, ymag_sh[3] = {0, 0, 0};
-	BIN_LOOP(t, i) {
+	BIN_PASSES(t, i, {
 		Word16 y = w->YY[i], ys = w->YY_shift[i];
 		if (ys & 1) {
 			y = shr(y, 1);
@@ -498,8 +725,9 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 		ymag_sh[t] = shr(ys, 1);
 		w->YY_shift[i] = sub(w->YY_shift[i], 8);
 		/* maxs is taken before the -8 (npp.c:1300-1330) */
-		part += npp_spec_term(w->YY, w->YY_shift, (Word16) maxs, i);
-	}
+		Word32 st = npp_spec_term(w->YY, w->YY_shift, (Word16) maxs, i);
+		part += ON_LANE0(t) ? st : 0;
+	})
 	L = wsum(part);
 	if (L == 0)
 		L = 1;
@@ -511,97 +739,42 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	{
 	PROF_SCOPE(36);
 	maxs = SW_MIN_;
-	LANE_LOOP(i, NPP_NB)
-		maxs = max(maxs, (int) s->sm_shift[i]);
+	BIN_PASSES(t, i, { maxs = max(maxs, (int) s->sm_shift[i]); })
 	maxs = wmax(maxs);
 	part = 0;
-	LANE_LOOP(i, NPP_NB)
-		part += npp_spec_term(s->smoothedspect, s->sm_shift, (Word16) maxs, i);
+	BIN_PASSES(t, i, {
+		Word32 st = npp_spec_term(s->smoothedspect, s->sm_shift, (Word16) maxs, i);
+		part += ON_LANE0(t) ? st : 0;
+	})
 	L = wsum(part);
 	Word16 amin;
 	Word16 anum = npp_sm_period_scalars(s, (Word16) maxs, L, YY_av, YY_av_shift, &amin);
 	part = 0;
-	LANE_LOOP(i, NPP_NB) {
+	BIN_PASSES(t, i, {
 		npp_sm_period_bin(s, w, anum, amin, i);
 		npp_bias1_bin(s, w, i);
-		part += w->var_rel[i];
-	}
+		part += ON_LANE0(t) ? (int) w->var_rel[i] : 0;
+	})
 	Word32 vsum = wsum(part);
 	wsync();
 	Word16 f1, f2;
 	Word16 vsq = npp_bias_scalars(s, w, vsum, &f1, &f2);
 	Word16 slope = npp_noise_slope(s);
-	LANE_LOOP(i, NPP_NB) {
+	BIN_PASSES(t, i, {
 		int16_t bsp, bsh, bsub, bsubsh;	/* bin i's, this lane's only */
 		npp_bias2_bin(s, w, bsp, bsh, bsub, bsubsh, vsq, f1, f2, i);
 		npp_min_search_bin(s, m, bsp, bsh, bsub, bsubsh, slope, i);
 		gk[i] = divide_s(shr(w->YY[i], 1), s->lambdaD[i]);
 		gks[i] = sub(add(w->YY_shift[i], 1), s->lambdaD_shift[i]);
-	}
+	})
 	wsync();
 	npp_min_search_post(s);
 	}
 
-	/* gain average with running rescale and the arg-max (npp.c:1336-1366):
-	 * order-dependent, so a uniform scan in reference order over the bins,
-	 * held one per lane and read with v_readlane (SGPRs, scalar ALU).
-	 * gk = divide_s(..) is in [0, 32767] and the shifts are small, so the
-	 * reference's saturating ops reduce to plain integer ones here: the
-	 * running sum is at most 129 * 2^22 < 2^31, a left-shifted term at most
-	 * 2^22 (shift <= 7), sub() of two shifts cannot saturate. */
 	Word16 gav, gavs, gmax, gmaxs;
 	{
 	PROF_SCOPE(37);
-	int gk0 = gk[lane], gk1 = gk[lane + 64], gk2 = gk[NPP_NB - 1];
-	int gs0 = gks[lane], gs1 = gks[lane + 64], gs2 = gks[NPP_NB - 1];
-	int acc, sh2;		/* L, sh of the reference */
-	int mn, ms;		/* gmax, gmaxs */
-	{
-		int g = __builtin_amdgcn_readlane(gk0, 0), e = __builtin_amdgcn_readlane(gs0, 0);
-		acc = g << 7;
-		sh2 = e - 1;
-		mn = g;
-		ms = e;
-	}
-	/* one bin: branch-free (selects), shift counts clamped to 31 where the
-	 * reference's saturating shift would give 0 (operands are >= 0) */
-	auto shc = [](int k) { return k < 0 ? 0 : (k > 31 ? 31 : k); };
-	auto step = [&](int g, int e, int ee) {
-		/* cmp_shift(gmax, gmaxs, g, e) < 0 for non-negative mantissas:
-		 * the value with the smaller exponent truncated to the larger */
-		int d = ms - e;
-		int a1 = d > 0 ? mn : mn >> shc(-d);
-		int b1 = d > 0 ? g >> shc(d) : g;
-		bool take = a1 < b1;
-		mn = take ? g : mn;
-		ms = take ? e : ms;
-		int t = sh2 - ee;
-		int n = t - 7;	/* L_shr(gk, t - 7), no saturation for t >= 1 */
-		int term = n >= 0 ? g >> shc(n) : g << shc(-n);
-		int accb = (acc >> shc(-t)) + (g << 7);
-		acc = t > 0 ? acc + term : accb;
-		sh2 = t > 0 ? sh2 : ee;
-	};
-	#pragma unroll 2
-	for (int i = 1; i < 64; i++) {
-		int e = __builtin_amdgcn_readlane(gs0, i);
-		step(__builtin_amdgcn_readlane(gk0, i), e, e);
-	}
-	#pragma unroll 2
-	for (int i = 0; i < 64; i++) {
-		int e = __builtin_amdgcn_readlane(gs1, i);
-		step(__builtin_amdgcn_readlane(gk1, i), e, e);
-	}
-	step(gk2, gs2, gs2 - 1);
-	L = acc;
-	sh = (Word16) sh2;
-	if (L == 0)
-		L = 1;
-	t1 = norm_l(L);
-	gav = extract_h(L_shl(L, t1));
-	gavs = add(sub(sh, t1), 2);
-	gmax = (Word16) mn;
-	gmaxs = (Word16) ms;
+	wv_gain_scan(gk, gks, lane, &gav, &gavs, &gmax, &gmaxs);
 	}
 	bool nflag = false;
 	if (cmp_shift(gmax, gmaxs, 18102, 6) < 0 && cmp_shift(gav, gavs, 23170, 1) < 0) {
@@ -622,8 +795,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 			s->agal_shift[i] = sub(ymag_sh[t], n);
 		}
 	} else {
-		LANE_LOOP(i, NPP_NB)
-			npp_ksi_bin(s, gk, gks, i);
+		BIN_PASSES(t, i, { npp_ksi_bin(s, gk, gks, i); })
 		t1 = mult(29491, s->Ksi_min_var);
 		t2 = mult(3277, npp_ksi_min_adapt(nflag, GM_MIN, s->SN_LT, s->SN_LT_shift));
 		Word16 kmv = add(t1, t2);
@@ -631,13 +803,13 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 		sh = norm_s(kmv);
 		t1 = shl(kmv, sh);
 		Word16 nsh = negate(sh);
-		LANE_LOOP(i, NPP_NB) {
+		BIN_PASSES(t, i, {
 			if (cmp_shift(s->ksi[i], s->ksi_shift[i], t1, nsh) < 0) {
 				s->ksi[i] = t1;
 				s->ksi_shift[i] = nsh;
 			}
 			s->qk[i] = ENH_QK_MAX;
-		}
+		})
 		if (!nflag) {
 			if (cmp_shift(gav, gavs, 23170, 1) > 0) {
 				L = L_mult(s->YY_LT, 32023);
@@ -683,16 +855,16 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 				s->SN_LT0_shift = sns;
 			}
 			bool first = !s->qk_started;
-			LANE_LOOP(i, NPP_NB) {
+			BIN_PASSES(t, i, {
 				npp_compute_qk_bin(s, s->qk, gk, gks, 19273, first, i);
 				if (s->qk[i] > ENH_QK_MAX)
 					s->qk[i] = ENH_QK_MAX;
 				else if (s->qk[i] < ENH_QK_MIN)
 					s->qk[i] = ENH_QK_MIN;
-			}
+			})
 			s->qk_started = 1;
 		}
-		BIN_LOOP(t, i) {
+		BIN_PASSES(t, i, {
 			npp_gain_log_mmse_bin(s, w, s->qk, s->Gain, gk, gks, i);
 			GainD[i] = s->Gain[i];
 			npp_gain_mod_bin(s, w, s->qk, GainD, i);
@@ -700,7 +872,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 			Word16 n = norm_l(v);
 			s->agal[i] = extract_h(L_shl(v, n));
 			s->agal_shift[i] = sub(ymag_sh[t], n);
-		}
+		})
 	}
 	}
 	wsync();
@@ -736,12 +908,13 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 		out[i] = mult(shl(yb[2 * i], osh), kc->win[i >> 6]);
 	/* noise power for the next frame (npp.c:1621-1635) */
 	maxs = SW_MIN_;
-	LANE_LOOP(i, NPP_NB)
-		maxs = max(maxs, (int) s->lambdaD_shift[i]);
+	BIN_PASSES(t, i, { maxs = max(maxs, (int) s->lambdaD_shift[i]); })
 	maxs = wmax(maxs);
 	part = 0;
-	LANE_LOOP(i, NPP_NB)
-		part += npp_spec_term(s->lambdaD, s->lambdaD_shift, (Word16) maxs, i);
+	BIN_PASSES(t, i, {
+		Word32 st = npp_spec_term(s->lambdaD, s->lambdaD_shift, (Word16) maxs, i);
+		part += ON_LANE0(t) ? st : 0;
+	})
 	L = wsum(part);
 	if (L == 0)
 		L = 1;

@@ -163,3 +163,70 @@ def test_mw_hostemu_many_channels_match_serial():
     want, _ = emu_encode_all(x.copy(), nsf)
     got, _ = emu_encode_mw(x.copy(), nsf, 4)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_mw_gpu_mapping_alternates_between_superframes():
+    """The two analysis mappings on the same records, switched between
+    superframes (lane, four-wave, lane, ...): the 1,024-channel goldens.
+    Both mappings read and write the channel records in one layout, so any
+    superframe can run on either (engine.hip ana_launch's live-count pick
+    relies on that)."""
+    from pairphone_amd import MelpeEngine
+    g = golden()
+    C, nsf = g["channels"], g["superframes"]
+    x = signals(g["seed"], C, nsf)
+    eng = MelpeEngine(C)
+    k = [0]
+
+    def enc(sp):
+        eng.set_ana_waves(1 if (k[0] // 3) % 2 == 0 else 4)
+        k[0] += 1
+        return eng.encode(sp)
+    bits, npp = run_superframes(enc, x, nsf)
+    bad = [c for c in range(C) if sha(bits[c]) != g["bits_sha256"][c]]
+    assert not bad, "bitstream mismatch on %d channels, first %s" % (len(bad), bad[:8])
+
+
+def _gpu_encode_masked(C, masks, live_max, waves, seed):
+    """C channels under per-superframe activity masks [nsf, C]; returns bits
+    [nsf, C, 11] (0xAB where a channel was inactive)"""
+    import torch
+    from pairphone_amd import MelpeEngine
+    dev = torch.device("cuda", 0)
+    eng = MelpeEngine(C)
+    eng.set_ana_waves(waves)
+    eng.set_mw_live_max(live_max)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    eng.synth_seed(seed)
+    nsf = masks.shape[0]
+    pcm = torch.empty((C, 540), dtype=torch.int16, device=dev)
+    bits = torch.full((nsf, C, 11), 0xAB, dtype=torch.uint8, device=dev)
+    m = torch.from_numpy(masks.astype(np.uint8)).to(dev)
+    for k in range(nsf):
+        eng.synth_dev(pcm.data_ptr(), 540, s)
+        eng.encode_dev(bits[k].data_ptr(), pcm.data_ptr(), m[k].data_ptr(), s)
+    torch.cuda.synchronize(dev)
+    eng.close()
+    return bits.cpu().numpy()
+
+
+@pytest.mark.gpu
+def test_mw_gpu_live_count_pick_ragged():
+    """65,536 channels (above the four-wave kernel's channel count) under
+    ragged masks whose live count crosses 32,768 both ways: with the
+    live-count pick on (the default) every superframe with <= 32,768 live
+    channels runs k_enc_ana_mw, the others the lane kernels, decided on the
+    device.  Every channel's bits equal the lane kernels' alone (pick off)
+    and the four-wave kernel's alone."""
+    C, nsf = 65536, 10
+    rng = np.random.default_rng(12)
+    live = [60000, 20000, 32768, 32769, 1000, 45000, 30000, 64, 65536, 16000]
+    masks = np.zeros((nsf, C), bool)
+    for k, n in enumerate(live):
+        masks[k, rng.choice(C, n, replace=False)] = True
+    got = _gpu_encode_masked(C, masks, 32768, 0, 5)
+    lane = _gpu_encode_masked(C, masks, 0, 0, 5)
+    np.testing.assert_array_equal(got, lane)
+    mw = _gpu_encode_masked(C, masks, 0, 4, 5)
+    np.testing.assert_array_equal(got, mw)

@@ -115,33 +115,6 @@ def test_encode_gpu_1024_channels_match_golden():
     assert not badn, "NPP output mismatch on %d channels, first %s" % (len(badn), badn[:8])
 
 
-_OPT_IN_CHILD = r"""
-import sys
-sys.path.insert(0, sys.argv[1])
-sys.path.insert(0, sys.argv[1] + "/tests")
-import test_encode as t
-from pairphone_amd import MelpeEngine
-g = t.golden()
-C, nsf = g["channels"], g["superframes"]
-bits, npp = t.run_superframes(MelpeEngine(C).encode, t.signals(g["seed"], C, nsf), nsf)
-bad = [c for c in range(C) if t.sha(bits[c]) != g["bits_sha256"][c] or t.sha(npp[c]) != g["npp_sha256"][c]]
-print("mismatch", len(bad), bad[:8])
-sys.exit(1 if bad else 0)
-"""
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("env", ["MELPE_LSFW", "MELPE_BANDS"])
-def test_encode_gpu_opt_in_analysis_splits_match_golden(env):
-    """the opt-in launch orders of the lane analysis (lsf_vq on a wave per
-    channel, k_lsf.hip; the voicing bands on four lanes per channel,
-    k_band.hip), read once per process: a child process per order runs the
-    1024-channel goldens"""
-    r = subprocess.run([sys.executable, "-c", _OPT_IN_CHILD, ROOT], env=dict(os.environ, **{env: "1"}),
-                       capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-
-
 def edge_signals(n):
     rng = np.random.default_rng(5)
     t = np.arange(n)
@@ -229,8 +202,7 @@ def test_single_stream_dropin_matches_golden():
 
 def emu_encode_split(x, nsf, fn="emu_encode_ana_split"):
     """the split lane analysis (encoder.h analysis_a / analysis_b, as
-    k_enc_ana / k_enc_harm / k_enc_tail run it; fn="emu_encode_ana_split3":
-    with the voicing bands 1..4 in k_enc_band's chains), NPP first"""
+    k_enc_ana / k_enc_harm / k_enc_tail run it), NPP first"""
     lib = emu()
     lib.emu_encode_npp.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     f = getattr(lib, fn)
@@ -247,12 +219,9 @@ def emu_encode_split(x, nsf, fn="emu_encode_ana_split"):
     return out
 
 
-@pytest.mark.parametrize("fn", ["emu_encode_ana_split", "emu_encode_ana_split3",
-                                "emu_encode_ana_split4"])
-def test_split_analysis_hostemu_matches_golden(fn):
-    """8 golden channels x 10 s through analysis_a (or analysis_a1, the band
-    chains, analysis_a2), find_harm on the written residuals, analysis_b:
-    the goldens' bits and NPP samples"""
+def test_split_analysis_hostemu_matches_golden(fn="emu_encode_ana_split"):
+    """8 golden channels x 10 s through analysis_a, find_harm on the written
+    residuals, analysis_b: the goldens' bits and NPP samples"""
     g = golden()
     ch, nsf = 8, g["superframes"]
     bits, npp = emu_encode_split(signals(g["seed"], ch, nsf), nsf, fn)
@@ -261,9 +230,7 @@ def test_split_analysis_hostemu_matches_golden(fn):
         assert sha(npp[c]) == g["npp_sha256"][c], "channel %d npp" % c
 
 
-@pytest.mark.parametrize("fn", ["emu_encode_ana_split", "emu_encode_ana_split3",
-                                "emu_encode_ana_split4"])
-def test_split_analysis_hostemu_edge_signals_match_serial(fn):
+def test_split_analysis_hostemu_edge_signals_match_serial(fn="emu_encode_ana_split"):
     nsf = 16
     sig = edge_signals(nsf * 540)
     x = np.stack([sig[k] for k in sorted(sig)])

@@ -27,7 +27,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "")
+    """demangled kernel name without its argument list and return type:
+    'void k_enc_ana<1>(EncState*, ...)' -> 'k_enc_ana<1>'"""
+    n = name.split("(")[0]
+    return n[5:] if n.startswith("void ") else n
+
+
+def is_codec(name):
+    return short(name).startswith("k_")
 
 
 def kernel_stats(db):
@@ -58,35 +65,35 @@ def main():
         rows = kernel_stats(kt[0])
         with open(os.path.join(prof, tag + "_kernel_stats.txt"), "w") as f:
             f.write("# rocprofv3 --kernel-trace --stats (%s); durations in ms (rocpd top_kernels, us / 1e3)\n" % tag)
-            f.write("%-14s %6s %14s %12s %7s\n" % ("kernel", "calls", "total_ms", "avg_ms", "pct"))
+            f.write("%-22s %6s %14s %12s %7s\n" % ("kernel", "calls", "total_ms", "avg_ms", "pct"))
             for n, calls, tot, avg, pct in rows:
-                f.write("%-14s %6d %14.1f %12.1f %7.2f\n" % (short(n)[:14], calls, tot / 1e3,
+                f.write("%-22s %6d %14.1f %12.3f %7.2f\n" % (short(n)[:22], calls, tot / 1e3,
                                                            avg / 1e3, pct))
             # the bench's legs launch the same kernels at different sizes:
             # per launch size (grid_x = threads = channels, or waves x 64 for
             # the wave-per-channel kernels), so a leg's HIP-event average can
             # be checked against the trace
             f.write("\n# per launch size (grid_x threads); durations in ms\n")
-            f.write("%-14s %10s %6s %12s %10s\n" % ("kernel", "grid_x", "calls", "total_ms", "avg_ms"))
+            f.write("%-22s %10s %6s %12s %10s\n" % ("kernel", "grid_x", "calls", "total_ms", "avg_ms"))
             c = sqlite3.connect(kt[0])
             for n, gx, calls, tot in c.execute(
                     "select name, grid_x, count(*), sum(duration) from kernels "
-                    "where name like 'k_%' group by name, grid_x order by sum(duration) desc"):
-                if short(n).startswith("k_derive"):
+                    "group by name, grid_x order by sum(duration) desc"):
+                if not is_codec(n) or short(n).startswith("k_derive"):
                     continue
-                f.write("%-14s %10d %6d %12.1f %10.3f\n" % (short(n)[:14], gx, calls, tot / 1e6,
+                f.write("%-22s %10d %6d %12.1f %10.3f\n" % (short(n)[:22], gx, calls, tot / 1e6,
                                                            tot / 1e6 / calls))
             # dispatch by dispatch for the short series (the bench's main
             # loop: W warmup then K timed steps, whose mean is its kernel_ms)
-            f.write("\n# dispatches in order, series of <= 16 (ms)\n")
-            for n, gx in list(c.execute("select name, grid_x from kernels where name like 'k_%' "
-                                        "group by name, grid_x having count(*) <= 16")):
-                if short(n).startswith(("k_derive", "k_reset", "k_synth_seed", "k_vad_reset",
+            f.write("\n# dispatches in order, series of <= 32 (ms)\n")
+            for n, gx in list(c.execute("select name, grid_x from kernels "
+                                        "group by name, grid_x having count(*) <= 32")):
+                if not is_codec(n) or short(n).startswith(("k_derive", "k_reset", "k_synth_seed", "k_vad_reset",
                                         "k_modem_reset")):
                     continue
                 d = [r[0] / 1e6 for r in c.execute("select duration from kernels where name = ? and "
                                                    "grid_x = ? order by start", (n, gx))]
-                f.write("%-14s %10d %s\n" % (short(n)[:14], gx, " ".join("%.2f" % x for x in d)))
+                f.write("%-22s %10d %s\n" % (short(n)[:22], gx, " ".join("%.2f" % x for x in d)))
     pm = {}
     if len(sys.argv) <= 3:	# PMC summaries only with the channel count they were taken at
         return
