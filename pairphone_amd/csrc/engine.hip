@@ -79,11 +79,11 @@ int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t
 		  const int *perm, const int *nlive, int nw, uint32_t *lqbuf, int cut, hipStream_t s);
 size_t kl_enc_ana_mw_lq_words(int n);
 int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto, hipStream_t s);
-int kl_npp_warm(hipStream_t s);
-int kl_ana_warm(hipStream_t s);
-int kl_harm_warm(hipStream_t s);
-int kl_ana_mw_warm(hipStream_t s);
-int kl_dec_warm(hipStream_t s);
+int kl_npp_warm(int n, hipStream_t s);
+int kl_ana_warm(int n, hipStream_t s);
+int kl_harm_warm(int n, hipStream_t s);
+int kl_ana_mw_warm(int n, hipStream_t s);
+int kl_dec_warm(int n, hipStream_t s);
 int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
 	      const int *perm, const int *nlive,
 	      hipStream_t s);
@@ -862,11 +862,12 @@ const char *melpe_last_error(void)
  * - the analysis hand-over buffers (the split lane analysis' residuals; the
  *   multi-wave kernel's score rows up to its 512 resident workgroups);
  * - the private-segment scratch of every codec kernel (the lane kernels
- *   hold ~27 KB per lane): the runtime reserves a queue's scratch at the
- *   first dispatch that needs it, so one empty workgroup of each kernel is
- *   dispatched on the engine's stream and waited for.  (Scratch is held per
- *   hardware queue: a caller's own stream may map to another queue, whose
- *   first dispatch reserves it again.)
+ *   hold ~27 KB per lane): the runtime sizes a queue's scratch by the
+ *   dispatches it sees, so each kernel is dispatched once on the engine's
+ *   stream with the grid of a real launch over the engine's channels and
+ *   no live channel (every lane exits at once), and waited for.  (Scratch
+ *   is held per hardware queue: a caller's own stream may map to another
+ *   queue, whose first dispatch reserves it again.)
  */
 static int engine_reserve(melpe_engine *e)
 {
@@ -883,9 +884,9 @@ static int engine_reserve(melpe_engine *e)
 		return fail("melpe_engine_create: multi-wave score rows", er);
 	}
 	e->lq_channels = mw;
-	int (*warm[])(hipStream_t) = {kl_npp_warm, kl_ana_warm, kl_harm_warm, kl_ana_mw_warm, kl_dec_warm};
+	int (*warm[])(int, hipStream_t) = {kl_npp_warm, kl_ana_warm, kl_harm_warm, kl_ana_mw_warm, kl_dec_warm};
 	for (auto f : warm)
-		if ((er = (hipError_t) f(e->stream)) != hipSuccess)
+		if ((er = (hipError_t) f(f == kl_ana_mw_warm ? mw : e->channels, e->stream)) != hipSuccess)
 			return fail("melpe_engine_create: codec kernel scratch could not be reserved", er);
 	if ((er = hipStreamSynchronize(e->stream)) != hipSuccess)
 		return fail("melpe_engine_create: codec kernel scratch could not be reserved", er);

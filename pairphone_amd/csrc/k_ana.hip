@@ -96,11 +96,12 @@ extern "C" int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto,
 	return (int) hipGetLastError();
 }
 
-/* one workgroup with no live channel (every lane exits at once): the launch
- * still makes the runtime reserve the kernel's private-segment scratch
- * (engine.hip melpe_engine_create) */
-extern "C" int kl_ana_warm(hipStream_t s)
+/* the grid of a launch over n channels with no live channel (every lane
+ * exits at once): the runtime still reserves the private-segment scratch
+ * such a launch needs (engine.hip engine_reserve) */
+extern "C" int kl_ana_warm(int n, hipStream_t s)
 {
-	k_enc_ana<1><<<1, WAVE, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, -1);
+	k_enc_ana<1><<<grid_for(n), WAVE, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+						   -1);
 	return (int) hipGetLastError();
 }

@@ -156,9 +156,9 @@ extern "C" int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, co
 	return (int) hipGetLastError();
 }
 
-extern "C" int kl_ana_mw_warm(hipStream_t s)
+extern "C" int kl_ana_mw_warm(int n, hipStream_t s)
 {
-	k_enc_ana_mw<4><<<1, WAVE * 4, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr,
-					       nullptr, INT32_MAX);
+	k_enc_ana_mw<4><<<grid_for(n), WAVE * 4, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr,
+							 nullptr, INT32_MAX);
 	return (int) hipGetLastError();
 }

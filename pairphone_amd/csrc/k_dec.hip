@@ -55,9 +55,12 @@ extern "C" int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const 
 	return (int) hipGetLastError();
 }
 
-extern "C" int kl_dec_warm(hipStream_t s)
+extern "C" int kl_dec_warm(int n, hipStream_t s)
 {
-	k_decode<<<1, WAVE, IDFT_LDS_WORDS * sizeof(int16_t), s>>>(nullptr, nullptr, nullptr, nullptr, 0,
-								      nullptr, nullptr);
+	int b = DEC_BLOCK;
+	while (b > WAVE && (n + b - 1) / b < 1024)
+		b /= 2;
+	k_decode<<<(n + b - 1) / b, b, IDFT_LDS_WORDS * sizeof(int16_t), s>>>(nullptr, nullptr, nullptr, nullptr,
+									     0, nullptr, nullptr);
 	return (int) hipGetLastError();
 }

@@ -224,9 +224,9 @@ extern "C" int kl_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active, 
 	return (int) hipGetLastError();
 }
 
-extern "C" int kl_harm_warm(hipStream_t s)
+extern "C" int kl_harm_warm(int n, hipStream_t s)
 {
-	k_enc_harm<<<1, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr, -1);
-	k_enc_tail<<<1, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr, -1);
+	k_enc_harm<<<n, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr, -1);
+	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr, -1);
 	return (int) hipGetLastError();
 }

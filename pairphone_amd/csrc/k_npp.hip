@@ -72,8 +72,8 @@ extern "C" int kl_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active, int
 	return (int) hipGetLastError();
 }
 
-extern "C" int kl_npp_warm(hipStream_t s)
+extern "C" int kl_npp_warm(int n, hipStream_t s)
 {
-	k_enc_npp<<<1, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0);
+	k_enc_npp<<<n, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0);
 	return (int) hipGetLastError();
 }

@@ -230,3 +230,31 @@ def test_mw_gpu_live_count_pick_ragged():
     np.testing.assert_array_equal(got, lane)
     mw = _gpu_encode_masked(C, masks, 0, 4, 5)
     np.testing.assert_array_equal(got, mw)
+
+
+@pytest.mark.gpu
+def test_engine_reserves_scratch_at_create():
+    """An engine's kernels get their private-segment scratch at create
+    (engine.hip engine_reserve), so a caller that then fills the device
+    (here torch's allocator, up to out-of-memory) still encodes and decodes:
+    a shortage shows at melpe_engine_create, never mid-stream."""
+    import torch
+    from pairphone_amd import MelpeEngine
+    dev = torch.device("cuda", 0)
+    C = 65536
+    eng = MelpeEngine(C)
+    hog, size = [], 1 << 30
+    while size >= (1 << 24):
+        try:
+            hog.append(torch.empty(size, dtype=torch.uint8, device=dev))
+        except RuntimeError:
+            size //= 2
+    try:
+        pcm = np.zeros((C, 540), np.int16)
+        bits = eng.encode(pcm)          # host path: staging buffers are the engine's own
+        out = eng.decode(bits)
+        assert bits.shape == (C, 11) and out.shape == (C, 540)
+    finally:
+        del hog
+        torch.cuda.empty_cache()
+        eng.close()
