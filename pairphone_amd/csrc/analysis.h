@@ -1180,13 +1180,25 @@ MN Word16 updateEn(Word16 prev, Word16 ifact, Word16 curr)
 MN void lpfilt(const int16_t *in, int16_t *lp, int len)
 {
 	const int16_t *lpar = TB(lpar);
+	const Word16 c0 = lpar[0], c1 = lpar[1], c2 = lpar[2], c3 = lpar[3];
 	v_copy(lp, &lp[len], PIT_COR_LEN - len);
-	for (int i = 0; i < len; i++) {
-		Word32 s = L_shr(L_deposit_h(in[i]), 3);
-		for (int j = 0; j < 4; j++)
-			s = L_mac(s, lp[PIT_COR_LEN - len + i - j - 1], lpar[j]);
-		lp[PIT_COR_LEN - len + i] = r_ound(s);
-	}
+	/* the four past outputs in registers (the reference reads them back from
+	 * lp), the inputs a block ahead; the taps in the reference's order */
+	int16_t *y = &lp[PIT_COR_LEN - len];
+	Word16 y1 = y[-1], y2 = y[-2], y3 = y[-3], y4 = y[-4];
+	v_batch(in, y, len, [&](int, int16_t x) {
+		Word32 s = L_shr(L_deposit_h(x), 3);
+		s = L_mac(s, y1, c0);
+		s = L_mac(s, y2, c1);
+		s = L_mac(s, y3, c2);
+		s = L_mac(s, y4, c3);
+		Word16 o = r_ound(s);
+		y4 = y3;
+		y3 = y2;
+		y2 = y1;
+		y1 = o;
+		return o;
+	});
 }
 
 /* ivfilt :138 -- 2nd-order inverse filter from 40-bit autocorrelations */
@@ -1244,12 +1256,17 @@ MN void ivfilt(int16_t *iv, const int16_t *lp, int len)
 		}
 		pc1 = mult(rc1, pc2);
 	}
-	for (int i = 0; i < len; i++) {
-		int k = PIT_COR_LEN - len + i;
-		Word32 t = L_shl(L_deposit_l(lp[k]), 13);
-		t = L_sub(t, L_mult(pc1, lp[k - 1]));
-		t = L_sub(t, L_mult(pc2, lp[k - 2]));
-		iv[k] = r_ound(L_shl(t, 3));
+	{	/* lp[k - 1], lp[k - 2] ride in registers, lp[k] a block ahead */
+		const int k0 = PIT_COR_LEN - len;
+		Word16 l1 = lp[k0 - 1], l2 = lp[k0 - 2];
+		v_batch(&lp[k0], &iv[k0], len, [&](int, int16_t x) {
+			Word32 t = L_shl(L_deposit_l(x), 13);
+			t = L_sub(t, L_mult(pc1, l1));
+			t = L_sub(t, L_mult(pc2, l2));
+			l2 = l1;
+			l1 = x;
+			return r_ound(L_shl(t, 3));
+		});
 	}
 }
 
@@ -1781,11 +1798,15 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 	norm40(&rk, &rks, &Lrk);
 	Word16 maxgp = cor_gain(&Lr0, &r0s, rks, Lrk, A, true);
 	int lo = 0, hi = hp;
-	const bool blocked = (hp - lp) == 10;
 	Word40 blk[10];
 #if !defined(MELPE_OPCOUNT)
-	if (blocked)
-		fc_corr_any(in, hp, win, blk);
+	/* Lag hp-1-n's window does not depend on how many lags the scan has, so
+	 * the ten-lag block holds the sums of a scan clamped at MINPITCH or
+	 * MAXPITCH too (its first hp - lp lags; the unused lags read inside
+	 * in[0 .. PIT_COR_LEN)).  One pass for every lane, instead of a
+	 * per-lag scalar sum wherever a lane's pitch sits near either bound. */
+	const bool blocked = true;
+	fc_corr_any(in, hp, win, blk);
 	/* The r0 / rk updates alternate with the parity of the lag, which
 	 * differs between lanes: one update of the selected side per lag,
 	 * branch-free (the reference's L40_msu / L40_mac pairs, in order). */
@@ -1818,6 +1839,7 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 			maxgp = g;
 	}
 #else
+	const bool blocked = (hp - lp) == 10;
 	if (blocked) {
 		if (hp & 1)
 			fc_corr10<1>(in, hp, win, blk);

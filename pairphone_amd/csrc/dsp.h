@@ -477,13 +477,52 @@ MD void v_map(int16_t *d, const int16_t *s, int n, F f)
 #define MELPE_VMAP_IIR 0
 #endif
 
+/* out[i] = f(i, in[i]) for i = 0 .. n-1, in order, the inputs loaded a block
+ * ahead of the outputs stored.  A plain loop over scratch arrays waits for
+ * every load: the compiler cannot move a load above the previous store when
+ * the two arrays may overlap, so each element costs a full memory round
+ * trip.  Here the loads of in[i + B .. i + 2B) are issued before out[i .. i
+ * + B) is stored, one wait per block.  Valid when out and in are disjoint,
+ * the same array, or out lies below in (a shift down: every in[j] is read
+ * before out[j] can overwrite it); a copy upward into an overlapping range
+ * runs element by element, as the reference's forward loop. */
+template <int B = 8, class F>
+MD void v_batch(const int16_t *in, int16_t *out, int n, F f)
+{
+	int i = 0;
+	if (n >= 2 * B && !(out > in && out < in + n)) {
+		int16_t v[B];
+		#pragma unroll
+		for (int q = 0; q < B; q++)
+			v[q] = in[q];
+		#pragma unroll 1
+		for (; i + 2 * B <= n; i += B) {
+			int16_t nv[B];
+			#pragma unroll
+			for (int q = 0; q < B; q++)
+				nv[q] = in[i + B + q];
+			#pragma unroll
+			for (int q = 0; q < B; q++)
+				out[i + q] = f(i + q, v[q]);
+			#pragma unroll
+			for (int q = 0; q < B; q++)
+				v[q] = nv[q];
+		}
+		#pragma unroll
+		for (int q = 0; q < B; q++)
+			out[i + q] = f(i + q, v[q]);
+		i += B;
+	}
+	for (; i < n; i++)
+		out[i] = f(i, in[i]);
+}
+
 MD void v_copy(int16_t *d, const int16_t *s, int n)	/* v_equ :136 */
 {
 #if MELPE_VMAP_COPY
 	v_map(d, s, n, [](int16_t x) { return x; });
 #else
-	for (int i = 0; i < n; i++)
-		d[i] = s[i];
+	v_batch(s, d, n, [](int, int16_t x) { return x; });
 #endif
 }
 
@@ -522,8 +561,7 @@ MD void v_equ_shr(int16_t *d, const int16_t *s, int16_t sc, int n)	/* :186 */
 #if MELPE_VMAP_COPY
 	v_map(d, s, n, [sc](int16_t x) { return (int16_t) shr(x, sc); });
 #else
-	for (int i = 0; i < n; i++)
-		d[i] = shr(s[i], sc);
+	v_batch(s, d, n, [sc](int, int16_t x) { return (int16_t) shr(x, sc); });
 #endif
 }
 
@@ -532,8 +570,7 @@ MD void v_scale(int16_t *a, int16_t sc, int n)	/* :409 */
 #if MELPE_VMAP_COPY
 	v_map(a, a, n, [sc](int16_t x) { return (int16_t) mult(x, sc); });
 #else
-	for (int i = 0; i < n; i++)
-		a[i] = mult(a[i], sc);
+	v_batch(a, a, n, [sc](int, int16_t x) { return (int16_t) mult(x, sc); });
 #endif
 }
 
@@ -776,19 +813,20 @@ MD Word16 add_shr(Word16 a, Word16 b)	/* :781 */
 MN void envelope(const int16_t *in, int16_t prev_in, int16_t *out, int n)
 {
 	/* the two past outputs ride in registers (out may be in: in[i] is
-	 * always read before out[i] is written, as in the reference) */
+	 * always read before out[i] is written, as in the reference); the
+	 * inputs come a block ahead (v_batch) */
 	Word16 pa = abs_s(prev_in), y1 = out[-1], y2 = out[-2];
-	for (int i = 0; i < n; i++) {
-		Word16 ca = abs_s(in[i]);
+	v_batch(in, out, n, [&](int, int16_t x) {
+		Word16 ca = abs_s(x);
 		Word32 acc = L_shr(L_deposit_h(sub(ca, pa)), 5);
 		acc = L_mac(acc, 31565, y1);
 		acc = L_mac(acc, -15415, y2);
 		Word16 y = r_ound(L_shl(acc, 1));
-		out[i] = y;
 		y2 = y1;
 		y1 = y;
 		pa = ca;
-	}
+		return y;
+	});
 }
 
 /* envelope, returning the exact energy (sum of L_mult(y, y)) of what it
@@ -798,18 +836,18 @@ MD int64_t envelope_e(const int16_t *in, int16_t prev_in, int16_t *out, int n)
 	PROF_SCOPE(48);
 	Word16 pa = abs_s(prev_in), y1 = out[-1], y2 = out[-2];
 	int64_t e = 0;
-	for (int i = 0; i < n; i++) {
-		Word16 ca = abs_s(in[i]);
+	v_batch(in, out, n, [&](int, int16_t x) {
+		Word16 ca = abs_s(x);
 		Word32 acc = L_shr(L_deposit_h(sub(ca, pa)), 5);
 		acc = L_mac(acc, 31565, y1);
 		acc = L_mac(acc, -15415, y2);
 		Word16 y = r_ound(L_shl(acc, 1));
-		out[i] = y;
 		e += L_mult(y, y);
 		y2 = y1;
 		y1 = y;
 		pa = ca;
-	}
+		return y;
+	});
 	return e;
 }
 
@@ -1755,6 +1793,13 @@ MN void lsp_to_freq(const int16_t *lsp, int16_t *freq, int order)
 	smag[2] = 0;
 	Word16 p2 = shr((Word16) order, 1);
 	Word16 count = 0;
+	/* a root's interpolation operands, divided after the scan: lanes find
+	 * their roots at different grid points, so dividing at each would run
+	 * the divider for the wave at nearly every point.  Only a scan with
+	 * exactly p2 roots keeps them (else the defaults below overwrite
+	 * freq[0 .. p2)), so later roots need no slot. */
+	Word32 rn[6], rd[6];
+	int16_t ri[6];
 	/* The reference steps the grid index by pc = add(pc, i), wrapping at
 	 * 512 (:668-672): term k of point i reads lsp_cos[k*i mod 512], never
 	 * saturating (k*i <= 1280).  Those indices are wave-uniform and
@@ -1782,11 +1827,11 @@ MN void lsp_to_freq(const int16_t *lsp, int16_t *freq, int order)
 				prev_less = true;
 			} else {
 				if (prev_less && (smag[0] ^ smag[2]) < 0) {
-					Word32 n1 = L_shr(L_sub(mag[0], mag[2]), 1);
-					Word32 d1 = L_add(L_sub(mag[0], L_shl(mag[1], 1)), mag[2]);
-					Word16 t = shr(L_divider2(n1, d1, 0, 0), 9);
-					t = add(shl(sub((Word16) i, 1), 6), t);
-					freq[count] = divide_s(t, shl(512, 5));
+					if (count < 6) {
+						rn[count] = L_shr(L_sub(mag[0], mag[2]), 1);
+						rd[count] = L_add(L_sub(mag[0], L_shl(mag[1], 1)), mag[2]);
+						ri[count] = (int16_t) i;
+					}
 					count = add(count, 1);
 				}
 				prev_less = false;
@@ -1801,6 +1846,12 @@ MN void lsp_to_freq(const int16_t *lsp, int16_t *freq, int order)
 		freq[0] = dw0;
 		for (int i = 1; i < p2; i++)
 			freq[i] = add(freq[i - 1], dw);
+	} else {
+		for (int k = 0; k < p2; k++) {
+			Word16 t = shr(L_divider2(rn[k], rd[k], 0, 0), 9);
+			t = add(shl(sub(ri[k], 1), 6), t);
+			freq[k] = divide_s(t, shl(512, 5));
+		}
 	}
 }
 

@@ -70,13 +70,13 @@ int kl_npp(EncState *enc, int16_t *sp, int frames, int stride, const uint8_t *ac
 	   int rate1200, hipStream_t s);
 int kl_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active, int n, hipStream_t s);
 int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
-	       const int *perm, const int *nlive, int16_t *res, int cut, hipStream_t s);
+	       const int *perm, const int *nlive, int16_t *res, hipStream_t s);
 int kl_enc_harm(EncState *enc, const int16_t *res, const uint8_t *active, int n, const int *perm,
-		const int *nlive, int cut, hipStream_t s);
+		const int *nlive, hipStream_t s);
 int kl_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active, int n, const int *perm,
-		const int *nlive, int cut, hipStream_t s);
+		const int *nlive, hipStream_t s);
 int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
-		  const int *perm, const int *nlive, int nw, uint32_t *lqbuf, int cut, hipStream_t s);
+		  const int *perm, const int *nlive, int nw, uint32_t *lqbuf, hipStream_t s);
 size_t kl_enc_ana_mw_lq_words(int n);
 int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto, hipStream_t s);
 int kl_npp_warm(int n, hipStream_t s);
@@ -84,6 +84,10 @@ int kl_ana_warm(int n, hipStream_t s);
 int kl_harm_warm(int n, hipStream_t s);
 int kl_ana_mw_warm(int n, hipStream_t s);
 int kl_dec_warm(int n, hipStream_t s);
+size_t kl_ana_private(void);
+size_t kl_ana_mw_private(void);
+size_t kl_harm_private(void);
+size_t kl_dec_private(void);
 int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
 	      const int *perm, const int *nlive,
 	      hipStream_t s);
@@ -628,10 +632,16 @@ struct melpe_engine {
 	int lane_order = -1;	/* 1 on, 0 off, -1 the MELPE_BIN default */
 	int ana_waves = 0;	/* waves per 64 channels in k_enc_ana(_mw); 0: by channel count */
 	uint32_t *d_lq = nullptr;	/* k_enc_ana_mw's lsf_vq score rows (engine_reserve) */
-	int lq_channels = 0;	/* channels d_lq has rows for */
 	/* the live-count mapping (ana_launch): a superframe with at most this
 	 * many live channels runs the multi-wave kernel (0: off) */
 	int mw_live_max = MW_MAX_CHANNELS;
+	/* the live count of the latest analysis launch whose readback has
+	 * landed (pinned host word, copied after the lane-order sort) */
+	int *h_live = nullptr;
+	hipEvent_t live_ev = nullptr;
+	bool live_pending = false;
+	int last_live = -1;	/* -1: none seen yet */
+	size_t scratch_need = 0;	/* bytes of scratch the largest launch takes */
 	int16_t *d_res = nullptr;	/* the split lane analysis' windowed residuals (C x NF x LPC_FRAME) */
 	/* one event per stream this engine's *_dev calls have used, recorded
 	 * after each call: the host-side calls wait on these (engine_wait)
@@ -699,43 +709,42 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 	const int *perm = on ? b.perm : nullptr;
 	const int *nlive = on ? (const int *) (b.ctl + 2 * NBIN) : nullptr;
 	int nw = ana_waves_for(e);
-	if (nw > 1 && e->lq_channels < e->channels) {
-		/* an explicit 4-wave mapping above MW_MAX_CHANNELS: score rows for
-		 * every channel (ordered after any work still reading the old
-		 * buffer: a fresh one) */
-		uint32_t *q;
-		er = hipMalloc(&q, sizeof(uint32_t) * kl_enc_ana_mw_lq_words(e->channels));
-		if (er != hipSuccess)
-			return (int) er;
-		hipFree(e->d_lq);
-		e->d_lq = q;
-		e->lq_channels = e->channels;
-	}
-	/* Above MW_MAX_CHANNELS the engine runs the lane kernels -- unless the
-	 * superframe has few live channels (ragged streams, BASELINE config 5):
-	 * with the lane order on, the live count is on the device (the bin sort
-	 * counted it), so both mappings are enqueued, each guarded by that count
-	 * (the lane kernels exit when at most mw_live_max channels are live, the
-	 * multi-wave kernel when more are), and the host never waits for it. */
-	const bool live_pick = nw == 1 && on && e->ana_waves == 0 && ana_nw_env() < 0 &&
+	/* Above MW_MAX_CHANNELS the engine runs the lane kernels -- unless few
+	 * channels are live (ragged streams, BASELINE config 5).  The count is
+	 * on the device (the lane-order sort counted it); the host takes the
+	 * latest one whose readback has landed, typically the previous
+	 * superframe's, so it never waits.  Either mapping gives the same bits
+	 * for any live count (the four-wave kernel grid-strides over every live
+	 * slot), so a stale count only costs speed. */
+	const bool auto_live = nw == 1 && on && e->ana_waves == 0 && ana_nw_env() < 0 &&
 			       e->mw_live_max > 0 && harm_split();
-	const int cut = live_pick ? e->mw_live_max : -1;
+	if (auto_live && e->live_pending && hipEventQuery(e->live_ev) == hipSuccess) {
+		e->last_live = *e->h_live;
+		e->live_pending = false;
+	}
+	if (auto_live && e->last_live >= 0 && e->last_live <= e->mw_live_max)
+		nw = 4;
 	int rc;
 	if (nw == 1 && harm_split()) {
 		/* lane-per-channel analysis up to the Fourier magnitudes, the
 		 * magnitudes with a wave per channel, then the packing (k_harm.hip) */
-		rc = kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, e->d_res, cut, s);
+		rc = kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, e->d_res, s);
 		if (rc == 0)
-			rc = kl_enc_harm(e->d_enc, e->d_res, d_act, e->channels, perm, nlive, cut, s);
+			rc = kl_enc_harm(e->d_enc, e->d_res, d_act, e->channels, perm, nlive, s);
 		if (rc == 0)
-			rc = kl_enc_tail(e->d_enc, d_bits, d_act, e->channels, perm, nlive, cut, s);
-		if (rc == 0 && live_pick)
-			rc = kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->mw_live_max, perm, nlive, 4, e->d_lq,
-					   cut, s);
+			rc = kl_enc_tail(e->d_enc, d_bits, d_act, e->channels, perm, nlive, s);
 	} else {
-		rc = nw == 1 ? kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nullptr, -1, s)
+		rc = nw == 1 ? kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nullptr, s)
 			     : kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nw,
-					     e->d_lq, INT32_MAX, s);
+					     e->d_lq, s);
+	}
+	if (rc == 0 && auto_live && !e->live_pending) {
+		/* this launch's live count, for a later launch's choice */
+		er = hipMemcpyAsync(e->h_live, b.ctl + 2 * NBIN, sizeof(int), hipMemcpyDeviceToHost, s);
+		if (er == hipSuccess)
+			er = hipEventRecord(e->live_ev, s);
+		rc = (int) er;
+		e->live_pending = rc == 0;
 	}
 	if (rc == 0 && on)
 		rc = (int) bin_release(b, s);
@@ -878,12 +887,40 @@ static int engine_reserve(melpe_engine *e)
 		e->d_res = nullptr;
 		return fail("melpe_engine_create: analysis residual buffer", er);
 	}
-	const int mw = e->channels < MW_MAX_CHANNELS ? e->channels : MW_MAX_CHANNELS;
-	if ((er = hipMalloc(&e->d_lq, sizeof(uint32_t) * kl_enc_ana_mw_lq_words(mw))) != hipSuccess) {
+	if ((er = hipMalloc(&e->d_lq, sizeof(uint32_t) * kl_enc_ana_mw_lq_words(e->channels))) != hipSuccess) {
 		e->d_lq = nullptr;
 		return fail("melpe_engine_create: multi-wave score rows", er);
 	}
-	e->lq_channels = mw;
+	const int mw = e->channels < MW_MAX_CHANNELS ? e->channels : MW_MAX_CHANNELS;
+	if ((er = hipHostMalloc((void **) &e->h_live, sizeof(int), hipHostMallocDefault)) != hipSuccess ||
+	    (er = hipEventCreateWithFlags(&e->live_ev, hipEventDisableTiming)) != hipSuccess)
+		return fail("melpe_engine_create: live-count readback", er);
+	/* The runtime keeps a queue's scratch between dispatches only below its
+	 * scratch limit threshold; above it the allocation is made for the
+	 * dispatch and given back.  Raise the threshold (never lower it) to
+	 * what this engine's largest launch needs: private bytes per lane x 64
+	 * lanes x the waves of the launch (lane kernels: one per 64 channels;
+	 * the four-wave kernel: 4 per group, at most 512 groups). */
+	{
+		const size_t lane = kl_ana_private() > kl_harm_private() ? kl_ana_private() : kl_harm_private();
+		const size_t per_wave = (lane > kl_dec_private() ? lane : kl_dec_private()) * WAVE;
+		const size_t mw_wave = kl_ana_mw_private() * WAVE;
+		const size_t waves = (size_t) (e->channels + WAVE - 1) / WAVE;
+		const size_t mw_waves = 4 * (size_t) ((mw + WAVE - 1) / WAVE);
+		size_t need = per_wave * waves;
+		if (mw_wave * mw_waves > need)
+			need = mw_wave * mw_waves;
+		size_t cur = 0, mx = 0;
+		if (hipDeviceGetLimit(&cur, hipExtLimitScratchCurrent) == hipSuccess &&
+		    hipDeviceGetLimit(&mx, hipExtLimitScratchMax) == hipSuccess && need > cur) {
+			if (need > mx)
+				return fail_msg("melpe_engine_create: the codec kernels' scratch exceeds the "
+						"device's scratch limit (fewer channels per engine)");
+			if ((er = hipDeviceSetLimit(hipExtLimitScratchCurrent, need)) != hipSuccess)
+				return fail("melpe_engine_create: raising the scratch limit", er);
+		}
+		e->scratch_need = need;
+	}
 	int (*warm[])(int, hipStream_t) = {kl_npp_warm, kl_ana_warm, kl_harm_warm, kl_ana_mw_warm, kl_dec_warm};
 	for (auto f : warm)
 		if ((er = (hipError_t) f(f == kl_ana_mw_warm ? mw : e->channels, e->stream)) != hipSuccess)
@@ -984,6 +1021,10 @@ int melpe_engine_destroy(melpe_engine *e)
 	hipFree(e->bin_dec.perm);
 	hipFree(e->d_lq);
 	hipFree(e->d_res);
+	if (e->h_live)
+		hipHostFree(e->h_live);
+	if (e->live_ev)
+		hipEventDestroy(e->live_ev);
 	for (auto &m : e->marks)
 		hipEventDestroy(m.second);
 	if (e->bin_enc.done)

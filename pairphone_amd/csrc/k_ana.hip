@@ -22,15 +22,13 @@ struct AnaLane {
 template <int MODE>
 __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits,
 						  const uint8_t *active, int n, const int *perm,
-						  const int *nlive, int16_t *res, int cut)
+						  const int *nlive, int16_t *res)
 {
 	/* lane g runs channel perm[g] when the engine ordered the live channels
-	 * by pitch class (engine.hip, MELPE_BIN), else channel g under the mask;
-	 * with at most `cut` live channels the multi-wave kernel takes the
-	 * superframe (engine.hip ana_launch) */
+	 * by pitch class (engine.hip, MELPE_BIN), else channel g under the mask */
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (perm) {
-		if (c >= *nlive || *nlive <= cut)
+		if (c >= *nlive)
 			return;
 		c = perm[c];
 	} else if (c >= n || (active && !active[c])) {
@@ -79,14 +77,12 @@ static unsigned ana_lds_bytes(void)
 }
 
 extern "C" int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
-			  int n, const int *perm, const int *nlive, int16_t *res, int cut, hipStream_t s)
+			  int n, const int *perm, const int *nlive, int16_t *res, hipStream_t s)
 {
 	if (res)
-		k_enc_ana<1><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res,
-									  cut);
+		k_enc_ana<1><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res);
 	else
-		k_enc_ana<0><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res,
-									  cut);
+		k_enc_ana<0><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res);
 	return (int) hipGetLastError();
 }
 
@@ -99,9 +95,15 @@ extern "C" int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto,
 /* the grid of a launch over n channels with no live channel (every lane
  * exits at once): the runtime still reserves the private-segment scratch
  * such a launch needs (engine.hip engine_reserve) */
+/* private-segment bytes per lane of the kernel (engine.hip engine_reserve) */
+extern "C" size_t kl_ana_private(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *) k_enc_ana<1>) == hipSuccess ? a.localSizeBytes : 0;
+}
+
 extern "C" int kl_ana_warm(int n, hipStream_t s)
 {
-	k_enc_ana<1><<<grid_for(n), WAVE, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
-						   -1);
+	k_enc_ana<1><<<grid_for(n), WAVE, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
 	return (int) hipGetLastError();
 }

@@ -72,16 +72,17 @@ template <int NW>
 __global__ __launch_bounds__(WAVE * NW, MELPE_MW_WAVES) void k_enc_ana_mw(EncState *enc, const int16_t *sp,
 									    uint8_t *bits, const uint8_t *active,
 									    int n, const int *perm, const int *nlive,
-									    uint32_t *lqbuf, int cut)
+									    uint32_t *lqbuf)
 {
-	/* a launch guarded by the live count (engine.hip ana_launch): the lane
-	 * kernels take the superframe when more than `cut` channels are live
-	 * (uniform in the workgroup, before any barrier) */
-	if (perm && *nlive > cut)
-		return;
 	__shared__ int16_t xs[XS_WORDS * WAVE];
 	const int w = threadIdx.x / WAVE, t = threadIdx.x % WAVE;
-	int c = blockIdx.x * WAVE + t;
+	/* groups of 64 slots, grid-stride: the engine launches at most 512
+	 * workgroups (all resident, two per CU), which take every live slot
+	 * however many there are (engine.hip ana_launch picks this kernel from
+	 * a live count that may be a superframe old) */
+	const int count = perm ? *nlive : n;
+	for (int grp = blockIdx.x; grp * WAVE < count; grp += gridDim.x) {
+	int c = grp * WAVE + t;
 	bool live;
 	if (perm) {
 		live = c < *nlive;
@@ -122,43 +123,60 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_MW_WAVES) void k_enc_ana_mw(EncSta
 		if (w == 0)
 			MW_T1(tp, MW_SLOT(p, 4));
 	}
-	if (!live)
-		return;
-	MW_T0(te);
-	for (int v = w; v < MW_NV; v += NW) {
-		size_t off[2], len[2];
-		int m = ana_mw_owned(v, off, len);
-		for (int k = 0; k < m; k++)
-			lane_copy((char *) rec + off[k], (const char *) &L.S + off[k], len[k]);
+	if (live) {
+		MW_T0(te);
+		for (int v = w; v < MW_NV; v += NW) {
+			size_t off[2], len[2];
+			int m = ana_mw_owned(v, off, len);
+			for (int k = 0; k < m; k++)
+				lane_copy((char *) rec + off[k], (const char *) &L.S + off[k], len[k]);
+		}
+		if (w == 0)
+			for (int k = 0; k < 11; k++)
+				bits[(size_t) c * 11 + k] = L.S.chbuf[k];
+		MW_T1(te, MW_SLOT(MW_PHASES, 1));
 	}
-	if (w == 0)
-		for (int k = 0; k < 11; k++)
-			bits[(size_t) c * 11 + k] = L.S.chbuf[k];
-	MW_T1(te, MW_SLOT(MW_PHASES, 1));
+	__syncthreads();	/* the next group reuses the exchange block */
+	}
 }
 
-/* lqbuf: LQ_ROW x (grid_for(n) * WAVE) dwords (kl_enc_ana_mw_lq_words) */
+/* workgroups of a launch over n slots: every group resident (two per CU,
+ * MW_MAX_GROUPS in all), larger counts grid-stride */
+#define MW_MAX_GROUPS 512
+static unsigned mw_grid(int n)
+{
+	unsigned g = grid_for(n);
+	return g < MW_MAX_GROUPS ? (g ? g : 1) : MW_MAX_GROUPS;
+}
+
+/* lqbuf: LQ_ROW x (mw_grid(n) * WAVE) dwords (kl_enc_ana_mw_lq_words) */
 extern "C" size_t kl_enc_ana_mw_lq_words(int n)
 {
-	return (size_t) LQ_ROW * grid_for(n) * WAVE;
+	return (size_t) LQ_ROW * mw_grid(n) * WAVE;
 }
 
 extern "C" int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
-			     int n, const int *perm, const int *nlive, int nw, uint32_t *lqbuf, int cut,
+			     int n, const int *perm, const int *nlive, int nw, uint32_t *lqbuf,
 			     hipStream_t s)
 {
 	/* 4 waves per 64 channels (2 measured no better at any channel count
 	 * and cost a third more compile time; ana_mw.h supports any count) */
 	if (nw == 4)
-		k_enc_ana_mw<4><<<grid_for(n), WAVE * 4, 0, s>>>(enc, sp, bits, active, n, perm, nlive, lqbuf, cut);
+		k_enc_ana_mw<4><<<mw_grid(n), WAVE * 4, 0, s>>>(enc, sp, bits, active, n, perm, nlive, lqbuf);
 	else
 		return (int) hipErrorInvalidValue;
 	return (int) hipGetLastError();
 }
 
+extern "C" size_t kl_ana_mw_private(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *) k_enc_ana_mw<4>) == hipSuccess ? a.localSizeBytes : 0;
+}
+
 extern "C" int kl_ana_mw_warm(int n, hipStream_t s)
 {
-	k_enc_ana_mw<4><<<grid_for(n), WAVE * 4, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr,
-							 nullptr, INT32_MAX);
+	k_enc_ana_mw<4><<<mw_grid(n), WAVE * 4, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr,
+							nullptr);
 	return (int) hipGetLastError();
 }

@@ -55,6 +55,12 @@ extern "C" int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const 
 	return (int) hipGetLastError();
 }
 
+extern "C" size_t kl_dec_private(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *) k_decode) == hipSuccess ? a.localSizeBytes : 0;
+}
+
 extern "C" int kl_dec_warm(int n, hipStream_t s)
 {
 	int b = DEC_BLOCK;

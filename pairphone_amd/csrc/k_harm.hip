@@ -142,11 +142,11 @@ MD void wv_find_harm(const int16_t v[4], int16_t *fsmag, Word16 pitch, uint32_t 
  * lane order) or channel g under the mask; the three frames in order */
 __global__ __launch_bounds__(WAVE) void k_enc_harm(EncState *enc, const int16_t *res,
 						   const uint8_t *active, int n, const int *perm,
-						   const int *nlive, int cut)
+						   const int *nlive)
 {
 	int c = blockIdx.x;
 	if (perm) {
-		if (c >= *nlive || *nlive <= cut)
+		if (c >= *nlive)
 			return;
 		c = perm[c];
 	} else if (c >= n || (active && !active[c])) {
@@ -176,9 +176,9 @@ __global__ __launch_bounds__(WAVE) void k_enc_harm(EncState *enc, const int16_t 
 }
 
 extern "C" int kl_enc_harm(EncState *enc, const int16_t *res, const uint8_t *active, int n,
-			   const int *perm, const int *nlive, int cut, hipStream_t s)
+			   const int *perm, const int *nlive, hipStream_t s)
 {
-	k_enc_harm<<<n, WAVE, 0, s>>>(enc, res, active, n, perm, nlive, cut);
+	k_enc_harm<<<n, WAVE, 0, s>>>(enc, res, active, n, perm, nlive);
 	return (int) hipGetLastError();
 }
 
@@ -190,11 +190,11 @@ struct TailLane {
 };
 
 __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active,
-						   int n, const int *perm, const int *nlive, int cut)
+						   int n, const int *perm, const int *nlive)
 {
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (perm) {
-		if (c >= *nlive || *nlive <= cut)
+		if (c >= *nlive)
 			return;
 		c = perm[c];
 	} else if (c >= n || (active && !active[c])) {
@@ -218,15 +218,21 @@ __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bi
 }
 
 extern "C" int kl_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active, int n,
-			   const int *perm, const int *nlive, int cut, hipStream_t s)
+			   const int *perm, const int *nlive, hipStream_t s)
 {
-	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(enc, bits, active, n, perm, nlive, cut);
+	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(enc, bits, active, n, perm, nlive);
 	return (int) hipGetLastError();
+}
+
+extern "C" size_t kl_harm_private(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *) k_enc_tail) == hipSuccess ? a.localSizeBytes : 0;
 }
 
 extern "C" int kl_harm_warm(int n, hipStream_t s)
 {
-	k_enc_harm<<<n, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr, -1);
-	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr, -1);
+	k_enc_harm<<<n, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr);
+	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr);
 	return (int) hipGetLastError();
 }

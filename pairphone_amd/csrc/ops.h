@@ -374,6 +374,13 @@ MD Word16 norm_l(Word32 x)
 
 MD Word16 norm_s(Word16 a) { OPC(25); return norm_l(L_deposit_h(a)); }
 
+/* divide_s: floor(num * 2^15 / den) for 0 <= num < den.  On the device the
+ * quotient comes from one float reciprocal and one integer correction
+ * instead of a 32-bit integer division: N = num << 15 < 2^30 converts with
+ * relative error <= 2^-24 and v_rcp_f32 is within 1 ulp, so the float
+ * estimate q' of N / den satisfies |q' - N / den| < 2^-7 (N / den < 2^15);
+ * truncated, it is floor(N / den) or one below or above it, and the
+ * remainder N - q den (exact: q den < 2^31) picks the right one. */
 MD Word16 divide_s(Word16 num, Word16 den)
 {
 	OPC(26);
@@ -381,7 +388,16 @@ MD Word16 divide_s(Word16 num, Word16 den)
 		return 0;
 	if (num == den)
 		return SW_MAX_;
+#if defined(__HIP_DEVICE_COMPILE__)
+	const int32_t N = (int32_t) num << 15, d = den;
+	int32_t q = (int32_t) ((float) N * __builtin_amdgcn_rcpf((float) d));
+	const int32_t r = N - q * d;
+	q += (r >= d) ? 1 : 0;
+	q -= (r < 0) ? 1 : 0;
+	return (Word16) q;
+#else
 	return (Word16) ((0x8000 * (Word32) num) / (Word32) den);
+#endif
 }
 
 /* ---- 40-bit accumulator (mathhalf_i.h:1763-2168) ---- */

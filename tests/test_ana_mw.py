@@ -11,11 +11,15 @@ build.  GPU: k_enc_ana_mw at each wave count against the goldens, and the
 live reference on sampled channels.
 """
 import ctypes
+import os
+import sys
 
 import numpy as np
 import pytest
 
 from test_encode import emu, golden, signals, sha, run_superframes, edge_signals
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def emu_mw(nw):
@@ -232,29 +236,38 @@ def test_mw_gpu_live_count_pick_ragged():
     np.testing.assert_array_equal(got, mw)
 
 
-@pytest.mark.gpu
-def test_engine_reserves_scratch_at_create():
-    """An engine's kernels get their private-segment scratch at create
-    (engine.hip engine_reserve), so a caller that then fills the device
-    (here torch's allocator, up to out-of-memory) still encodes and decodes:
-    a shortage shows at melpe_engine_create, never mid-stream."""
-    import torch
-    from pairphone_amd import MelpeEngine
-    dev = torch.device("cuda", 0)
-    C = 65536
-    eng = MelpeEngine(C)
-    hog, size = [], 1 << 30
-    while size >= (1 << 24):
-        try:
-            hog.append(torch.empty(size, dtype=torch.uint8, device=dev))
-        except RuntimeError:
-            size //= 2
+_SCRATCH_CHILD = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+from pairphone_amd import MelpeEngine
+dev = torch.device("cuda", 0)
+C = 65536
+hog, size = [], 1 << 30
+while size >= (1 << 22):
     try:
-        pcm = np.zeros((C, 540), np.int16)
-        bits = eng.encode(pcm)          # host path: staging buffers are the engine's own
-        out = eng.decode(bits)
-        assert bits.shape == (C, 11) and out.shape == (C, 540)
-    finally:
-        del hog
-        torch.cuda.empty_cache()
-        eng.close()
+        hog.append(torch.empty(size, dtype=torch.uint8, device=dev))
+    except RuntimeError:
+        size //= 2
+try:
+    MelpeEngine(C)
+    print("CREATED")
+except RuntimeError as e:
+    print("CREATE FAILED:", e)
+"""
+
+
+@pytest.mark.gpu
+def test_engine_create_fails_cleanly_without_scratch():
+    """The engine's buffers and its kernels' private-segment scratch are
+    had at melpe_engine_create (engine.hip engine_reserve: one dispatch of
+    each kernel with a real launch's grid): on a device torch has filled,
+    create fails with an error message instead of the first encode
+    faulting mid-stream.  Run in a child process, so the filled device and
+    any queue the runtime tears down stay out of this suite."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", _SCRATCH_CHILD, ROOT], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "CREATE FAILED" in r.stdout, r.stdout[-2000:]

@@ -82,6 +82,14 @@ def cases(name, g):
         if name == "divide_s":   # the reference's domain: 0 <= num <= den
             a = np.concatenate([a, np.abs(b) // 3, np.abs(b)])
             b = np.concatenate([b, np.abs(b), np.abs(b)])
+            # every denominator, with the numerators at the edges of the
+            # quotient's correction (0, 1, den - 1, den, halves) and random
+            # ones: the device's reciprocal-and-correct quotient (ops.h)
+            d = np.arange(1, 32768, dtype=np.int64)
+            nums = [np.zeros_like(d), np.minimum(1, d), d - 1, d, d // 2, (d + 1) // 2, d // 3]
+            nums += [(g.random(len(d)) * d).astype(np.int64) for _ in range(32)]
+            a = np.concatenate([a] + nums)
+            b = np.concatenate([b] + [d] * len(nums))
         return a, b, None
     if name in ("negate", "abs_s", "norm_s"):
         return all16(), None, None
