@@ -35,6 +35,9 @@
  * (the engine records an event on each stream it is given), and for nothing
  * else on the device.  To reset channels in stream order (no host sync), use
  * melpe_engine_reset_dev on the stream that carries the encode/decode work.
+ * The engines of one process share one internal stream per device for their
+ * own work (create and the *_host calls), so the runtime holds kernel scratch
+ * on one hardware queue for all of them rather than on one queue per engine.
  * One engine may be called from several host threads: its calls take a
  * per-engine lock while they enqueue (the host side of a call is short; the
  * device work is not serialised by it).  A call that fails after enqueueing

@@ -1927,12 +1927,11 @@ MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *
 			bq[k].o0 = E->cls.bpfdel[2 * k + 3];
 			bq[k].o1 = E->cls.bpfdel[2 * k + 2];
 		}
-		int j = 0;
-		for (; j + 2 <= slen; j += 2) {
-			int16_t v0 = x[j], v1 = x[j + 1];
-			y[j] = biq_step(bq[2], biq_step(bq[1], biq_step(bq[0], v0)));
-			y[j + 1] = biq_step(bq[2], biq_step(bq[1], biq_step(bq[0], v1)));
-		}
+		/* inputs a block ahead (v_batch); slen is even, as the
+		 * reference's pairwise loop assumes */
+		v_batch(x, y, slen, [&](int, int16_t v) {
+			return biq_step(bq[2], biq_step(bq[1], biq_step(bq[0], v)));
+		});
 		for (int k = 0; k < 3; k++) {
 			E->cls.bpfdel[2 * k] = bq[k].i1;
 			E->cls.bpfdel[2 * k + 1] = bq[k].i0;

@@ -1289,26 +1289,14 @@ MD void iir3_s(int16_t *x, const int16_t *den, const int16_t *num, int16_t *din,
 		v_map(x, x, n, filt);
 	}
 #else
-	int i = 0;
-	for (; i + 4 <= n; i += 4) {
+	/* inputs a block ahead (v_batch); the memories after sample snap - 1
+	 * are taken as sample snap is about to be filtered */
+	v_batch(x, x, n, [&](int i, int16_t v) {
 		if (i == snap)
 			for (int s = 0; s < 3; s++)
 				keep[s] = b[s];
-		int16_t v0 = x[i], v1 = x[i + 1], v2 = x[i + 2], v3 = x[i + 3];
-		v0 = biq_step(b[2], biq_step(b[1], biq_step(b[0], v0)));
-		v1 = biq_step(b[2], biq_step(b[1], biq_step(b[0], v1)));
-		v2 = biq_step(b[2], biq_step(b[1], biq_step(b[0], v2)));
-		v3 = biq_step(b[2], biq_step(b[1], biq_step(b[0], v3)));
-		x[i] = v0;
-		x[i + 1] = v1;
-		x[i + 2] = v2;
-		x[i + 3] = v3;
-	}
-	if (i == snap)
-		for (int s = 0; s < 3; s++)
-			keep[s] = b[s];
-	for (; i < n; i++)
-		x[i] = biq_step(b[2], biq_step(b[1], biq_step(b[0], x[i])));
+		return biq_step(b[2], biq_step(b[1], biq_step(b[0], v)));
+	});
 #endif
 	for (int s = 0; s < 3; s++) {
 		const Biq &o = snap > 0 ? keep[s] : b[s];
@@ -1337,37 +1325,12 @@ MD void iir3_s_io(const int16_t *in, int16_t *out, const int16_t *den, const int
 		b[s].o0 = dout[2 * s];
 		b[s].o1 = dout[2 * s + 1];
 	}
-	/* in place or disjoint: inputs are read one group of four ahead of the
-	 * outputs written */
-	int i = 0;
-	if (n >= 4) {
-		int16_t v[4] = {in[0], in[1], in[2], in[3]};
-		#pragma unroll 1
-		for (; i + 8 <= n; i += 4) {
-			int16_t nv[4] = {in[i + 4], in[i + 5], in[i + 6], in[i + 7]};
-			#pragma unroll
-			for (int q = 0; q < 4; q++) {
-				int16_t y = biq_step(b[2], biq_step(b[1], biq_step(b[0], v[q])));
-				out[i + q] = y;
-				f(i + q, y);
-			}
-			#pragma unroll
-			for (int q = 0; q < 4; q++)
-				v[q] = nv[q];
-		}
-		#pragma unroll
-		for (int q = 0; q < 4; q++) {
-			int16_t y = biq_step(b[2], biq_step(b[1], biq_step(b[0], v[q])));
-			out[i + q] = y;
-			f(i + q, y);
-		}
-		i += 4;
-	}
-	for (; i < n; i++) {
-		int16_t y = biq_step(b[2], biq_step(b[1], biq_step(b[0], in[i])));
-		out[i] = y;
+	/* in place or disjoint: inputs a block ahead of the outputs (v_batch) */
+	v_batch(in, out, n, [&](int i, int16_t v) {
+		int16_t y = biq_step(b[2], biq_step(b[1], biq_step(b[0], v)));
 		f(i, y);
-	}
+		return y;
+	});
 	for (int s = 0; s < 3; s++) {
 		din[2 * s] = b[s].i0;
 		din[2 * s + 1] = b[s].i1;
@@ -1427,16 +1390,9 @@ MD void iir3_d(const int16_t *in, int16_t *out, const int16_t *den, const int16_
 		return biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], v)));
 	});
 #else
-	int i = 0;
-	for (; i + 4 <= n; i += 4) {
-		int16_t v0 = in[i], v1 = in[i + 1], v2 = in[i + 2], v3 = in[i + 3];
-		out[i] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], v0)));
-		out[i + 1] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], v1)));
-		out[i + 2] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], v2)));
-		out[i + 3] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], v3)));
-	}
-	for (; i < n; i++)
-		out[i] = biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], in[i])));
+	v_batch(in, out, n, [&](int, int16_t v) {
+		return biqd_step(b[2], biqd_step(b[1], biqd_step(b[0], v)));
+	});
 #endif
 	for (int s = 0; s < 3; s++) {
 		din[2 * s] = b[s].i0;
@@ -1529,16 +1485,7 @@ MD void iir2_d(int16_t *x, const int16_t *den1, const int16_t *num1, int16_t *di
 #if MELPE_VMAP_IIR
 	v_map(x, x, n, [&](int16_t v) -> int16_t { return biqd_step(b, biqd_step(a, v)); });
 #else
-	int i = 0;
-	for (; i + 4 <= n; i += 4) {
-		int16_t v0 = x[i], v1 = x[i + 1], v2 = x[i + 2], v3 = x[i + 3];
-		x[i] = biqd_step(b, biqd_step(a, v0));
-		x[i + 1] = biqd_step(b, biqd_step(a, v1));
-		x[i + 2] = biqd_step(b, biqd_step(a, v2));
-		x[i + 3] = biqd_step(b, biqd_step(a, v3));
-	}
-	for (; i < n; i++)
-		x[i] = biqd_step(b, biqd_step(a, x[i]));
+	v_batch(x, x, n, [&](int, int16_t v) { return biqd_step(b, biqd_step(a, v)); });
 #endif
 	biqd_store(a, din1, dhi1, dlo1);
 	biqd_store(b, din2, dhi2, dlo2);

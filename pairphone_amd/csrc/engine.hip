@@ -619,7 +619,7 @@ static hipError_t bin_release(BinBuf &b, hipStream_t s)
 struct melpe_engine {
 	int device = 0;
 	int channels = 0;
-	hipStream_t stream = nullptr;
+	hipStream_t stream = nullptr;	/* the device's engine stream (g_dev_stream), shared */
 	hipEvent_t ev0 = nullptr, ev1 = nullptr;
 	EncState *d_enc = nullptr;
 	DecState *d_dec = nullptr;
@@ -771,6 +771,15 @@ static int dec_launch(melpe_engine *e, int16_t *d_sp, const uint8_t *d_bits, con
 
 static std::mutex g_dev_mu;
 static bool g_dev_ready[64];
+/* One stream per device for every engine's own work (create's warm-ups and
+ * the host-buffer calls).  The runtime holds kernel scratch per hardware
+ * queue and keeps it between dispatches; engines each on a stream of their
+ * own end up on every hardware queue the process has, each holding the
+ * scratch of the largest codec launch it ran, and together they can exhaust
+ * the device's scratch pool (a later launch then aborts its queue with
+ * HSA_STATUS_ERROR_OUT_OF_RESOURCES).  Sharing one stream keeps that to one
+ * queue plus the callers' own streams. */
+static hipStream_t g_dev_stream[64];
 
 static int ensure_device_tables(int dev)
 {
@@ -789,6 +798,8 @@ static int ensure_device_tables(int dev)
 	for (auto f : up)
 		if (int rc = f(melpe_tables_blob, bytes))
 			return fail("table upload", (hipError_t) rc);
+	if (hipError_t er = hipStreamCreateWithFlags(&g_dev_stream[dev], hipStreamNonBlocking))
+		return fail("engine stream", er);
 	g_dev_ready[dev] = true;
 	return 0;
 }
@@ -836,13 +847,14 @@ static int engine_mark(melpe_engine *e, hipStream_t s)
 }
 
 /* the host waits for every call of this engine already enqueued, on any
- * stream (not for other engines or unrelated work on the device) */
+ * stream (not for other engines or unrelated work on the device).  The
+ * engines' shared stream needs no wait of its own: every call that enqueues
+ * on it synchronises it before returning. */
 static int engine_wait(melpe_engine *e)
 {
 	std::lock_guard<std::recursive_mutex> lk(e->mu);
 	for (auto &m : e->marks)
 		HIPCHK(hipEventSynchronize(m.second));
-	HIPCHK(hipStreamSynchronize(e->stream));
 	return 0;
 }
 #define ENGINE_WAIT(e) do { if (int _r = engine_wait(e)) return _r; } while (0)
@@ -948,7 +960,7 @@ int melpe_engine_create(melpe_engine **out, int device, int channels)
 	hipError_t er = hipSuccess;
 	const char *what = nullptr;
 #define CREATE_STEP(expr) if (er == hipSuccess && (er = (expr)) != hipSuccess) what = #expr
-	CREATE_STEP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+	e->stream = g_dev_stream[device];
 	CREATE_STEP(hipEventCreate(&e->ev0));
 	CREATE_STEP(hipEventCreate(&e->ev1));
 	CREATE_STEP(hipMalloc(&e->d_enc, sizeof(EncState) * (size_t) channels));
@@ -1035,8 +1047,6 @@ int melpe_engine_destroy(melpe_engine *e)
 		hipEventDestroy(e->ev0);
 	if (e->ev1)
 		hipEventDestroy(e->ev1);
-	if (e->stream)
-		hipStreamDestroy(e->stream);
 	delete e;
 	return 0;
 }

@@ -37,14 +37,16 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 	AnaLane L;
 	PIN_FRAME(L);
 	constexpr size_t nb = ENC_ANA_BYTES;
-	static_assert(nb % 4 == 0, "the record copy is in dwords");
-	lane_copy((char *) &L.S + ENC_ANA_OFF, (const char *) &enc[c] + ENC_ANA_OFF, nb);
+	static_assert(nb % 16 == 0 && ENC_ANA_OFF % 16 == 0 && sizeof(EncState) % 16 == 0 &&
+			      offsetof(AnaLane, S) % 16 == 0,
+		      "the record copy is in 16-byte pieces");
+	lane_copy_x4((char *) &L.S + ENC_ANA_OFF, (const char *) &enc[c] + ENC_ANA_OFF, nb);
 	lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
 	if (MODE == 0)
 		analysis(&L.S, L.x);
 	else
 		analysis_a(&L.S, L.x, res + (size_t) c * NF * LPC_FRAME);
-	lane_copy((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, nb);
+	lane_copy_x4((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, nb);
 	if (MODE == 0)
 		for (int k = 0; k < 11; k++)
 			bits[(size_t) c * 11 + k] = L.S.chbuf[k];

@@ -37,11 +37,12 @@ __global__ __launch_bounds__(DEC_BLOCK, MELPE_DEC_WAVES) void k_decode(DecState 
 	}
 	DecLane L;
 	PIN_FRAME(L);
-	lane_copy(&L.S, &dec[c], sizeof(DecState));
+	static_assert(sizeof(DecState) % 16 == 0 && offsetof(DecLane, S) % 16 == 0, "16-byte record copy");
+	lane_copy_x4(&L.S, &dec[c], sizeof(DecState));
 	for (int k = 0; k < 11; k++)
 		L.S.chbuf[k] = bits[(size_t) c * 11 + k];
 	decode_superframe(&L.S, L.out);
-	lane_copy(&dec[c], &L.S, sizeof(DecState));
+	lane_copy_x4(&dec[c], &L.S, sizeof(DecState));
 	lane_copy(sp + (size_t) c * BLOCK, L.out, sizeof(int16_t) * BLOCK);
 }
 

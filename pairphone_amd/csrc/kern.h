@@ -70,6 +70,20 @@ __device__ __forceinline__ void lane_copy(void *dst, const void *src, size_t byt
 		d[i] = s[i];
 }
 
+/* lane_copy for 16-byte aligned ranges (sizes multiples of 16): one
+ * dwordx4 load / store per 16 bytes, eight in flight, so each lane pulls a
+ * whole 128-byte line of its record per batch instead of re-touching it
+ * over four dword batches while the wave's other 63 records stream past */
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4), __may_alias__));
+__device__ __forceinline__ void lane_copy_x4(void *dst, const void *src, size_t bytes)
+{
+	v4u32 *d = (v4u32 *) dst;
+	const v4u32 *s = (const v4u32 *) src;
+#pragma unroll 8
+	for (size_t i = 0; i < bytes / 16; i++)
+		d[i] = s[i];
+}
+
 #define MELPE_CHK(expr) do { hipError_t _e = (expr); if (_e != hipSuccess) return (int) _e; } while (0)
 
 /* per-TU table upload (+ derivation of g_der) and stage-timer readout */

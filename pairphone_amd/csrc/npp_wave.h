@@ -41,29 +41,16 @@ namespace wv {
 #define BIN_LOOP(t, i) \
 	_Pragma("unroll") for (int t = 0, i = lane; t < 3; t++, i += WV) if (i < NPP_NB)
 
-/* bins 0..127 as two full passes of the wave, then bin 128 (NPP_NB - 1)
- * in wave-uniform control flow.  A third pass would issue every vector
- * instruction of the body for lane 0 alone; with the bin index a constant
- * the body's values are uniform, so the compiler keeps them in scalar
- * registers and on the scalar unit, beside the other waves' vector work.
- * Every lane runs bin 128: its stores write one value from all lanes, and a
- * body that adds bin terms into a per-lane partial sum counts bin 128 on
- * lane 0 only (ON_LANE0(t)). */
-#if !defined(MELPE_NPP_LANE128)
-#define BIN_PASSES(t, i, ...) \
-	_Pragma("unroll") for (int t = 0; t < 3; t++) { \
-		const int i = t < 2 ? lane + WV * t : NPP_NB - 1; \
-		__VA_ARGS__ \
-	}
-#define ON_LANE0(t) ((t) < 2 || lane == 0)
-#else	/* A/B diagnostics: bin 128 as a third vector pass on lane 0 */
+/* The per-bin loops over the 129 bins: bin i on lane i % 64, three passes
+ * unrolled (t = 0, 1, 2), the third on lane 0 alone.  Measured against
+ * running bin 128 in wave-uniform control flow (its values on the scalar
+ * unit, every lane taking part): 11.0 vs 11.2 ms per k_enc_npp launch at
+ * 262,144 channels (profiles/r04_c_npp_*.json) -- the third vector pass
+ * costs no more than the scalar code, so the simpler form stays. */
 #define BIN_PASSES(t, i, ...) \
 	_Pragma("unroll") for (int t = 0, i = lane; t < 3; t++, i += WV) if (i < NPP_NB) { \
 		__VA_ARGS__ \
 	}
-#define ON_LANE0(t) true
-#endif
-
 __device__ __forceinline__ void wsync()
 {
 	__syncthreads();
@@ -726,7 +713,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 		w->YY_shift[i] = sub(w->YY_shift[i], 8);
 		/* maxs is taken before the -8 (npp.c:1300-1330) */
 		Word32 st = npp_spec_term(w->YY, w->YY_shift, (Word16) maxs, i);
-		part += ON_LANE0(t) ? st : 0;
+		part += st;
 	})
 	L = wsum(part);
 	if (L == 0)
@@ -744,7 +731,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	part = 0;
 	BIN_PASSES(t, i, {
 		Word32 st = npp_spec_term(s->smoothedspect, s->sm_shift, (Word16) maxs, i);
-		part += ON_LANE0(t) ? st : 0;
+		part += st;
 	})
 	L = wsum(part);
 	Word16 amin;
@@ -753,7 +740,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	BIN_PASSES(t, i, {
 		npp_sm_period_bin(s, w, anum, amin, i);
 		npp_bias1_bin(s, w, i);
-		part += ON_LANE0(t) ? (int) w->var_rel[i] : 0;
+		part += w->var_rel[i];
 	})
 	Word32 vsum = wsum(part);
 	wsync();
@@ -913,7 +900,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	part = 0;
 	BIN_PASSES(t, i, {
 		Word32 st = npp_spec_term(s->lambdaD, s->lambdaD_shift, (Word16) maxs, i);
-		part += ON_LANE0(t) ? st : 0;
+		part += st;
 	})
 	L = wsum(part);
 	if (L == 0)

@@ -119,8 +119,10 @@ struct alignas(4) BandState {
 struct EncState {
 	NppState npp;
 	/* ---- driver group ---- */
-	/* melpe/global.c */
-	int16_t hpspeech[IN_BEG + BLOCK];
+	/* melpe/global.c.  The analysis part of the record starts on a 16-byte
+	 * boundary (and the record is a multiple of 16 bytes), so the lane
+	 * kernels move it with 16-byte loads and stores (kern.h lane_copy_x4) */
+	alignas(16) int16_t hpspeech[IN_BEG + BLOCK];
 	int16_t dcdelin[DC_ORD], dcdelout_hi[DC_ORD], dcdelout_lo[DC_ORD];
 	MelpParam par[NF];
 	QuantParam qpar;
@@ -158,15 +160,17 @@ struct EncState {
 	ClsState cls;
 	PautoState pa;
 	BandState band[NUM_BANDS];	/* band[0] belongs to the driver group */
+	uint32_t fmt_pad_[2];	/* the tag in the record's last 4 bytes (16-byte size) */
 	/* record format tag (reset sets it, no kernel writes it):
 	 * melpe_engine_import rejects records of another layout */
 	uint32_t fmt;
 };
+static_assert(offsetof(EncState, fmt) + 4 == sizeof(EncState), "EncState's tag ends the record");
 
 #define MIX_ORD 32
 #define DISP_ORD 64
 
-struct DecState {
+struct alignas(16) DecState {	/* 16-byte aligned: moved with dwordx4 (k_dec.hip) */
 	MelpParam par[NF];	/* melp_par: error paths read last superframe's */
 	QuantParam qpar;	/* quant_par: ditto (uv_flag, indices) */
 	/* melpe/melp_syn.c */
@@ -196,10 +200,11 @@ struct DecState {
 	int16_t qgd_prev_gain, qgd_prev_err;
 	uint32_t fmt;	/* record format tag, as EncState's */
 };
+static_assert(offsetof(DecState, fmt) + 4 == sizeof(DecState), "DecState's tag ends the record");
 
 /* Layout version of the records (bump on any change to EncState /
  * DecState); the tag also folds in the record size. */
-#define MELPE_REC_LAYOUT 3u
+#define MELPE_REC_LAYOUT 4u
 #define ENC_REC_FMT (0x4d450000u ^ (MELPE_REC_LAYOUT << 24) ^ (uint32_t) sizeof(EncState))
 #define DEC_REC_FMT (0x4d440000u ^ (MELPE_REC_LAYOUT << 24) ^ (uint32_t) sizeof(DecState))
 
