@@ -735,6 +735,28 @@ extern __shared__ int16_t s_idft_cos[];
 /* entry k in [0, 2 len) of a row */
 #define IDFT_AT(c, k, len) ((c)[(k) >= (len) ? (k) - (len) : (k)])
 
+/* (a + b) mod n for a, b in [0, n): the conditional subtraction as an
+ * unsigned min (a + b - n wraps above a + b when a + b < n) */
+MD int mod_add(int a, int b, int n)
+{
+	const unsigned s = (unsigned) (a + b), r = s - (unsigned) n;
+	return (int) (s < r ? s : r);
+}
+
+/* phase mod len in [0, len); decoded phases lie in [0, len] */
+MD int16_t idft_phase_mod(int p, int len)
+{
+	if ((unsigned) p >= (unsigned) len) {
+		p -= len;
+		if ((unsigned) p >= (unsigned) len) {
+			p %= len;
+			if (p < 0)
+				p += len;
+		}
+	}
+	return (int16_t) p;
+}
+
 /* realIDFT :63 -- direct real inverse DFT of one pitch period.  The
  * reference steps the cosine index k by adding phase[j], wrapping into
  * [0, len), then subtracting phase[j] and adding i, so before harmonic j
@@ -754,11 +776,9 @@ MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 	const int16_t *c = cbuf;
 #else
 	const int16_t *c = IDFT_ROW(len);
-	int16_t phm[PITCHMAX / 2 + 1];	/* phase[j] mod len, in [0, len) */
-	for (int j = 1; j < len2; j++) {
-		int p = phase[j] % len;
-		phm[j] = (int16_t) (p < 0 ? p + len : p);
-	}
+	int16_t phm[PITCHMAX / 2 + 1];
+	for (int j = 1; j < len2; j++)
+		phm[j] = idft_phase_mod(phase[j], len);
 #endif
 	w = shr(w, 1);
 	Word16 w2 = shr(w, 1);
@@ -779,34 +799,48 @@ MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 	 * clamp, the chain is an exact integer sum in any order, and each term
 	 * is one 24-bit multiply-add (|2 mag| < 2^17).  Decoded magnitudes are
 	 * scaled by 2/len, so this is the common case; a wave with any lane
-	 * outside it runs the saturating chain below for all of them. */
+	 * outside it runs the saturating chain below for all of them.
+	 *
+	 * Loop order: harmonic j outer, the block's IDFT_BLK outputs inner.
+	 * Output t reads entry (j t + phase[j]) mod len, so along the block
+	 * the index steps by j (< len: one conditional subtraction, done as an
+	 * unsigned min), and the block's first index follows from
+	 * base = (j i) mod len, stepped by i per harmonic.  The block's table
+	 * gathers are issued together before its multiply-adds, and harmonic
+	 * j + 1's (2 mag, phase) word is loaded while j's are in flight. */
 	{
 		int A = 0;
 		for (int j = 0; j < len2; j++)
 			A += mag[j] < 0 ? -mag[j] : mag[j];
 		if (wave_all(A <= 32766)) {
+			/* (2 mag[j]) * 256 + (phase[j] mod len): len <= PITCHMAX < 256 */
+			int pk[PITCHMAX / 2 + 2];
+			for (int j = 1; j < len2; j++)
+				pk[j] = 2 * (int) mag[j] * 256 + phm[j];
+			pk[len2] = 0;
 			const int m0 = (int) mag[0] * 65536 + 32768;
 			for (i = 0; i < len; i += IDFT_BLK) {
-				/* iq = (i + q) mod len (q < IDFT_BLK < PITCHMIN: one
-				 * subtraction), so every index stays in the row even for
-				 * the last block's unused outputs */
-				int Lq[IDFT_BLK], bq[IDFT_BLK], iq[IDFT_BLK];
+				int Lq[IDFT_BLK];
 #pragma unroll
-				for (int q = 0; q < IDFT_BLK; q++) {
+				for (int q = 0; q < IDFT_BLK; q++)
 					Lq[q] = m0;
-					bq[q] = 0;
-					iq[q] = i + q < len ? i + q : i + q - len;
-				}
+				int base = 0;	/* (j * i) mod len */
+				int nxt = pk[1];
 				for (int j = 1; j < len2; j++) {
-					const int m2 = 2 * (int) mag[j];
-					const int p = phm[j];
+					const int cur = nxt;
+					nxt = pk[j + 1];
+					const int m2 = cur >> 8;
+					base = mod_add(base, i, len);
+					int k = mod_add(base, cur & 255, len);
+					int cv[IDFT_BLK];
 #pragma unroll
 					for (int q = 0; q < IDFT_BLK; q++) {
-						bq[q] += iq[q];
-						if (bq[q] >= len)
-							bq[q] -= len;
-						Lq[q] += m2 * (int) IDFT_AT(c, bq[q] + p, len);
+						cv[q] = c[k];
+						k = mod_add(k, j, len);
 					}
+#pragma unroll
+					for (int q = 0; q < IDFT_BLK; q++)
+						Lq[q] += m2 * cv[q];
 				}
 #pragma unroll
 				for (int q = 0; q < IDFT_BLK; q++)
@@ -1280,6 +1314,7 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 	{
 		const int total = D->syn_begin - sb_start;
 		v_copy(D->disp_del, &pre[total], DISP_ORD);
+		static_assert(DISP_ORD == 64, "zerflt_Q's unrolled dispersion path (dsp.h)");
 		zerflt_Q(&pre[DISP_ORD], TB(disp_cof), &pre[DISP_ORD], DISP_ORD, total, 15);
 		v_copy(&out[sb_start], &pre[DISP_ORD], FRAME - sb_start);
 		v_copy(D->sigsave, &pre[DISP_ORD + FRAME - sb_start], total - (FRAME - sb_start));

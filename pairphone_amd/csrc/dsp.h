@@ -1138,12 +1138,61 @@ MD void zerflt_q_long(const int16_t *in, const int16_t *c, int16_t *out, int ord
 	}
 }
 
+/* the decoder's dispersion FIR (ORDER = DISP_ORD): eight outputs per block,
+ * the block's ORDER + 8 inputs loaded together up front (one memory wait per
+ * block instead of one per tap).  With no coefficient at MIN16 -- checked
+ * on entry -- L_mult(x, c) is x * 2c exactly, so each tap of an output's
+ * chain is one 24-bit multiply and one saturating add, in the reference's
+ * tap order. */
+template <int ORDER>
+MD bool zerflt_q_blk8(const int16_t *in, const int16_t *c, int16_t *out, int n, Word16 sc)
+{
+	bool ok = true;
+	for (int j = 0; j <= ORDER; j++)
+		ok &= c[j] != SW_MIN_;
+	if (!ok)
+		return false;
+	int i = n - 1;
+#pragma unroll 1
+	for (; i >= 7; i -= 8) {
+		int16_t w[ORDER + 8];	/* w[k] = in[i - k] */
+#pragma unroll
+		for (int k = 0; k < ORDER + 8; k++)
+			w[k] = in[i - k];
+		Word32 a[8];
+#pragma unroll
+		for (int q = 0; q < 8; q++)
+			a[q] = 0;
+#pragma unroll
+		for (int j = 0; j <= ORDER; j++) {
+			const int32_t c2 = 2 * (int32_t) c[j];
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+				a[q] = sat_add32(a[q], (int32_t) w[j + q] * c2);
+		}
+#pragma unroll
+		for (int q = 0; q < 8; q++)
+			out[i - q] = r_ound(L_shl(a[q], sc));
+	}
+	for (; i >= 0; i--) {
+		Word32 acc = 0;
+		for (int j = 0; j <= ORDER; j++)
+			acc = L_mac(acc, in[i - j], c[j]);
+		out[i] = r_ound(L_shl(acc, sc));
+	}
+	return true;
+}
+
 MN void zerflt_Q(const int16_t *in, const int16_t *c, int16_t *out, int order,
 		 int n, Word16 qc)
 {
 	PROF_SCOPE(28);
 	Word16 sc = sub(15, qc);
 	if (order >= 16) {
+#if !defined(MELPE_OPCOUNT)
+		if (order == 64 && zerflt_q_blk8<64>(in, c, out, n, sc))	/* DISP_ORD */
+			return;
+#endif
 		zerflt_q_long(in, c, out, order, n, sc);
 		return;
 	}
@@ -1948,12 +1997,60 @@ MD void lpc_syn(const int16_t *x, int16_t *y, const int16_t *a, int order, int n
 	PROF_SCOPE(29);
 	if (order == 10) {
 		Word16 c[10], h[10];	/* h[k] = y[j - 1 - k] */
+		bool dbl = true;
 #pragma unroll
 		for (int k = 0; k < 10; k++) {
 			c[k] = a[k];
 			h[k] = y[-1 - k];
+			dbl &= c[k] != SW_MIN_;
 		}
-		for (int j = 0; j < n; j++) {
+		int j = 0;
+#if !defined(MELPE_OPCOUNT)
+		/* With no coefficient at MIN16, L_msu(acc, h, c) is the saturating
+		 * acc - h * 2c; the inputs are loaded a block of eight ahead of
+		 * the outputs stored (x == y, or y below x: each x[j] is read
+		 * before y[j] can overwrite it) */
+		if (n >= 16 && wave_all(dbl) && !(y > x && y < x + n)) {
+			int32_t c2[10];
+#pragma unroll
+			for (int k = 0; k < 10; k++)
+				c2[k] = 2 * (int32_t) c[k];
+			auto step = [&](int16_t xv) {
+				Word32 acc = L_shr(L_deposit_h(xv), 3);
+#pragma unroll
+				for (int i = 10; i > 0; i--)
+					acc = sat_sub32(acc, (int32_t) h[i - 1] * c2[i - 1]);
+				Word16 v = r_ound(L_shl(acc, 3));
+#pragma unroll
+				for (int k = 9; k > 0; k--)
+					h[k] = h[k - 1];
+				h[0] = v;
+				return v;
+			};
+			int16_t v[8];
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+				v[q] = x[q];
+#pragma unroll 1
+			for (; j + 16 <= n; j += 8) {
+				int16_t nv[8];
+#pragma unroll
+				for (int q = 0; q < 8; q++)
+					nv[q] = x[j + 8 + q];
+#pragma unroll
+				for (int q = 0; q < 8; q++)
+					y[j + q] = step(v[q]);
+#pragma unroll
+				for (int q = 0; q < 8; q++)
+					v[q] = nv[q];
+			}
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+				y[j + q] = step(v[q]);
+			j += 8;
+		}
+#endif
+		for (; j < n; j++) {
 			Word32 acc = L_shr(L_deposit_h(x[j]), 3);
 #pragma unroll
 			for (int i = 10; i > 0; i--)
