@@ -2053,6 +2053,27 @@ MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *
  * FFT into hb (512 packed complex bins, re | im << 16) */
 MN void find_harm_fft(const int16_t *in, uint32_t *hb, int len)
 {
+#if defined(MELPE_OPCOUNT)
+	/* census build: the reference's sequence (fs_lib.c:78-95), the
+	 * unpacked rfft with its per-stage block_max guards, same values */
+	{
+		Word16 m = 0;
+		for (int i = 0; i < len; i++) {
+			Word16 a = abs_s(in[i]);
+			if (a > m)
+				m = a;
+		}
+		Word16 sh = norm_s(m);
+		int16_t buf[2 * 512];
+		v_zero(buf, 2 * 512);
+		for (int i = 0; i < len; i++)
+			buf[i] = shl(in[i], sh);
+		rfft(buf, 512);
+		for (int k = 0; k < 512; k++)
+			hb[k] = pk(buf[2 * k], buf[2 * k + 1]);
+		return;
+	}
+#endif
 	Word16 mx = 0;
 	for (int i = 0; i < len; i++) {
 		Word16 t = abs_s(in[i]);

@@ -70,24 +70,58 @@ MN void noise_sup(int16_t *gain, Word16 ng, Word16 max_noise, Word16 max_att, Wo
 
 /* scale_adj :768 -- match the period's energy to the target gain with a
  * SCALEOVER-sample cross-fade from the previous scale */
+/* L_mac chain of shr(a[i], sh) squared, i = 0 .. n-1: L_v_magsq of the
+ * shifted copy the reference builds (v_equ_shr then L_v_magsq, its final
+ * shift left to the caller), read straight from a[] in pairs */
+MD Word32 magsq_shr(const int16_t *a, int n, Word16 sh)
+{
+	Word32 acc = 0;
+	P16 ra;
+	int np = p16_open(ra, a, n);
+	int i = 0;
+#pragma unroll 8
+	for (int k = 0; k < np; k++, i += 2) {
+		uint32_t x = p16_next(ra);
+		const Word16 t0 = shr(lo16(x), sh), t1 = shr(hi16(x), sh);
+		acc = L_mac(acc, t0, t0);
+		acc = L_mac(acc, t1, t1);
+	}
+	for (; i < n; i++) {
+		const Word16 t = shr(a[i], sh);
+		acc = L_mac(acc, t, t);
+	}
+	return acc;
+}
+
 MN void scale_adj(DecState *D, int16_t *sp, Word16 gain, int len, Word16 over, Word16 inv_over)
 {
 	PROF_SCOPE(21);
-	int16_t tb[PITCHMAX + 8];
 	Word16 sh = 4, t;
+#if defined(MELPE_OPCOUNT)
+	/* census build: the reference's passes */
+	int16_t tb[PITCHMAX + 8];
 	v_equ_shr(tb, sp, sh, len);
 	Word32 msq = L_v_magsq(tb, len, 0, 1);
+#else
+	/* L_v_magsq(tb, len, 0, 1) of tb = sp >> 4: its final shift is 0 */
+	Word32 msq = magsq_shr(sp, len, sh);
+#endif
 	if (msq) {
 		t = sub(norm_l(msq), 1);
 		sh = sub(sh, shr(t, 1));
 	} else {
 		sh = 0;
 	}
+#if defined(MELPE_OPCOUNT)
 	v_equ_shr(tb, sp, sh, len);
+	msq = L_v_magsq(tb, len, 0, 0);
+#else
+	/* L_v_magsq(tb, len, 0, 0) of tb = sp >> sh: its final shift is -1 */
+	msq = L_shl(magsq_shr(sp, len, sh), -1);
+#endif
 	sh = shl(sh, 1);
 	t = shl(256, sh);
 	sh = log10_fxp(t, 8);
-	msq = L_v_magsq(tb, len, 0, 0);
 	msq = L_add(msq, 1);
 	Word16 lmsq = L_log10_fxp(msq, 0);
 	msq = L_add(L_shl(L_deposit_l(lmsq), 1), L_deposit_l(sh));
@@ -107,7 +141,13 @@ MN void scale_adj(DecState *D, int16_t *sp, Word16 gain, int len, Word16 over, W
 		Word32 s = extract_h(L_add(i1, i2));
 		sp[i - 1] = extract_h(L_shl(L_mult(sp[i - 1], (Word16) s), 2));
 	}
+#if defined(MELPE_OPCOUNT)
 	v_scale_shl(&sp[over - 1], scale, (int16_t) (len - over + 1), 2);
+#else
+	v_batch(&sp[over - 1], &sp[over - 1], len - over + 1, [scale](int, int16_t x) {
+		return (int16_t) extract_h(L_shl(L_mult(x, scale), 2));	/* v_scale_shl :462 */
+	});
+#endif
 	D->prev_scale = scale;
 }
 
@@ -777,20 +817,47 @@ MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 #else
 	const int16_t *c = IDFT_ROW(len);
 	int16_t phm[PITCHMAX / 2 + 1];
-	for (int j = 1; j < len2; j++)
-		phm[j] = idft_phase_mod(phase[j], len);
 #endif
 	w = shr(w, 1);
 	Word16 w2 = shr(w, 1);
-	mag[0] = mult(mag[0], w2);
 	Word16 t = sub(len2, 1);
 	int i;
+#if defined(MELPE_OPCOUNT)
+	mag[0] = mult(mag[0], w2);
 	for (i = 1; i < t; i++)
 		mag[i] = mult(mag[i], w);
 	if (shl((Word16) i, 1) == len)
 		mag[i] = mult(mag[i], w2);
 	else
 		mag[i] = mult(mag[i], w);
+#else
+	/* one pass over the harmonics: the magnitude scaling (w2 on the first
+	 * and, for an even len, the last), the fast path's bound A = sum |mag|,
+	 * phase[j] mod len, and the fast path's packed (2 mag, phase) word; the
+	 * next harmonic's inputs are loaded before this one's stores */
+	int A = 0;
+	int pk[PITCHMAX / 2 + 2];	/* (2 mag[j]) * 256 + (phase[j] mod len): len <= PITCHMAX < 256 */
+	{
+		const bool even = shl(t, 1) == len;
+		int16_t mn = mag[0], pn = 0;
+		for (int j = 0; j < len2; j++) {
+			const int16_t mj = mn, pj = pn;
+			if (j + 1 < len2) {
+				mn = mag[j + 1];
+				pn = phase[j + 1];
+			}
+			const Word16 m = mult(mj, (j == 0 || (j == t && even)) ? w2 : w);
+			mag[j] = m;
+			A += m < 0 ? -m : m;
+			if (j) {
+				const int16_t p = idft_phase_mod(pj, len);
+				phm[j] = p;
+				pk[j] = 2 * (int) m * 256 + p;
+			}
+		}
+		pk[len2] = 0;
+	}
+#endif
 #if !defined(MELPE_OPCOUNT)
 	/* No-clamp fast path.  Every partial sum of an output's chain is
 	 * mag[0] * 2^16 plus terms 2 mag[j] c[k] with |c| <= 2^15, so with
@@ -809,15 +876,7 @@ MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 	 * gathers are issued together before its multiply-adds, and harmonic
 	 * j + 1's (2 mag, phase) word is loaded while j's are in flight. */
 	{
-		int A = 0;
-		for (int j = 0; j < len2; j++)
-			A += mag[j] < 0 ? -mag[j] : mag[j];
 		if (wave_all(A <= 32766)) {
-			/* (2 mag[j]) * 256 + (phase[j] mod len): len <= PITCHMAX < 256 */
-			int pk[PITCHMAX / 2 + 2];
-			for (int j = 1; j < len2; j++)
-				pk[j] = 2 * (int) mag[j] * 256 + phm[j];
-			pk[len2] = 0;
 			const int m0 = (int) mag[0] * 65536 + 32768;
 			for (i = 0; i < len; i += IDFT_BLK) {
 				int Lq[IDFT_BLK];
@@ -944,9 +1003,17 @@ MN void harm_syn_pitch(DecState *D, const int16_t *amp, int16_t *sig, Word16 fc,
 	PROF_SCOPE(19);
 	int16_t rnd[129], mag[129], phase[129];
 	Word16 fc1, fc2, factor;
+#if defined(MELPE_OPCOUNT)
 	v_zero(phase, 129);
-	for (int i = 0; i < len / 2 + 1; i++)
-		rnd[i] = mult(len, rand_minstdgen(&D->seed));
+#endif
+	/* (no zeroing of phase[] outside the census build: the loops below
+	 * write phase[0 .. max(mc, len/2)], every entry realIDFT reads) */
+	{
+		uint32_t seed = D->seed;
+		for (int i = 0; i < len / 2 + 1; i++)
+			rnd[i] = mult(len, rand_minstdgen(&seed));
+		D->seed = seed;
+	}
 	if (fc <= 4000) {
 		fc1 = mult(13926, fc);
 		fc2 = mult(17203, fc);
@@ -1029,6 +1096,50 @@ MD Word16 pf_energy(const int16_t *sp, Word16 *sh_out)
 	return extract_h(L_shl(sum, ts));
 }
 
+/* The postfilter's pole-zero taps L_add(L, L_mult(m, a)) / L_sub(L,
+ * L_mult(m, a)).  With no coefficient at MIN16 (mult() never returns it, so
+ * only an imported record could hold one; checked per call over the wave)
+ * L_mult(m, a) is m * 2a exactly and is never MIN32, so each tap is one
+ * 24-bit multiply and one clamped add or subtract.  pz_run instantiates the
+ * filter loop for both forms and runs the one the check allows. */
+template <bool DBL>
+struct PzTaps {
+	int32_t f2[LPC_ORD], i2[LPC_ORD];
+	const int16_t *f, *i;
+	MM PzTaps(const int16_t *af, const int16_t *ai) : f(af), i(ai)
+	{
+#pragma unroll
+		for (int k = 0; k < LPC_ORD; k++) {
+			f2[k] = 2 * (int32_t) af[k];
+			i2[k] = 2 * (int32_t) ai[k];
+		}
+	}
+	MM Word32 fir(Word32 L, Word16 m, int k) const
+	{
+		return DBL ? sat_add32(L, (int32_t) m * f2[k]) : L_add(L, L_mult(m, f[k]));
+	}
+	MM Word32 iir(Word32 L, Word16 m, int k) const
+	{
+		return DBL ? sat_sub32(L, (int32_t) m * i2[k]) : L_sub(L, L_mult(m, i[k]));
+	}
+};
+
+template <class F>
+MD void pz_run(const int16_t *af, const int16_t *ai, F loop)
+{
+	bool ok = true;
+#pragma unroll
+	for (int k = 0; k < LPC_ORD; k++)
+		ok &= af[k] != SW_MIN_ && ai[k] != SW_MIN_;
+#if defined(MELPE_OPCOUNT)
+	ok = false;
+#endif
+	if (wave_all(ok))
+		loop(PzTaps<true>(af, ai));
+	else
+		loop(PzTaps<false>(af, ai));
+}
+
 /* postfilt :60 */
 MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_t *cur_lsf)
 {
@@ -1050,10 +1161,14 @@ MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_
 		if (t < 0)
 			t = 0;
 		Word16 emph = shl(t, 3);
-		for (int j = 0; j < 45; j++) {
-			t = mult(emph, D->pf_hpm);
-			D->pf_hpm = sp[i * 45 + j];
-			synhp[j] = sub(D->pf_hpm, t);
+		{
+			Word16 hpm = D->pf_hpm;
+			v_batch(&sp[i * 45], synhp, 45, [&](int, int16_t x) {
+				const Word16 u = mult(emph, hpm);
+				hpm = x;
+				return (int16_t) sub(x, u);
+			});
+			D->pf_hpm = hpm;
 		}
 		if (i == 0) {
 			/* run the previous frame's filter over the first 20 samples for
@@ -1066,28 +1181,33 @@ MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_
 				af[k] = D->pf_aFIR[k];
 				ai[k] = D->pf_aIIR[k];
 			}
+			pz_run(af, ai, [&](const auto &pc) {
+			Word16 xn = synhp[0];	/* the next sample, loaded one ahead */
 			for (int j = 0; j < 20; j++) {
+				const Word16 x = xn;
+				xn = synhp[j + 1 < 45 ? j + 1 : 44];
 				L = 0;
 #pragma unroll
 				for (int k = 0; k < LPC_ORD; k++)
-					L = L_add(L, L_mult(m1o[k], af[k]));
+					L = pc.fir(L, m1o[k], k);
 #pragma unroll
 				for (int k = LPC_ORD - 1; k > 0; k--)
 					m1o[k] = m1o[k - 1];
-				m1o[0] = synhp[j];
-				L = L_add(L, L_shl(L_deposit_l(synhp[j]), 13));
+				m1o[0] = x;
+				L = L_add(L, L_shl(L_deposit_l(x), 13));
 #pragma unroll
 				for (int k = 0; k < LPC_ORD; k++)
-					L = L_sub(L, L_mult(m2o[k], ai[k]));
+					L = pc.iir(L, m2o[k], k);
 #pragma unroll
 				for (int k = LPC_ORD - 1; k > 0; k--)
 					m2o[k] = m2o[k - 1];
 				t1 = extract_l(L_shr(L, 13));
 				m2o[0] = t1;
-				t = sub(SW_MAX_, (Word16) (j * 1638));	/* window[j] */
-				t1 = mult(t, t1);
+				Word16 wt = sub(SW_MAX_, (Word16) (j * 1638));	/* window[j] */
+				t1 = mult(wt, t1);
 				nokori[j] = extract_l(L_shr(L_mult(D->pf_gain, t1), 15));
 			}
+			});
 		}
 		t1 = 18678;	/* ALPH */
 		t2 = 24576;	/* BETA */
@@ -1107,19 +1227,23 @@ MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_
 				af[k] = D->pf_aFIR[k];
 				ai[k] = D->pf_aIIR[k];
 			}
+			pz_run(af, ai, [&](const auto &pc) {
+			Word16 xn = synhp[0];	/* the next sample, loaded one ahead */
 			for (int j = 0; j < 45; j++) {
+				const Word16 x = xn;
+				xn = synhp[j + 1 < 45 ? j + 1 : 44];
 				L = 0;
 #pragma unroll
 				for (int k = 0; k < LPC_ORD; k++)
-					L = L_add(L, L_mult(m1[k], af[k]));
+					L = pc.fir(L, m1[k], k);
 #pragma unroll
 				for (int k = LPC_ORD - 1; k > 0; k--)
 					m1[k] = m1[k - 1];
-				m1[0] = synhp[j];
-				L = L_add(L, L_shl(L_deposit_l(synhp[j]), 13));
+				m1[0] = x;
+				L = L_add(L, L_shl(L_deposit_l(x), 13));
 #pragma unroll
 				for (int k = 0; k < LPC_ORD; k++)
-					L = L_sub(L, L_mult(m2[k], ai[k]));
+					L = pc.iir(L, m2[k], k);
 #pragma unroll
 				for (int k = LPC_ORD - 1; k > 0; k--)
 					m2[k] = m2[k - 1];
@@ -1127,6 +1251,7 @@ MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_
 				m2[0] = extract_l(L);
 				sp[i * 45 + j] = extract_l(L);
 			}
+			});
 #pragma unroll
 			for (int k = 0; k < LPC_ORD; k++) {
 				D->pf_mem1[k] = m1[k];
@@ -1151,11 +1276,18 @@ MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_
 	} else {
 		D->pf_gain = 0;
 	}
-	for (int i = 0; i < FRAME; i++)
-		sp[i] = extract_l(L_shr(L_mult(D->pf_gain, sp[i]), 15));
-	for (int i = 0; i < 20; i++)
-		sp[i] = add(mult(sp[i], (Word16) (i * 1638)), nokori[i]);
-	v_scale(sp, 29088, FRAME);
+	/* the gain, the first 20 samples' cross-fade with the previous
+	 * filter's tail and v_scale(sp, 29088) in one pass, each sample's ops in
+	 * the reference's order */
+	{
+		const Word16 g = D->pf_gain;
+		v_batch(sp, sp, FRAME, [&](int i, int16_t x) {
+			Word16 y = extract_l(L_shr(L_mult(g, x), 15));
+			if (i < 20)
+				y = add(mult(y, (Word16) (i * 1638)), nokori[i]);
+			return (int16_t) mult(y, 29088);
+		});
+	}
 	iir2_d(sp, TB(lpf3500_den), TB(lpf3500_num), D->lpf_din, D->lpf_dhi, D->lpf_dlo,
 	       TB(hpf60_den), TB(hpf60_num), D->hpf_din, D->hpf_dhi, D->hpf_dlo, FRAME);
 }

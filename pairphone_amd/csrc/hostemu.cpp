@@ -14,7 +14,9 @@
 #include <vector>
 
 #include "codec.h"
+#if !defined(MELPE_OPCOUNT)	/* the census counts the reference's serial order */
 #include "ana_mw.h"
+#endif
 #include "helpers_eval.h"
 #include "codec2400.h"
 #include "voice_crypt.h"
@@ -143,6 +145,7 @@ int emu_encode_ana(emu_engine *e, unsigned char *bits, const int16_t *sp)
 	return 0;
 }
 
+#if !defined(MELPE_OPCOUNT)
 /* the multi-wave analysis (ana_mw.h) as k_enc_ana_mw runs it: nw physical
  * waves, each with its own private copy of the record, phase by phase (the
  * barriers), the exchange block and the HBM record the only shared data;
@@ -194,6 +197,7 @@ int emu_encode_ana_mw(emu_engine *e, unsigned char *bits, const int16_t *sp, int
 	}
 	return 0;
 }
+#endif
 
 /* host build of the helper self-test (helpers_eval.h), same layout as
  * melpe_helpers_eval_dev */

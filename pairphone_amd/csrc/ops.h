@@ -24,6 +24,7 @@
 #if defined(__HIP__)
 #include <hip/hip_runtime.h>
 #define MD __device__ __attribute__((always_inline)) inline
+#define MM __device__ __attribute__((always_inline)) inline	/* member functions */
 #define MF __device__
 /* big routines stay out of line: bounded compile time and register use */
 #if defined(MELPE_INLINE_ALL)
@@ -39,6 +40,7 @@
 #define MDEV_TAB static __constant__
 #else
 #define MD static inline
+#define MM inline
 #define MF static
 #define MN static
 #define MDEV_CONST static

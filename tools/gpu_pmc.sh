@@ -1,8 +1,8 @@
 # kernel trace + PMC passes of the encode/decode step at one channel count
 # (one counter group per pass, each its own run and time limit), summarised
-# into profiles/r03_<tag>_* and merged into profiles/pmc_latest.json (one
+# into profiles/r04_<tag>_* and merged into profiles/pmc_latest.json (one
 # set per channel count), copied back under gpurun_out/<tag>/profiles
-#   bash tools/gpu_r03_pmc.sh <tag> <channels>
+#   bash tools/gpu_pmc.sh <tag> <channels>
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/$1/profiles && export TMPDIR=/tmp &&
 C=$2 &&
 B="bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-side-legs --total-channels 0 --tx-channels 0 --channels $C" &&
@@ -12,5 +12,6 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/$1/pmc_write -o w -
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_FLAT GRBM_GUI_ACTIVE -d gpurun_out/$1/pmc_a -o a -- python3 $B > gpurun_out/$1/pmc_a.log 2>&1 &&
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY -d gpurun_out/$1/pmc_b -o b -- python3 $B > gpurun_out/$1/pmc_b.log 2>&1 &&
 timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/$1/pmc_c -o c -- python3 $B > gpurun_out/$1/pmc_c.log 2>&1 &&
-python3 tools/prof_summary.py gpurun_out/$1 r03_$1 $C > gpurun_out/$1/summary.log 2>&1 &&
-cp profiles/r03_$1_* profiles/pmc_latest.json gpurun_out/$1/profiles/
+python3 tools/prof_summary.py gpurun_out/$1 r04_$1 $C > gpurun_out/$1/summary.log 2>&1 &&
+cp profiles/r04_$1_* profiles/pmc_latest.json gpurun_out/$1/profiles/ &&
+rm -rf gpurun_out/$1/pmc_fetch gpurun_out/$1/pmc_write gpurun_out/$1/pmc_a gpurun_out/$1/pmc_b gpurun_out/$1/pmc_c
