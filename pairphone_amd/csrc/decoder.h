@@ -805,6 +805,7 @@ MD int16_t idft_phase_mod(int p, int len)
  * cosines come from the per-len table built at init. */
 MN void realIDFT(int16_t *mag, const int16_t *phase, int16_t *sig, Word16 len)
 {
+	PROF_SCOPE(49);
 	Word16 len2 = add(shr(len, 1), 1);
 	Word16 w = divide_s(16, len);	/* TWO_Q3 */
 #if defined(MELPE_OPCOUNT)
@@ -1078,18 +1079,63 @@ MN void harm_syn_pitch(DecState *D, const int16_t *amp, int16_t *sig, Word16 fc,
 /* block energy in (mantissa, shift) form (postfilt.c:95-110 / 220-235) */
 MD Word16 pf_energy(const int16_t *sp, Word16 *sh_out)
 {
+	PROF_SCOPE(52);
 	Word16 mx = 0;
+	Word32 sum = 0;
+	Word16 ts;
+#if defined(MELPE_OPCOUNT)
 	for (int i = 0; i < FRAME; i++) {
 		Word16 t = abs_s(sp[i]);
 		if (mx < t)
 			mx = t;
 	}
-	Word16 ts = norm_s(mx);
-	Word32 sum = 0;
+	ts = norm_s(mx);
 	for (int i = 0; i < FRAME; i++) {
 		Word16 t = shl(sp[i], ts);
 		sum = L_add(sum, L_shr(L_mult(t, t), 8));
 	}
+#else
+	/* Both passes on packed pairs, branch-free.  ts = norm_s(max |x|), so
+	 * shl(x, ts) never saturates and is x << ts; each term is at most
+	 * (2^31 - 1) >> 8, and FRAME of them stay below 2^31, so L_add never
+	 * clamps and the sum may be formed in any order. */
+	static_assert(FRAME % 2 == 0, "pairs");
+	{
+		P16 r;
+		const int np = p16_open(r, sp, FRAME);
+		int i = 0;
+#pragma unroll 8
+		for (int k = 0; k < np; k++, i += 2) {
+			const uint32_t x = p16_next(r);
+			const Word16 a = abs_s(lo16(x)), b = abs_s(hi16(x));
+			mx = a > mx ? a : mx;
+			mx = b > mx ? b : mx;
+		}
+		for (; i < FRAME; i++) {
+			const Word16 a = abs_s(sp[i]);
+			mx = a > mx ? a : mx;
+		}
+	}
+	ts = norm_s(mx);
+	{
+		P16 r;
+		const int np = p16_open(r, sp, FRAME);
+		int i = 0;
+		int32_t acc = 0;
+#pragma unroll 8
+		for (int k = 0; k < np; k++, i += 2) {
+			const uint32_t x = p16_next(r);
+			const Word16 a = (Word16) (lo16(x) * (1 << ts)), b = (Word16) (hi16(x) * (1 << ts));
+			acc += (int32_t) ((uint32_t) L_mult(a, a) >> 8);
+			acc += (int32_t) ((uint32_t) L_mult(b, b) >> 8);
+		}
+		for (; i < FRAME; i++) {
+			const Word16 a = (Word16) (sp[i] * (1 << ts));
+			acc += (int32_t) ((uint32_t) L_mult(a, a) >> 8);
+		}
+		sum = acc;
+	}
+#endif
 	Word16 sh = sub(8, shl(ts, 1));
 	ts = norm_l(sum);
 	*sh_out = sub(sh, ts);
@@ -1357,8 +1403,11 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 	v_copy(pre, D->disp_del, DISP_ORD);
 	while (D->syn_begin < FRAME) {
 		Word16 sb0 = D->syn_begin;
+		Word16 len, gain, fc, pulse_gain;
+		{
+		PROF_SCOPE(50);
 		Word16 ifact = divide_s(sb0, FRAME);
-		Word16 gcnt, ifg, gain, intfact;
+		Word16 gcnt, ifg, intfact;
 		if (sb0 >= 90) {
 			gcnt = 2;
 			ifg = divide_s(sub(sb0, 90), 90);
@@ -1396,21 +1445,21 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 		t1 = add(mult(lpc_gain, intfact), mult(D->prev_lpc_gain, if1));
 		Word16 syn_gain = mult(32000, t1);
 		Word16 pitch = add(mult(par->pitch, intfact), mult(prev->pitch, if1));
-		Word16 pulse_gain = extract_h(L_shl(L_mult(syn_gain, sqrt_fxp(pitch, 7)), 4));
+		pulse_gain = extract_h(L_shl(L_mult(syn_gain, sqrt_fxp(pitch, 7)), 4));
 		t1 = sqrt_fxp(ifact, 15);
 		interp_array(D->prev_pcof, cur_p, pul, t1, MIX_ORD + 1);
 		interp_array(D->prev_ncof, cur_n, noi, t1, MIX_ORD + 1);
 		Word16 fc_prev = set_fc(prev->bpvc);
 		Word16 fc_cur = set_fc(par->bpvc);
 		t2 = sub(SW_MAX_, t1);
-		Word16 fc = add(mult(t1, fc_cur), mult(t2, fc_prev));
+		fc = add(mult(t1, fc_cur), mult(t2, fc_prev));
 		Word16 jitter = add(mult(par->jitter, ifact), mult(prev->jitter, sub(SW_MAX_, ifact)));
 		gain = mult(26214, gain);	/* X005_Q19 */
 		int16_t r;
 		rand_num(&r, SW_MAX_, 1, &D->seed);
 		t1 = shr(mult(jitter, r), 1);
 		t1 = mult(pitch, sub(16384, t1));
-		Word16 len = shift_r(t1, -6);
+		len = shift_r(t1, -6);
 		if (len < PITCHMIN)
 			len = PITCHMIN;
 		if (len > PITCHMAX)
@@ -1418,6 +1467,7 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 		v_set(fs_real, 8192, len);
 		fs_real[0] = 0;
 		interp_array(prev->fs_mag, par->fs_mag, &fs_real[1], intfact, NUM_HARM);
+		}
 		harm_syn_pitch(D, fs_real, &sb[BEGIN], fc, len);
 		v_scale(&sb[BEGIN], pulse_gain, len);
 		v_copy(&sb[BEGIN - LPC_ORD], D->ase_del, LPC_ORD);
@@ -1444,6 +1494,7 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 	 * chain is the reference's.  The run's part past FRAME is the next
 	 * frame's start (sigsave). */
 	{
+		PROF_SCOPE(51);
 		const int total = D->syn_begin - sb_start;
 		v_copy(D->disp_del, &pre[total], DISP_ORD);
 		static_assert(DISP_ORD == 64, "zerflt_Q's unrolled dispersion path (dsp.h)");

@@ -261,7 +261,25 @@ MD Word32 L_negate(Word32 a) { OPC(15); return a == LW_MIN_ ? LW_MAX_ : -a; }
 MD Word16 abs_s(Word16 a) { OPC(16); return a == SW_MIN_ ? (Word16) SW_MAX_ : (Word16) (a < 0 ? -a : a); }
 MD Word32 L_abs(Word32 a) { OPC(17); return a == LW_MIN_ ? LW_MAX_ : (a < 0 ? -a : a); }
 
-/* shl/shr: mathhalf_i.h:781-935 */
+/* shl/shr: mathhalf_i.h:781-935, branch-free.  For any 16-bit a and n:
+ * a right shift by min(-n, 15) when n < 0 (15 and beyond give the sign),
+ * else a * 2^min(n, 16) clamped to 16 bits (a nonzero a shifted by 15 or
+ * more saturates to its sign, as the reference's n >= 15 case, except -1 << 15
+ * = MIN16, which the reference returns too).  shr(a, n) = shl(a, -n) over
+ * the whole range, n <= -15 included.  Without branches the compiler keeps
+ * the loads of an element loop in flight across elements. */
+MD Word16 shl_core(Word16 a, int n)
+{
+	const int sn = n < 0 ? (-n < 15 ? -n : 15) : 0;
+	const int sp = n > 0 ? (n < 16 ? n : 16) : 0;
+	int v = ((int) a * (1 << sp)) >> sn;
+	v = v > SW_MAX_ ? SW_MAX_ : (v < SW_MIN_ ? SW_MIN_ : v);
+	return (Word16) v;
+}
+
+#if defined(MELPE_SHIFT_BRANCHY)
+/* the branching form (k_ana_mw.hip: the multi-wave kernel's code is 1 MB,
+ * and the branch-free shifts' larger code made it 3x slower there) */
 MD Word16 shr(Word16 a, Word16 n);
 MD Word16 shl(Word16 a, Word16 n)
 {
@@ -297,8 +315,22 @@ MD Word16 shr(Word16 a, Word16 n)
 		return (Word16) (a < 0 ? -1 : 0);
 	return (Word16) (a >> n);
 }
+#else
+MD Word16 shl(Word16 a, Word16 n)
+{
+	OPC(18);
+	return shl_core(a, n);
+}
+
+MD Word16 shr(Word16 a, Word16 n)
+{
+	OPC(19);
+	return shl_core(a, -(int) n);
+}
+#endif
 
 /* L_shl/L_shr: mathhalf_i.h:942-1047 */
+#if defined(MELPE_SHIFT_BRANCHY)
 MD Word32 L_shl(Word32 a, Word16 n);
 MD Word32 L_shr(Word32 a, Word16 n)
 {
@@ -336,6 +368,31 @@ MD Word32 L_shl(Word32 a, Word16 n)
 		return (Word32) v;
 	}
 }
+#else
+/* branch-free, as shl: a right shift by min(-n, 31) for n < 0, else
+ * a * 2^min(n, 32) in 64 bits clamped to 32; L_shr(a, n) = L_shl(a, -n)
+ * over the whole range */
+MD Word32 L_shl_core(Word32 a, int n)
+{
+	const int sn = n < 0 ? (-n < 31 ? -n : 31) : 0;
+	const int sp = n > 0 ? (n < 32 ? n : 32) : 0;
+	int64_t v = ((int64_t) a * ((int64_t) 1 << sp)) >> sn;
+	v = v > LW_MAX_ ? LW_MAX_ : (v < LW_MIN_ ? LW_MIN_ : v);
+	return (Word32) v;
+}
+
+MD Word32 L_shl(Word32 a, Word16 n)
+{
+	OPC(21);
+	return L_shl_core(a, n);
+}
+
+MD Word32 L_shr(Word32 a, Word16 n)
+{
+	OPC(20);
+	return L_shl_core(a, -(int) n);
+}
+#endif
 
 /* shift_r / L_shift_r: mathhalf_i.h:1108-1230 */
 MD Word16 shift_r(Word16 a, Word16 n)
