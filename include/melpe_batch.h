@@ -27,17 +27,20 @@
  * All functions return 0 on success and a negative code on error;
  * melpe_last_error() describes the last error of the calling thread.
  *
- * Ordering: the *_dev calls are ordered by their stream only; two *_dev
- * calls of one engine on different streams may run concurrently when their
- * active masks are disjoint (the engine orders its own shared scratch).  The
+ * Ordering: a *_dev call is ordered after the work already enqueued on its
+ * stream, and later work on that stream after it.  Its kernels run on the
+ * device's engine stream (two event hops), so the *_dev calls of all engines
+ * on a device execute in the order they were made, whatever streams they
+ * name.  The
  * *_host calls, melpe_engine_reset and the state export/import first wait
  * for every *_dev call of the same engine already enqueued, on any stream
  * (the engine records an event on each stream it is given), and for nothing
  * else on the device.  To reset channels in stream order (no host sync), use
  * melpe_engine_reset_dev on the stream that carries the encode/decode work.
- * The engines of one process share one internal stream per device for their
- * own work (create and the *_host calls), so the runtime holds kernel scratch
- * on one hardware queue for all of them rather than on one queue per engine.
+ * The engines of one process share that internal stream per device for all
+ * their kernels (create's scratch reservation, the *_host and the *_dev
+ * calls), so the runtime holds the codec kernels' scratch on one hardware
+ * queue rather than on every queue a caller's stream maps to.
  * One engine may be called from several host threads: its calls take a
  * per-engine lock while they enqueue (the host side of a call is short; the
  * device work is not serialised by it).  A call that fails after enqueueing

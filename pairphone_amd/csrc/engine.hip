@@ -621,6 +621,7 @@ struct melpe_engine {
 	int channels = 0;
 	hipStream_t stream = nullptr;	/* the device's engine stream (g_dev_stream), shared */
 	hipEvent_t ev0 = nullptr, ev1 = nullptr;
+	hipEvent_t ev_in = nullptr, ev_out = nullptr;	/* EngineCall's hops to and from the engine stream */
 	EncState *d_enc = nullptr;
 	DecState *d_dec = nullptr;
 	synth_state *d_syn = nullptr;
@@ -863,12 +864,30 @@ static int engine_wait(melpe_engine *e)
  * every thread) and records the stream's mark when it ends */
 struct EngineCall {
 	melpe_engine *e;
-	hipStream_t s;
+	hipStream_t user, run;
 	std::lock_guard<std::recursive_mutex> lk;
-	EngineCall(melpe_engine *e_, hipStream_t s_) : e(e_), s(s_), lk(e_->mu) {}
-	~EngineCall() { engine_mark(e, s); }
+	EngineCall(melpe_engine *e_, hipStream_t s_) : e(e_), user(s_), run(s_), lk(e_->mu)
+	{
+		/* the call's kernels run on the device's engine stream, ordered
+		 * after the caller's stream and before its later work (two event
+		 * hops).  The runtime holds kernel scratch per hardware queue; the
+		 * codec kernels' is reserved on the engine stream's queue at create
+		 * (engine_reserve), and a second queue running them would hold its
+		 * own -- at 14 GB per queue for the analysis kernels two queues
+		 * exceed the runtime's threshold and it reclaims one queue's
+		 * scratch to grant the other's, hundreds of ms per launch. */
+		if (s_ != e->stream && hipEventRecord(e->ev_in, s_) == hipSuccess &&
+		    hipStreamWaitEvent(e->stream, e->ev_in, 0) == hipSuccess)
+			run = e->stream;
+	}
+	~EngineCall()
+	{
+		if (run != user && hipEventRecord(e->ev_out, run) == hipSuccess)
+			hipStreamWaitEvent(user, e->ev_out, 0);
+		engine_mark(e, user);
+	}
 };
-#define ENGINE_CALL(e, s) EngineCall _call(e, s)
+#define ENGINE_CALL(e, s) EngineCall _call(e, s); s = _call.run
 
 extern "C" {
 
@@ -963,6 +982,8 @@ int melpe_engine_create(melpe_engine **out, int device, int channels)
 	e->stream = g_dev_stream[device];
 	CREATE_STEP(hipEventCreate(&e->ev0));
 	CREATE_STEP(hipEventCreate(&e->ev1));
+	CREATE_STEP(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
+	CREATE_STEP(hipEventCreateWithFlags(&e->ev_out, hipEventDisableTiming));
 	CREATE_STEP(hipMalloc(&e->d_enc, sizeof(EncState) * (size_t) channels));
 	CREATE_STEP(hipMalloc(&e->d_dec, sizeof(DecState) * (size_t) channels));
 	CREATE_STEP(hipMalloc(&e->d_syn, sizeof(synth_state) * (size_t) channels));
@@ -1047,6 +1068,10 @@ int melpe_engine_destroy(melpe_engine *e)
 		hipEventDestroy(e->ev0);
 	if (e->ev1)
 		hipEventDestroy(e->ev1);
+	if (e->ev_in)
+		hipEventDestroy(e->ev_in);
+	if (e->ev_out)
+		hipEventDestroy(e->ev_out);
 	delete e;
 	return 0;
 }
@@ -1073,8 +1098,9 @@ int melpe_engine_reset_dev(melpe_engine *e, const void *d_mask, int which, void 
 	if (!e || which < 1 || which > 3)
 		return fail_msg("melpe_engine_reset_dev: bad arguments");
 	DEVGUARD(e->device);
-	ENGINE_CALL(e, (hipStream_t) hip_stream);
-	k_reset<<<grid_for(e->channels), WAVE, 0, (hipStream_t) hip_stream>>>(
+	hipStream_t s = (hipStream_t) hip_stream;
+	ENGINE_CALL(e, s);
+	k_reset<<<grid_for(e->channels), WAVE, 0, s>>>(
 		e->d_enc, e->d_dec, (const uint8_t *) d_mask, e->channels, which);
 	HIPCHK(hipGetLastError());
 	return 0;
@@ -1178,9 +1204,10 @@ int melpe_encode_npp_dev(melpe_engine *e, void *d_sp, const void *d_active, void
 	if (!e || !d_sp)
 		return fail_msg("melpe_encode_npp_dev: null argument");
 	DEVGUARD(e->device);
-	ENGINE_CALL(e, (hipStream_t) hip_stream);
+	hipStream_t s = (hipStream_t) hip_stream;
+	ENGINE_CALL(e, s);
 	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, (int16_t *) d_sp, (const uint8_t *) d_active,
-				       e->channels, (hipStream_t) hip_stream));
+				       e->channels, s));
 	return 0;
 }
 
@@ -1190,9 +1217,10 @@ int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const 
 	if (!e || !d_bits || !d_sp)
 		return fail_msg("melpe_encode_ana_dev: null argument");
 	DEVGUARD(e->device);
-	ENGINE_CALL(e, (hipStream_t) hip_stream);
+	hipStream_t s = (hipStream_t) hip_stream;
+	ENGINE_CALL(e, s);
 	HIPCHK((hipError_t) ana_launch(e, (const int16_t *) d_sp, (uint8_t *) d_bits,
-				       (const uint8_t *) d_active, (hipStream_t) hip_stream));
+				       (const uint8_t *) d_active, s));
 	return 0;
 }
 
@@ -1420,8 +1448,9 @@ int melpe_synth_dev(melpe_engine *e, void *d_sp, int samples, void *hip_stream)
 	if (!e || !d_sp || samples <= 0)
 		return fail_msg("melpe_synth_dev: bad arguments");
 	DEVGUARD(e->device);
-	ENGINE_CALL(e, (hipStream_t) hip_stream);
-	k_synth<<<grid_for(e->channels), WAVE, 0, (hipStream_t) hip_stream>>>(
+	hipStream_t s = (hipStream_t) hip_stream;
+	ENGINE_CALL(e, s);
+	k_synth<<<grid_for(e->channels), WAVE, 0, s>>>(
 		e->d_syn, (int16_t *) d_sp, samples, e->channels);
 	HIPCHK(hipGetLastError());
 	return 0;
