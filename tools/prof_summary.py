@@ -45,13 +45,23 @@ def kernel_stats(db):
 
 
 def pmc_means(db):
+    """mean counter values per dispatch of each kernel, leaving out each
+    kernel's first dispatch when it has more than one: melpe_engine_create
+    launches every codec kernel once at its full grid with no work (the
+    scratch reservation), and that launch would dilute the means"""
     c = sqlite3.connect(db)
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for name, disp, cn, cv in c.execute(
             "select name,dispatch_id,counter_name,counter_value from pmc_events"):
         per[(short(name), disp)][cn] += cv
+    first = {}
+    for (k, disp) in per:
+        first[k] = min(first.get(k, disp), disp)
+    count = collections.Counter(k for (k, _) in per)
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for (k, _), v in per.items():
+    for (k, disp), v in per.items():
+        if count[k] > 1 and disp == first[k]:
+            continue
         for cn, cv in v.items():
             agg[k][cn].append(cv)
     return {k: {cn: sum(v) / len(v) for cn, v in d.items()} for k, d in agg.items()}
