@@ -2,8 +2,6 @@
  * k_ana_mw.hip -- the lanes-per-channel analysis kernel (ana_mw.h), in its
  * own translation unit so it compiles beside k_ana.hip.
  */
-/* the branching shl/shr/L_shl/L_shr (ops.h): smaller code for this 1 MB kernel */
-#define MELPE_SHIFT_BRANCHY
 #include "kern.h"
 #include "ana_mw.h"
 

@@ -277,45 +277,6 @@ MD Word16 shl_core(Word16 a, int n)
 	return (Word16) v;
 }
 
-#if defined(MELPE_SHIFT_BRANCHY)
-/* the branching form (k_ana_mw.hip: the multi-wave kernel's code is 1 MB,
- * and the branch-free shifts' larger code made it 3x slower there) */
-MD Word16 shr(Word16 a, Word16 n);
-MD Word16 shl(Word16 a, Word16 n)
-{
-	OPC(18);
-	if (n == 0 || a == 0)
-		return a;
-	if (n < 0) {
-		if (n <= -15)
-			return (Word16) (a < 0 ? -1 : 0);
-		return (Word16) (a >> (-n));
-	}
-	if (n >= 15)
-		return (Word16) (a > 0 ? SW_MAX_ : SW_MIN_);
-	{
-		Word32 v = (Word32) a * (1 << n);
-		if (v != (Word16) v)
-			return (Word16) (a > 0 ? SW_MAX_ : SW_MIN_);
-		return (Word16) v;
-	}
-}
-
-MD Word16 shr(Word16 a, Word16 n)
-{
-	OPC(19);
-	if (n == 0 || a == 0)
-		return a;
-	if (n < 0) {
-		if (n <= -15)
-			return (Word16) (a > 0 ? SW_MAX_ : SW_MIN_);
-		return shl(a, (Word16) -n);
-	}
-	if (n >= 15)
-		return (Word16) (a < 0 ? -1 : 0);
-	return (Word16) (a >> n);
-}
-#else
 MD Word16 shl(Word16 a, Word16 n)
 {
 	OPC(18);
@@ -327,48 +288,8 @@ MD Word16 shr(Word16 a, Word16 n)
 	OPC(19);
 	return shl_core(a, -(int) n);
 }
-#endif
 
 /* L_shl/L_shr: mathhalf_i.h:942-1047 */
-#if defined(MELPE_SHIFT_BRANCHY)
-MD Word32 L_shl(Word32 a, Word16 n);
-MD Word32 L_shr(Word32 a, Word16 n)
-{
-	OPC(20);
-	if (n == 0 || a == 0)
-		return a;
-	if (n < 0) {
-		if (n <= -31)
-			return a > 0 ? LW_MAX_ : LW_MIN_;
-		return L_shl(a, (Word16) -n);
-	}
-	if (n >= 31)
-		return a > 0 ? 0 : -1;
-	return a >> n;
-}
-
-MD Word32 L_shl(Word32 a, Word16 n)
-{
-	OPC(21);
-	if (n == 0 || a == 0)
-		return a;
-	if (n < 0) {
-		if (n <= -31)
-			return a > 0 ? 0 : -1;
-		return a >> (-n);
-	}
-	if (n >= 31)
-		return a > 0 ? LW_MAX_ : LW_MIN_;
-	{
-		int64_t v = (int64_t) a * ((int64_t) 1 << n);
-		if (v > LW_MAX_)
-			return LW_MAX_;
-		if (v < LW_MIN_)
-			return LW_MIN_;
-		return (Word32) v;
-	}
-}
-#else
 /* branch-free, as shl: a right shift by min(-n, 31) for n < 0, else
  * a * 2^min(n, 32) in 64 bits clamped to 32; L_shr(a, n) = L_shl(a, -n)
  * over the whole range */
@@ -392,7 +313,6 @@ MD Word32 L_shr(Word32 a, Word16 n)
 	OPC(20);
 	return L_shl_core(a, -(int) n);
 }
-#endif
 
 /* shift_r / L_shift_r: mathhalf_i.h:1108-1230 */
 MD Word16 shift_r(Word16 a, Word16 n)
