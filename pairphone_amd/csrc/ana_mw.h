@@ -188,7 +188,7 @@ MD void pv_replay(const PvqWork &w, X &xc, const D &db, int16_t *il, Word32 *dl)
  * 140-145; each wave filters its own copy, only wave 0 keeps the result),
  * reading the superframe's PCM (4-byte aligned) where the caller holds it:
  * the three frames are one run of the same biquads */
-MD void ana_mw_begin(EncState *E, const int16_t *sp_in)
+MD void ana_mw_begin(EncAna *E, const int16_t *sp_in)
 {
 	static_assert(BLOCK % 36 == 0, "dc removal batches");
 	iir3_d_batched(sp_in, &E->hpspeech[IN_BEG], TB(dc_den), TB(dc_num), E->dcdelin,
@@ -197,7 +197,7 @@ MD void ana_mw_begin(EncState *E, const int16_t *sp_in)
 
 /* band k (1..4) of frame i on a non-driver wave */
 template <class X>
-MD void ana_mw_band(EncState *E, X &xc, int i, int k)
+MD void ana_mw_band(EncAna *E, X &xc, int i, int k)
 {
 	if (!E->bp_started && i == 0)	/* bpvc_ana's first call, on this band's copy */
 		bpvc_init_band(E, k);
@@ -211,7 +211,7 @@ MD void ana_mw_band(EncState *E, X &xc, int i, int k)
  * subframes taken from the exchange block; the frame's autocorrelation is
  * recomputed here (lpc_acor, a few hundred ops) instead of exchanged */
 template <class X>
-MD void ana_mw_classify(EncState *E, X &xc, int i)
+MD void ana_mw_classify(EncAna *E, X &xc, int i)
 {
 	const int16_t *speech = &E->hpspeech[i * FRAME];
 	int16_t ac[17];
@@ -227,7 +227,7 @@ MD void ana_mw_classify(EncState *E, X &xc, int i)
 /* virtual wave v's work in phase p; rec is the channel's HBM record, which
  * carries classify's and pitchAuto's tracks to v0 before phase NF+1 */
 template <class X, class D>
-MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, D &db, AnaMwTmp &tmp, int v, int p)
+MD void ana_mw_phase(EncAna *E, EncAna *rec, X &xc, D &db, AnaMwTmp &tmp, int v, int p)
 {
 	if (p < NF) {
 		const int i = p;
@@ -446,7 +446,7 @@ MD void ana_mw_phase(EncState *E, EncState *rec, X &xc, D &db, AnaMwTmp &tmp, in
  * its own group.  Nothing else of the copy is read before it is written;
  * the host build (emu_encode_ana_mw) fills the rest of each copy with a
  * pattern to check exactly that. */
-MD void ana_mw_copy_in(EncState *E, const EncState *rec, int w, int nw)
+MD void ana_mw_copy_in(EncAna *E, const EncAna *rec, int w, int nw)
 {
 	auto cp32 = [&](size_t off, size_t len) {
 		lane_copy32((char *) E + off, (const char *) rec + off, len);
@@ -454,40 +454,42 @@ MD void ana_mw_copy_in(EncState *E, const EncState *rec, int w, int nw)
 	auto cp16 = [&](size_t off, size_t len) {
 		lane_copy16((char *) E + off, (const char *) rec + off, len);
 	};
-	const size_t bs = sizeof(BandState), band0 = offsetof(EncState, band);
+	const size_t bs = sizeof(BandState), band0 = offsetof(EncAna, band);
 	if (w == 0) {
-		cp32(offsetof(EncState, hpspeech), offsetof(EncState, cls) - offsetof(EncState, hpspeech));
+		cp32(ENC_DRV_BEG, ENC_ANA_LIVE - ENC_DRV_BEG);
 		cp32(band0, bs);
 	} else {
-		cp32(offsetof(EncState, hpspeech), sizeof(int16_t) * IN_BEG);
-		cp32(offsetof(EncState, dcdelin), offsetof(EncState, sigbuf) - offsetof(EncState, dcdelin));
-		cp16(offsetof(EncState, classStat), offsetof(EncState, ana_started) - offsetof(EncState, classStat));
-		cp16(offsetof(EncState, bp_started), sizeof(int16_t));
-		cp16(offsetof(EncState, lsf_started), sizeof(int16_t) * (1 + LPC_ORD));
+		cp32(offsetof(EncAna, hpspeech), sizeof(int16_t) * IN_BEG);
+		/* dc memories, parameters, energies, the tracks and trackers */
+		cp32(ENC_DRV_BEG, offsetof(EncAna, ana_started) - ENC_DRV_BEG);
+		cp16(offsetof(EncAna, bp_started), sizeof(int16_t));
+		cp16(offsetof(EncAna, lsf_started), sizeof(int16_t) * (1 + LPC_ORD));
 	}
 	for (int v = w; v < MW_NV; v += nw) {
 		if (v == 1)
 			cp32(band0 + bs, 2 * bs);
 		else if (v == 2) {
-			cp32(offsetof(EncState, pa), sizeof(PautoState));
+			cp32(offsetof(EncAna, pa), sizeof(PautoState));
 			cp32(band0 + 3 * bs, bs);
 		} else if (v == 3) {
-			cp32(offsetof(EncState, cls), sizeof(ClsState));
+			cp32(offsetof(EncAna, cls), sizeof(ClsState));
 			cp32(band0 + 4 * bs, bs);
 		}
 	}
 }
 
-/* the byte ranges of the record virtual wave v owns (and writes back) */
+/* the byte ranges of the record virtual wave v owns (and writes back): the
+ * driver group up to the carried speech history (the rest of the record is
+ * working storage, state.h) */
 MD int ana_mw_owned(int v, size_t *off, size_t *len)
 {
-	const size_t cls = offsetof(EncState, cls), pa = offsetof(EncState, pa);
+	const size_t cls = offsetof(EncAna, cls), pa = offsetof(EncAna, pa);
 	const size_t bs = sizeof(BandState);
-	auto band = [&](int k) { return offsetof(EncState, band) + k * bs; };
+	auto band = [&](int k) { return offsetof(EncAna, band) + k * bs; };
 	switch (v) {
 	case 0:
-		off[0] = offsetof(EncState, hpspeech);
-		len[0] = cls - off[0];
+		off[0] = ENC_DRV_BEG;
+		len[0] = ENC_ANA_LIVE - ENC_DRV_BEG;
 		off[1] = band(0);
 		len[1] = bs;
 		return 2;

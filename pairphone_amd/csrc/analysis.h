@@ -834,7 +834,7 @@ MN Word16 double_chk(const int16_t *sig, Word16 *pcorr, Word16 pitch, Word16 pdo
 }
 
 /* p_avg_update :515 */
-MD Word16 p_avg_update(EncState *E, Word16 pitch, Word16 pcorr, Word16 pthresh)
+MD Word16 p_avg_update(EncAna *E, Word16 pitch, Word16 pcorr, Word16 pthresh)
 {
 	if (!E->pavg_started) {
 		v_set(E->good_pitch, DEFAULT_PITCH_Q7, NF);
@@ -853,7 +853,7 @@ MD Word16 p_avg_update(EncState *E, Word16 pitch, Word16 pcorr, Word16 pthresh)
 /* pitch_ana :571 -- final pitch from the lowpassed residual, with the
  * speech fallback; pa_sigbuf is persistent (its tail 323..326 can be read
  * stale by double_chk) */
-MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Word16 pest,
+MN Word16 pitch_ana(EncAna *E, const int16_t *speech, const int16_t *resid, Word16 pest,
 		    Word16 pavg, Word16 *pcorr2)
 {
 	PROF_SCOPE(7);
@@ -950,7 +950,7 @@ MN Word16 pitch_ana(EncState *E, const int16_t *speech, const int16_t *resid, Wo
 /* bpvc_ana, melpe/melp_sub.c:77 -- 5-band bandpass voicing           */
 /* ------------------------------------------------------------------ */
 /* bpvc_ana's first-call zeroing of the band memories (melp_sub.c:91-101) */
-MD void bpvc_init_band(EncState *E, int b)
+MD void bpvc_init_band(EncAna *E, int b)
 {
 	BandState *B = &E->band[b];
 	v_zero(B->fsp, PITCH_FR - FRAME);
@@ -960,7 +960,7 @@ MD void bpvc_init_band(EncState *E, int b)
 	B->env2 = 0;
 }
 
-MD void bpvc_init(EncState *E)
+MD void bpvc_init(EncAna *E)
 {
 	if (!E->bp_started) {
 		for (int i = 0; i < NUM_BANDS; i++)
@@ -971,7 +971,7 @@ MD void bpvc_init(EncState *E)
 
 #if defined(MELPE_OPCOUNT)
 /* census build: the reference's pass structure, op for op */
-MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
+MN void bpvc_ana(EncAna *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
 		 Word16 *pitch)
 {
 	PROF_SCOPE(4);
@@ -1064,7 +1064,7 @@ MD int64_t bp_window(int16_t *hist, const int16_t *sp, int16_t *w, const int16_t
 /* band 0 of bpvc_ana (melp_sub.c:104-135): the lowest band's window, the
  * better of the two pitch candidates' correlations -> bpvc[0], *pitch.
  * `speech` as bpvc_ana's. */
-MN void bpvc_band0(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc0,
+MN void bpvc_band0(EncAna *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc0,
 		   Word16 *pitch)
 {
 	int16_t sb[BPF_ORD + PITCH_FR];
@@ -1117,13 +1117,13 @@ MN void bpvc_band_s(BandState *B, const int16_t *sp, int i, Word16 pitch, int16_
 		*bpvci = pcorr;
 }
 
-MN void bpvc_band(EncState *E, const int16_t *speech, int i, Word16 pitch, int16_t *bpvci)
+MN void bpvc_band(EncAna *E, const int16_t *speech, int i, Word16 pitch, int16_t *bpvci)
 {
 	bpvc_band_s(&E->band[i], &speech[PITCH_FR - FRAME - PITCHMAX], i, pitch, bpvci);
 }
 
 /* bpvc_ana, melpe/melp_sub.c:77 */
-MN void bpvc_ana(EncState *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
+MN void bpvc_ana(EncAna *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc,
 		 Word16 *pitch)
 {
 	PROF_SCOPE(4);
@@ -1547,7 +1547,7 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 }
 
 /* pitchAuto :63 */
-MN void pitchAuto(EncState *E, const int16_t *in, PitTrack *pt, ClassParam *cs)
+MN void pitchAuto(EncAna *E, const int16_t *in, PitTrack *pt, ClassParam *cs)
 {
 	PROF_SCOPE(5);
 	if (!E->pa.pauto_started) {
@@ -1878,7 +1878,7 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 
 /* classify :92 -- silence/unvoiced/voiced/transition decision per 90-sample
  * subframe; cs[-1] is the previous subframe's parameters */
-MN void classify(EncState *E, const int16_t *in, ClassParam *cs, const int16_t *ac)
+MN void classify(EncAna *E, const int16_t *in, ClassParam *cs, const int16_t *ac)
 {
 	PROF_SCOPE(6);
 	/* so[2..222): the band-passed signal frac_cor reads; so[2..132) is

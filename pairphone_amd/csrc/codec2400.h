@@ -329,7 +329,7 @@ MD Word16 fec_decode24(QuantParam *q, Word16 erase)
 
 /* melp_chn_write :109 -- 54 bits: fields into a bit buffer, then out in
  * bit_order (melp_chn.c:77) into chbuf[0..6] */
-MN void melp_chn_write24(EncState *E)
+MN void melp_chn_write24(EncAna *E)
 {
 	QuantParam *q = &E->qpar;
 	fec_code24(q);
@@ -401,7 +401,7 @@ MN Word16 melp_chn_read24(DecState *D, MelpParam *par, const MelpParam *prev)
 }
 
 /* analysis() at RATE2400: one NPP-processed 180-sample frame -> chbuf[0..6] */
-MN void analysis24(EncState *E, const int16_t *sp_in)
+MN void analysis24(EncAna *E, const int16_t *sp_in)
 {
 	MelpParam *par = &E->par[0];
 	QuantParam *q = &E->qpar;

@@ -30,7 +30,7 @@ namespace mlp {
  * different waves of one workgroup. */
 
 /* the first call's initialisation (melp_ana.c:300-306) */
-MD void ana_first(EncState *E)
+MD void ana_first(EncAna *E)
 {
 	if (!E->ana_started) {
 		v_zero(E->lpfsp_delin, LPF_ORD);
@@ -56,7 +56,7 @@ MN Word16 global_pitch(const int16_t *speech, int16_t *sb, int16_t *delin, int16
 	return shl(p, 7);
 }
 
-MN void ana_global_pitch(EncState *E, const int16_t *speech)
+MN void ana_global_pitch(EncAna *E, const int16_t *speech)
 {
 #if !defined(MELPE_KO_GPITCH)
 	E->fpitch[1] = global_pitch(speech, E->sigbuf, E->lpfsp_delin, E->lpfsp_delout);
@@ -66,7 +66,7 @@ MN void ana_global_pitch(EncState *E, const int16_t *speech)
 /* LPC analysis (melp_ana.c:366-393): ac[17] (the autocorrelation classify
  * also reads), lpc[0..LPC_ORD] and, when lsf is given, the LSFs */
 template <bool R24>
-MN void ana_lpc(EncState *E, const int16_t *speech, int16_t *ac, int16_t *lpc, int16_t *lsf)
+MN void ana_lpc(EncAna *E, const int16_t *speech, int16_t *ac, int16_t *lpc, int16_t *lsf)
 {
 	lpc_acor(&speech[FRAME_END - LPC_FRAME / 2], TB(win_cof), ac, 4, R24 ? LPC_ORD : 16,
 		 LPC_FRAME);
@@ -85,7 +85,7 @@ MN void ana_lpc(EncState *E, const int16_t *speech, int16_t *ac, int16_t *lpc, i
 }
 
 /* the prediction residual into sigbuf and its peakiness (melp_ana.c:395-399) */
-MN Word16 ana_resid(EncState *E, const int16_t *speech, const int16_t *lpc)
+MN Word16 ana_resid(EncAna *E, const int16_t *speech, const int16_t *lpc)
 {
 	int16_t *sb = E->sigbuf;
 	zerflt(&speech[PITCH_BEG], lpc, &sb[LPF_ORD], LPC_ORD, PITCH_FR);
@@ -104,7 +104,7 @@ MD void ana_peaky(int16_t *bpvc, Word16 t, int lo, int hi)
 
 /* pitchAuto + classify of one 90-sample subframe of frame subnum
  * (melp_ana.c:411-426): sub 0 / 1 */
-MN void ana_track_pa(EncState *E, const int16_t *speech, int subnum, int sub)
+MN void ana_track_pa(EncAna *E, const int16_t *speech, int subnum, int sub)
 {
 	int ct = CUR_TRACK + subnum * PIT_SUBNUM;
 #if !defined(MELPE_KO_PAUTO)
@@ -113,7 +113,7 @@ MN void ana_track_pa(EncState *E, const int16_t *speech, int subnum, int sub)
 #endif
 }
 
-MN void ana_track_cl(EncState *E, const int16_t *speech, int subnum, int sub, const int16_t *ac)
+MN void ana_track_cl(EncAna *E, const int16_t *speech, int subnum, int sub, const int16_t *ac)
 {
 	int ct = CUR_TRACK + subnum * PIT_SUBNUM;
 #if !defined(MELPE_KO_CLASSIFY)
@@ -124,7 +124,7 @@ MN void ana_track_cl(EncState *E, const int16_t *speech, int subnum, int sub, co
 
 /* final pitch, gains, pitch average and voicing (melp_ana.c:428-468) */
 template <bool R24>
-MN void ana_pitch_gain(EncState *E, const int16_t *speech, MelpParam *par, Word16 sub_pitch)
+MN void ana_pitch_gain(EncAna *E, const int16_t *speech, MelpParam *par, Word16 sub_pitch)
 {
 	int16_t *sb = E->sigbuf;
 	Word16 pcorr, t;
@@ -150,7 +150,7 @@ MN void ana_pitch_gain(EncState *E, const int16_t *speech, MelpParam *par, Word1
 }
 
 template <bool R24>
-MN void melp_ana(EncState *E, const int16_t *speech, MelpParam *par, int subnum)
+MN void melp_ana(EncAna *E, const int16_t *speech, MelpParam *par, int subnum)
 {
 	PROF_SCOPE(1);
 	int16_t ac[17], lpc[LPC_ORD + 1];
@@ -216,7 +216,7 @@ MN void sc_track_fix(PitTrack *pt, int16_t *pitch, Word16 prev_pitch)
 }
 
 /* sc_ana :522 -- superframe pitch smoothing and bpvc smoothing */
-MN void sc_ana(EncState *E, MelpParam *par)
+MN void sc_ana(EncAna *E, MelpParam *par)
 {
 	PROF_SCOPE(8);
 	ClassParam *cs = E->classStat;
@@ -432,7 +432,7 @@ MN void sc_ana(EncState *E, MelpParam *par)
 /* analysis() in the two parts the GPU runs as separate kernels:
  * analysis_frame: dc removal and melp_ana of frame i (melp_ana.c:140-160);
  * analysis_tail: sc_ana, the quantisers and channel packing (:162-265) */
-MD void analysis_frame(EncState *E, const int16_t *sp_in, int i)
+MD void analysis_frame(EncAna *E, const int16_t *sp_in, int i)
 {
 	dc_rmv(&sp_in[i * FRAME], &E->hpspeech[IN_BEG + i * FRAME], E->dcdelin,
 	       E->dcdelout_hi, E->dcdelout_lo, FRAME);
@@ -441,7 +441,7 @@ MD void analysis_frame(EncState *E, const int16_t *sp_in, int i)
 
 /* the Fourier magnitudes of frame i (melp_ana.c:224-236): the LPC residual
  * of the quantised LSFs, windowed, through find_harm; 8192s when unvoiced */
-MN void ana_fsmag_frame(EncState *E, MelpParam *par, int i)
+MN void ana_fsmag_frame(EncAna *E, MelpParam *par, int i)
 {
 	int16_t lpc[LPC_ORD + 1];
 	lpc[0] = 4096;
@@ -460,7 +460,7 @@ MN void ana_fsmag_frame(EncState *E, MelpParam *par, int i)
 /* ana_fsmag_frame's pitch-independent half, run before the frame's pitch is
  * quantised (ana_mw.h): the residual of the quantised LSFs, windowed, and
  * its FFT (melp_ana.c:224-233) */
-MN void ana_fsmag_fft(EncState *E, MelpParam *par, int i, uint32_t *hb)
+MN void ana_fsmag_fft(EncAna *E, MelpParam *par, int i, uint32_t *hb)
 {
 	int16_t lpc[LPC_ORD + 1];
 	lpc[0] = 4096;
@@ -472,7 +472,7 @@ MN void ana_fsmag_fft(EncState *E, MelpParam *par, int i, uint32_t *hb)
 }
 
 /* quant_fsmag, the channel write and the history shift (melp_ana.c:238-265) */
-MN void ana_pack(EncState *E)
+MN void ana_pack(EncAna *E)
 {
 	MelpParam *par = E->par;
 	quant_fsmag(E, par);
@@ -482,7 +482,7 @@ MN void ana_pack(EncState *E)
 	v_copy(E->hpspeech, &E->hpspeech[NF * FRAME], IN_BEG);
 }
 
-MN void analysis_tail(EncState *E)
+MN void analysis_tail(EncAna *E)
 {
 	MelpParam *par = E->par;
 	sc_ana(E, par);
@@ -510,7 +510,7 @@ MN void analysis_tail(EncState *E)
  * analysis_b packs the superframe.  The shift reads only hpspeech, which
  * nothing after it reads, so moving it ahead of the packing changes no
  * value. */
-MN void analysis_a2(EncState *E, int16_t *res)
+MN void analysis_a2(EncAna *E, int16_t *res)
 {
 	MelpParam *par = E->par;
 	sc_ana(E, par);
@@ -538,7 +538,7 @@ MN void analysis_a2(EncState *E, int16_t *res)
 	v_copy(E->hpspeech, &E->hpspeech[NF * FRAME], IN_BEG);
 }
 
-MN void analysis_a(EncState *E, const int16_t *sp_in, int16_t *res)
+MN void analysis_a(EncAna *E, const int16_t *sp_in, int16_t *res)
 {
 #if defined(MELPE_KO_ANALYSIS)
 	return;
@@ -549,12 +549,12 @@ MN void analysis_a(EncState *E, const int16_t *sp_in, int16_t *res)
 }
 
 /* the history shift at the end of analysis (melp_ana.c:262) */
-MD void ana_shift(EncState *E)
+MD void ana_shift(EncAna *E)
 {
 	v_copy(E->hpspeech, &E->hpspeech[NF * FRAME], IN_BEG);
 }
 
-MN void analysis_b(EncState *E)
+MN void analysis_b(EncAna *E)
 {
 	MelpParam *par = E->par;
 	quant_fsmag(E, par);
@@ -563,7 +563,7 @@ MN void analysis_b(EncState *E)
 	low_rate_chn_write(E);
 }
 
-MN void analysis(EncState *E, const int16_t *sp_in)
+MN void analysis(EncAna *E, const int16_t *sp_in)
 {
 	PROF_SCOPE(15);
 #if defined(MELPE_KO_ANALYSIS)
@@ -577,7 +577,7 @@ MN void analysis(EncState *E, const int16_t *sp_in)
 /* debug aid: analysis() stopped after `upto` of its stages (1 = dc_rmv +
  * melp_ana, 2 = + sc_ana, 3 = + lsf_vq, 4 = + pitch/gain/jitter/bp,
  * 5 = + Fourier magnitudes, 6 = + channel write) */
-MN void analysis_upto(EncState *E, const int16_t *sp_in, int upto)
+MN void analysis_upto(EncAna *E, const int16_t *sp_in, int upto)
 {
 	MelpParam *par = E->par;
 	int16_t lpc[LPC_ORD + 1];
@@ -625,13 +625,13 @@ MN void analysis_upto(EncState *E, const int16_t *sp_in, int upto)
 
 /* melpe_a :91 -- sp (540) is denoised in place, then analysed; the 11-byte
  * frame is left in E->chbuf */
-MN void encode_superframe(EncState *E, NppScratch *w, int16_t *sp)
+MN void encode_superframe(EncState *S, NppScratch *w, int16_t *sp)
 {
 	PROF_SCOPE(16);
-	npp_frame(&E->npp, w, sp, sp);
-	npp_frame(&E->npp, w, sp + FRAME, sp + FRAME);
-	npp_frame(&E->npp, w, sp + 2 * FRAME, sp + 2 * FRAME);
-	analysis(E, sp);
+	npp_frame(&S->npp, w, sp, sp);
+	npp_frame(&S->npp, w, sp + FRAME, sp + FRAME);
+	npp_frame(&S->npp, w, sp + 2 * FRAME, sp + 2 * FRAME);
+	analysis(&S->a, sp);
 }
 
 }  // namespace mlp

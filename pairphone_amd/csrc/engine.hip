@@ -118,7 +118,7 @@ __global__ __launch_bounds__(WAVE) void k_reset(EncState *enc, DecState *dec,
 __global__ void k_melpe_i(EncState *enc, DecState *dec)
 {
 	if (threadIdx.x == 0) {
-		enc_melpe_i(enc);
+		enc_melpe_i(&enc->a);
 		dec_melpe_i(dec);
 	}
 }
@@ -132,16 +132,17 @@ __global__ void k_share_params(EncState *enc, DecState *dec, int dir)
 {
 	if (threadIdx.x != 0)
 		return;
+	EncAna *a = &enc->a;
 	if (dir == 0) {
 		for (int i = 0; i < NF; i++)
-			dec->par[i] = enc->par[i];
-		dec->qpar = enc->qpar;
+			dec->par[i] = a->par[i];
+		dec->qpar = a->qpar;
 	} else {
 		for (int i = 0; i < NF; i++)
-			enc->par[i] = dec->par[i];
-		enc->qpar = dec->qpar;
+			a->par[i] = dec->par[i];
+		a->qpar = dec->qpar;
 		for (int k = 0; k < 11; k++)
-			enc->chbuf[k] = dec->chbuf[k];
+			a->chbuf[k] = dec->chbuf[k];
 	}
 }
 
@@ -702,8 +703,8 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 	BinBuf &b = e->bin_enc;
 	bool on;
 	hipError_t er = bin_launch(e->lane_order, b, e->d_enc, sizeof(EncState),
-				   (int) offsetof(EncState, par),
-				   (int) (offsetof(EncState, qpar) + offsetof(QuantParam, uv_flag)),
+				   (int) (offsetof(EncState, a) + offsetof(EncAna, par)),
+				   (int) (offsetof(EncState, a) + offsetof(EncAna, qpar) + offsetof(QuantParam, uv_flag)),
 				   d_act, e->channels, s, &on);
 	if (er != hipSuccess)
 		return (int) er;

@@ -95,7 +95,7 @@ int emu_encode(emu_engine *e, unsigned char *bits, int16_t *sp)
 	for (int c = 0; c < e->channels; c++) {
 		encode_superframe(&e->enc[c], &g_npp_scratch, sp + (size_t) c * BLOCK);
 		for (int k = 0; k < 11; k++)
-			bits[c * 11 + k] = e->enc[c].chbuf[k];
+			bits[c * 11 + k] = e->enc[c].a.chbuf[k];
 	}
 	return 0;
 }
@@ -117,11 +117,18 @@ int emu_encode_npp(emu_engine *e, int16_t *sp)
 int emu_encode_ana_split(emu_engine *e, unsigned char *bits, const int16_t *sp)
 {
 	static int16_t res[NF * LPC_FRAME];
+	static EncAna L;	/* the lane's private copy (k_ana.hip AnaLane) */
 	for (int c = 0; c < e->channels; c++) {
-		EncState *E = &e->enc[c];
+		EncAna *E = &L;
 		for (int k = 0; k < NF * LPC_FRAME; k++)
 			res[k] = (int16_t) 0x5a5a;	/* unvoiced rows stay unread */
+		/* the live prefix in, the working storage a pattern (state.h):
+		 * nothing may read it before writing it */
+		memcpy(E, &e->enc[c].a, ENC_ANA_LIVE);
+		memset((char *) E + ENC_ANA_LIVE, 0x5a + (c & 7), sizeof(EncAna) - ENC_ANA_LIVE);
 		analysis_a(E, sp + (size_t) c * BLOCK, res);
+		memcpy(&e->enc[c].a, E, ENC_ANA_LIVE);
+		E = &e->enc[c].a;
 		for (int i = 0; i < NF; i++) {
 			MelpParam *par = &E->par[i];
 			v_set(par->fs_mag, 8192, NUM_HARM);
@@ -138,9 +145,9 @@ int emu_encode_ana_split(emu_engine *e, unsigned char *bits, const int16_t *sp)
 int emu_encode_ana(emu_engine *e, unsigned char *bits, const int16_t *sp)
 {
 	for (int c = 0; c < e->channels; c++) {
-		analysis(&e->enc[c], sp + (size_t) c * BLOCK);
+		analysis(&e->enc[c].a, sp + (size_t) c * BLOCK);
 		for (int k = 0; k < 11; k++)
-			bits[c * 11 + k] = e->enc[c].chbuf[k];
+			bits[c * 11 + k] = e->enc[c].a.chbuf[k];
 	}
 	return 0;
 }
@@ -167,9 +174,9 @@ int emu_encode_ana_mw(emu_engine *e, unsigned char *bits, const int16_t *sp, int
 {
 	if (nw < 1 || nw > MW_NV)
 		return -1;
-	std::vector<EncState> W(nw);
+	std::vector<EncAna> W(nw);
 	for (int c = 0; c < e->channels; c++) {
-		EncState &rec = e->enc[c];
+		EncAna &rec = e->enc[c].a;
 		const int16_t *x = sp + (size_t) c * BLOCK;
 		HostXch xc;
 		memset(&xc, 0x5a, sizeof xc);	/* nothing may read a slot before it is written */
@@ -177,7 +184,7 @@ int emu_encode_ana_mw(emu_engine *e, unsigned char *bits, const int16_t *sp, int
 		memset(&db, 0xa5, sizeof db);
 		AnaMwTmp tmp[MW_NV];
 		for (int w = 0; w < nw; w++) {
-			memset(&W[w], 0xa5 + w, sizeof(EncState));	/* uncopied bytes: a pattern */
+			memset(&W[w], 0xa5 + w, sizeof(EncAna));	/* uncopied bytes: a pattern */
 			ana_mw_copy_in(&W[w], &rec, w, nw);
 			ana_mw_begin(&W[w], x);
 		}
@@ -228,7 +235,7 @@ int emu_decode(emu_engine *e, int16_t *sp, const unsigned char *bits)
  * quant_par (30 int16), in the layout oracle/ref_tool.c dumps */
 int emu_enc_params(emu_engine *e, int c, int16_t *out)
 {
-	const EncState *E = &e->enc[c];
+	const EncAna *E = &e->enc[c].a;
 	memcpy(out, E->par, sizeof(E->par));
 	const QuantParam *q = &E->qpar;
 	int16_t *w = out + 90;
@@ -256,7 +263,7 @@ int emu_enc_params(emu_engine *e, int c, int16_t *out)
  * melpe_s (engine.hip k_share_params), channel 0 */
 int emu_share(emu_engine *e, int dir)
 {
-	EncState *E = &e->enc[0];
+	EncAna *E = &e->enc[0].a;
 	DecState *D = &e->dec[0];
 	if (dir == 0) {
 		memcpy(D->par, E->par, sizeof(D->par));
@@ -373,8 +380,8 @@ int emu_encode2400(emu_engine *e, unsigned char *bits, int16_t *sp)
 		EncState *S = &e->enc[c];
 		int16_t *x = sp + (size_t) c * FRAME;
 		npp_frame(&S->npp, &g_npp_scratch, x, x, false);
-		analysis24(S, x);
-		memcpy(bits + (size_t) c * R24_BYTES, S->chbuf, R24_BYTES);
+		analysis24(&S->a, x);
+		memcpy(bits + (size_t) c * R24_BYTES, S->a.chbuf, R24_BYTES);
 	}
 	return 0;
 }

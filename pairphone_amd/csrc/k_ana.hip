@@ -9,9 +9,11 @@
 
 MELPE_TU(ana)
 
+/* the lane's frame: the analysis state only (not the NPP state), whose
+ * live prefix moves in and out (state.h ENC_ANA_LIVE), and the PCM block */
 struct AnaLane {
 	uint8_t guard[FLAT_GUARD_BYTES];
-	EncState S;	/* only the part after the NPP state is live */
+	EncAna S;
 	int16_t x[BLOCK];
 };
 
@@ -36,17 +38,15 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 	}
 	AnaLane L;
 	PIN_FRAME(L);
-	constexpr size_t nb = ENC_ANA_BYTES;
-	static_assert(nb % 16 == 0 && ENC_ANA_OFF % 16 == 0 && sizeof(EncState) % 16 == 0 &&
-			      offsetof(AnaLane, S) % 16 == 0,
-		      "the record copy is in 16-byte pieces");
-	lane_copy_x4((char *) &L.S + ENC_ANA_OFF, (const char *) &enc[c] + ENC_ANA_OFF, nb);
+	constexpr size_t nb = ENC_ANA_LIVE;
+	static_assert(offsetof(AnaLane, S) % 16 == 0, "the record copy is in 16-byte pieces");
+	lane_copy_x4(&L.S, &enc[c].a, nb);
 	lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
 	if (MODE == 0)
 		analysis(&L.S, L.x);
 	else
 		analysis_a(&L.S, L.x, res + (size_t) c * NF * LPC_FRAME);
-	lane_copy_x4((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, nb);
+	lane_copy_x4(&enc[c].a, &L.S, nb);
 	if (MODE == 0)
 		for (int k = 0; k < 11; k++)
 			bits[(size_t) c * 11 + k] = L.S.chbuf[k];
@@ -60,10 +60,10 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana_dbg(EncState 
 		return;
 	AnaLane L;
 	PIN_FRAME(L);
-	lane_copy((char *) &L.S + ENC_ANA_OFF, (const char *) &enc[c] + ENC_ANA_OFF, ENC_ANA_BYTES);
+	lane_copy(&L.S, &enc[c].a, ENC_ANA_LIVE);
 	lane_copy(L.x, sp + (size_t) c * BLOCK, sizeof(int16_t) * BLOCK);
 	analysis_upto(&L.S, L.x, upto);
-	lane_copy((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, ENC_ANA_BYTES);
+	lane_copy(&enc[c].a, &L.S, ENC_ANA_LIVE);
 }
 
 /* MELPE_ANA_LDS (diagnostic): reserve that many bytes of LDS per wave to cap

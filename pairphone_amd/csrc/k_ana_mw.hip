@@ -55,7 +55,7 @@ struct GlbDb {
 
 struct AnaMwLane {
 	uint8_t guard[FLAT_GUARD_BYTES];
-	EncState S;	/* only the part after the NPP state is live */
+	EncAna S;
 	AnaMwTmp tmp;
 };
 
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_MW_WAVES) void k_enc_ana_mw(EncSta
 	PIN_FRAME(L);
 	LdsXch xc{xs, t};
 	GlbDb db{lqbuf + blockIdx.x * WAVE + t, (size_t) gridDim.x * WAVE};
-	EncState *rec = &enc[c];
+	EncAna *rec = &enc[c].a;
 	MW_T0(tb);
 	if (live)
 		ana_mw_copy_in(&L.S, rec, w, NW);

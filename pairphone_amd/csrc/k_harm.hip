@@ -157,7 +157,7 @@ __global__ __launch_bounds__(WAVE) void k_enc_harm(EncState *enc, const int16_t 
 	WvConst kc;
 	wv_const_init(&kc, lane);
 	for (int i = 0; i < NF; i++) {
-		MelpParam *par = &enc[c].par[i];
+		MelpParam *par = &enc[c].a.par[i];
 		const Word16 uv = par->uv_flag, pitch = par->pitch;
 		if (uv) {	/* ana_fsmag_frame: 8192s, no FFT */
 			if (lane < NUM_HARM)
@@ -186,7 +186,7 @@ extern "C" int kl_enc_harm(EncState *enc, const int16_t *res, const uint8_t *act
  * channel, on the part of the record it reads and writes */
 struct TailLane {
 	uint8_t guard[FLAT_GUARD_BYTES];
-	EncState S;
+	EncAna S;
 };
 
 __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active,
@@ -204,15 +204,16 @@ __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bi
 	PIN_FRAME(L);
 	/* par + qpar, and fsm_prev_uv .. chbuf, widened to dwords (the extra
 	 * int16 at either end goes back unchanged) */
-	constexpr size_t o = offsetof(EncState, par), e = offsetof(EncState, voicedEn);
-	constexpr size_t o2 = offsetof(EncState, fsm_prev_uv) & ~(size_t) 3;
-	constexpr size_t e2 = (offsetof(EncState, top_lpc) + 3) & ~(size_t) 3;
+	constexpr size_t o = offsetof(EncAna, par), e = offsetof(EncAna, voicedEn);
+	constexpr size_t o2 = offsetof(EncAna, fsm_prev_uv) & ~(size_t) 3;
+	constexpr size_t e2 = (offsetof(EncAna, top_lpc) + 3) & ~(size_t) 3;
 	static_assert(o % 4 == 0 && e % 4 == 0, "the tail's record ranges are dword copies");
-	lane_copy((char *) &L.S + o, (const char *) &enc[c] + o, e - o);
-	lane_copy((char *) &L.S + o2, (const char *) &enc[c] + o2, e2 - o2);
+	EncAna *R = &enc[c].a;
+	lane_copy((char *) &L.S + o, (const char *) R + o, e - o);
+	lane_copy((char *) &L.S + o2, (const char *) R + o2, e2 - o2);
 	analysis_b(&L.S);
-	lane_copy((char *) &enc[c] + o, (const char *) &L.S + o, e - o);
-	lane_copy((char *) &enc[c] + o2, (const char *) &L.S + o2, e2 - o2);
+	lane_copy((char *) R + o, (const char *) &L.S + o, e - o);
+	lane_copy((char *) R + o2, (const char *) &L.S + o2, e2 - o2);
 	for (int k = 0; k < 11; k++)
 		bits[(size_t) c * 11 + k] = L.S.chbuf[k];
 }

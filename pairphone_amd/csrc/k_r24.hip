@@ -12,7 +12,7 @@ MELPE_TU(r24)
 
 struct Ana24Lane {
 	uint8_t guard[FLAT_GUARD_BYTES];
-	EncState S;	/* only the part after the NPP state is live */
+	EncAna S;
 	int16_t x[FRAME];
 };
 
@@ -25,10 +25,10 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc24(EncState *enc, 
 		return;
 	Ana24Lane L;
 	PIN_FRAME(L);
-	lane_copy((char *) &L.S + ENC_ANA_OFF, (const char *) &enc[c] + ENC_ANA_OFF, ENC_ANA_BYTES);
+	lane_copy(&L.S, &enc[c].a, sizeof(EncAna));
 	lane_copy(L.x, sp + (size_t) c * FRAME, sizeof(int16_t) * FRAME);
 	analysis24(&L.S, L.x);
-	lane_copy((char *) &enc[c] + ENC_ANA_OFF, (const char *) &L.S + ENC_ANA_OFF, ENC_ANA_BYTES);
+	lane_copy(&enc[c].a, &L.S, sizeof(EncAna));
 	for (int k = 0; k < R24_BYTES; k++)
 		bits[(size_t) c * R24_BYTES + k] = L.S.chbuf[k];
 }

@@ -132,8 +132,5 @@ static inline unsigned grid_for(int n)
 	return (unsigned) ((n + WAVE - 1) / WAVE);
 }
 
-/* the encoder state after the NPP part: what analysis() touches */
-#define ENC_ANA_OFF offsetof(EncState, hpspeech)
-#define ENC_ANA_BYTES (sizeof(EncState) - ENC_ANA_OFF)
 
 #endif

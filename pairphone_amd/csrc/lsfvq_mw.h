@@ -175,7 +175,7 @@ MD void lq_next_job(LsfLead &L, MelpParam *par, int job)
 }
 
 /* lsf_vq's prelude (qnt12.c:908-955): weights, voicing pattern, first job */
-MD void lq_prelude(LsfLead &L, EncState *E, MelpParam *par)
+MD void lq_prelude(LsfLead &L, EncAna *E, MelpParam *par)
 {
 	int16_t lpc[LPC_ORD];
 	if (!E->lsf_started) {
@@ -208,7 +208,7 @@ MD void lq_prelude(LsfLead &L, EncState *E, MelpParam *par)
 
 /* publish the next compute step */
 template <class X>
-MD void lq_publish(const LsfLead &L, const EncState *E, const MelpParam *par, X &xc, int b)
+MD void lq_publish(const LsfLead &L, const EncAna *E, const MelpParam *par, X &xc, int b)
 {
 	if (L.done) {
 		xc.put(b + XL_JOB, 0);
@@ -329,7 +329,7 @@ MD void lq_vq_scan(LsfLead &L, const D &db)
 }
 
 /* lsf_vq's end (qnt12.c:1127-1137) */
-MD void lq_epilogue(EncState *E, MelpParam *par)
+MD void lq_epilogue(EncAna *E, MelpParam *par)
 {
 	lspStable(par[0].lsf, LPC_ORD);
 	lspStable(par[1].lsf, LPC_ORD);
@@ -341,7 +341,7 @@ MD void lq_epilogue(EncState *E, MelpParam *par)
 /* the leader's scan phase: finish the step computed last phase, start and
  * publish the next */
 template <class X, class D>
-MD void lq_scan(LsfLead &L, EncState *E, MelpParam *par, X &xc, int b, const D &db)
+MD void lq_scan(LsfLead &L, EncAna *E, MelpParam *par, X &xc, int b, const D &db)
 {
 	if (L.done)
 		return;

@@ -193,7 +193,7 @@ MD int pvq_cb(const PvqWork &w, int *size)
 	return w.cnt == NF ? TOFF_pitch_vq_cb_vvv : TOFF_pitch_vq_cb_uvv;
 }
 
-MN int pvq_prelude(EncState *E, MelpParam *par, PvqWork &w)
+MN int pvq_prelude(EncAna *E, MelpParam *par, PvqWork &w)
 {
 	QuantParam *q = &E->qpar;
 	for (int i = 0; i < NF; i++)
@@ -239,7 +239,7 @@ MN int pvq_prelude(EncState *E, MelpParam *par, PvqWork &w)
 	return cnt;
 }
 
-MN void pvq_finish(EncState *E, MelpParam *par, const PvqWork &w, const int16_t *il,
+MN void pvq_finish(EncAna *E, MelpParam *par, const PvqWork &w, const int16_t *il,
 		   const Word32 *dl)
 {
 	int size;
@@ -263,7 +263,7 @@ MN void pvq_finish(EncState *E, MelpParam *par, const PvqWork &w, const int16_t 
 	E->qpar.pitch_index = pi;
 }
 
-MN void pitch_vq(EncState *E, MelpParam *par)
+MN void pitch_vq(EncAna *E, MelpParam *par)
 {
 	PROF_SCOPE(10);
 	PvqWork w;
@@ -278,7 +278,7 @@ MN void pitch_vq(EncState *E, MelpParam *par)
 }
 
 /* gain_vq :368 -- 1024 x 6 full search with the reference's early skip */
-MN void gain_vq(EncState *E, MelpParam *par)
+MN void gain_vq(EncAna *E, MelpParam *par)
 {
 	PROF_SCOPE(11);
 	const int16_t *cb = TB(gain_vq_cb);
@@ -312,7 +312,7 @@ MN void gain_vq(EncState *E, MelpParam *par)
 }
 
 /* quant_bp :447 */
-MD void quant_bp(EncState *E, MelpParam *par)
+MD void quant_bp(EncAna *E, MelpParam *par)
 {
 	for (int i = 0; i < NF; i++) {
 		par[i].uv_flag = q_bpvc(par[i].bpvc, &E->qpar.bpvc_index[i], NUM_BANDS);
@@ -571,7 +571,7 @@ MD Word16 lsf_uvc(const MelpParam *par)
 }
 
 /* lsf_vq :895, on the voicing pattern uvc (lsf_uvc of the flags it sees) */
-MN void lsf_vq_u(EncState *E, MelpParam *par, Word16 uvc)
+MN void lsf_vq_u(EncAna *E, MelpParam *par, Word16 uvc)
 {
 	PROF_SCOPE(9);
 	QuantParam *q = &E->qpar;
@@ -751,13 +751,13 @@ MN void lsf_vq_u(EncState *E, MelpParam *par, Word16 uvc)
 #undef lsp
 }
 
-MN void lsf_vq(EncState *E, MelpParam *par)
+MN void lsf_vq(EncAna *E, MelpParam *par)
 {
 	lsf_vq_u(E, par, lsf_uvc(par));
 }
 
 /* quant_jitter :1198 */
-MN void quant_jitter(EncState *E, MelpParam *par)
+MN void quant_jitter(EncAna *E, MelpParam *par)
 {
 	Word16 uvc = 0;
 	int16_t jit[NF];
@@ -800,7 +800,7 @@ MN void quant_jitter(EncState *E, MelpParam *par)
 }
 
 /* quant_fsmag :1277 */
-MN void quant_fsmag(EncState *E, MelpParam *par)
+MN void quant_fsmag(EncAna *E, MelpParam *par)
 {
 	PROF_SCOPE(13);
 	int16_t qmag[NUM_HARM];
@@ -936,7 +936,7 @@ MD Word16 parity(Word16 x, int len)	/* melp_chn.c:1367 */
 }
 
 /* low_rate_chn_write :262 -- 81-bit superframe into chbuf (11 bytes) */
-MN void low_rate_chn_write(EncState *E)
+MN void low_rate_chn_write(EncAna *E)
 {
 	PROF_SCOPE(14);
 	QuantParam *q = &E->qpar;

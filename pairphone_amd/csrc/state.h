@@ -116,20 +116,29 @@ struct alignas(4) BandState {
 	int16_t env[ENV_ORD], env2;	/* envdel[b], envdel2[b] */
 };
 
-struct EncState {
-	NppState npp;
+/* The analysis state of one channel: everything analysis() reads or writes.
+ * The lane kernels hold a private copy of this part only (not the NPP
+ * state), and move just its live prefix, [0, ENC_ANA_LIVE): the other
+ * chains' groups, the driver group and the carried speech history
+ * hpspeech[0, IN_BEG).  What follows it -- the superframe's new samples
+ * hpspeech[IN_BEG, IN_BEG + BLOCK) (dc_rmv writes each frame's before
+ * melp_ana reads it) and sigbuf (each stage that uses it writes the part it
+ * reads first) -- is per-superframe working storage, never read before it
+ * is written; the host build (emu_encode_ana_split) fills it with a pattern
+ * to check exactly that. */
+struct alignas(16) EncAna {
+	/* ---- the other chains' groups (ana_mw.h) ---- */
+	ClsState cls;
+	PautoState pa;
+	BandState band[NUM_BANDS];	/* band[0] belongs to the driver group */
 	/* ---- driver group ---- */
-	/* melpe/global.c.  The analysis part of the record starts on a 16-byte
-	 * boundary (and the record is a multiple of 16 bytes), so the lane
-	 * kernels move it with 16-byte loads and stores (kern.h lane_copy_x4) */
-	alignas(16) int16_t hpspeech[IN_BEG + BLOCK];
+	/* melpe/global.c */
 	int16_t dcdelin[DC_ORD], dcdelout_hi[DC_ORD], dcdelout_lo[DC_ORD];
 	MelpParam par[NF];
 	QuantParam qpar;
 	int16_t voicedEn, silenceEn;
 	int32_t voicedCnt;
 	/* melpe/melp_ana.c */
-	int16_t sigbuf[SIG_LENGTH];
 	ClassParam classStat[TRACK_NUM];
 	PitTrack pitTrack[TRACK_NUM];
 	int16_t ana_started;
@@ -156,16 +165,30 @@ struct EncState {
 	int16_t top_lpc[LPC_ORD];
 	int16_t qg_prev_gain;
 	int16_t pad24_;
-	/* ---- the other chains' groups ---- */
-	ClsState cls;
-	PautoState pa;
-	BandState band[NUM_BANDS];	/* band[0] belongs to the driver group */
-	uint32_t fmt_pad_[2];	/* the tag in the record's last 4 bytes (16-byte size) */
+	/* melpe/global.c speech history: [0, IN_BEG) carried, the rest the new
+	 * superframe (working storage, see above); on a 16-byte boundary, so
+	 * the live prefix ends on one (IN_BEG int16 = 45 x 16 bytes) */
+	alignas(16) int16_t hpspeech[IN_BEG + BLOCK];
+	/* melpe/melp_ana.c sigbuf: working storage */
+	int16_t sigbuf[SIG_LENGTH];
+};
+
+/* the first byte of the driver group, the end of the live prefix */
+#define ENC_DRV_BEG offsetof(EncAna, dcdelin)
+#define ENC_ANA_LIVE (offsetof(EncAna, hpspeech) + sizeof(int16_t) * IN_BEG)
+static_assert(ENC_ANA_LIVE % 16 == 0 && sizeof(EncAna) % 16 == 0,
+	      "the lane kernels move the live prefix in 16-byte pieces (kern.h lane_copy_x4)");
+
+struct EncState {
+	NppState npp;
+	EncAna a;	/* 16-byte aligned */
+	uint32_t fmt_pad_[3];	/* the tag in the record's last 4 bytes (16-byte size) */
 	/* record format tag (reset sets it, no kernel writes it):
 	 * melpe_engine_import rejects records of another layout */
 	uint32_t fmt;
 };
 static_assert(offsetof(EncState, fmt) + 4 == sizeof(EncState), "EncState's tag ends the record");
+static_assert(offsetof(EncState, a) % 16 == 0 && sizeof(EncState) % 16 == 0, "16-byte record copies");
 
 #define MIX_ORD 32
 #define DISP_ORD 64
@@ -204,12 +227,12 @@ static_assert(offsetof(DecState, fmt) + 4 == sizeof(DecState), "DecState's tag e
 
 /* Layout version of the records (bump on any change to EncState /
  * DecState); the tag also folds in the record size. */
-#define MELPE_REC_LAYOUT 4u
+#define MELPE_REC_LAYOUT 5u
 #define ENC_REC_FMT (0x4d450000u ^ (MELPE_REC_LAYOUT << 24) ^ (uint32_t) sizeof(EncState))
 #define DEC_REC_FMT (0x4d440000u ^ (MELPE_REC_LAYOUT << 24) ^ (uint32_t) sizeof(DecState))
 
 /* melp_ana_init, melpe/melp_ana.c:475-506 (the part melpe_i re-runs) */
-MD void enc_melpe_i(EncState *e)
+MD void enc_melpe_i(EncAna *e)
 {
 	for (int i = 0; i < IN_BEG + BLOCK; i++)
 		e->hpspeech[i] = 0;
@@ -234,13 +257,14 @@ MD void enc_reset(EncState *e)
 	for (unsigned i = 0; i < sizeof(EncState) / 2; i++)
 		p[i] = 0;
 	npp_reset(&e->npp);
-	e->sc_prev_uv = UNVOICED;	/* melp_ana.c:525-527 */
-	e->sc_prev_pitch = 6400;
-	e->pvq_prev_uv_flag = 1;	/* qnt12.c:78-80 */
-	e->pvq_prev_pitch = LOG_UV_PITCH_Q12;
-	e->pvq_prev_qpitch = LOG_UV_PITCH_Q12;
-	e->fsm_prev_uv = 1;	/* qnt12.c:1279 */
-	enc_melpe_i(e);
+	EncAna *a = &e->a;
+	a->sc_prev_uv = UNVOICED;	/* melp_ana.c:525-527 */
+	a->sc_prev_pitch = 6400;
+	a->pvq_prev_uv_flag = 1;	/* qnt12.c:78-80 */
+	a->pvq_prev_pitch = LOG_UV_PITCH_Q12;
+	a->pvq_prev_qpitch = LOG_UV_PITCH_Q12;
+	a->fsm_prev_uv = 1;	/* qnt12.c:1279 */
+	enc_melpe_i(a);
 	e->fmt = ENC_REC_FMT;
 }
 
