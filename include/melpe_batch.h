@@ -95,11 +95,18 @@ int melpe_engine_set_ana_waves(melpe_engine *e, int waves);
 /* The live-count mapping of the automatic choice above 32,768 channels: a
  * superframe with at most live_max live channels (ragged streams, paused
  * channels) runs the four-wave analysis, more run one lane per channel.
- * The count comes from the lane-order sort on the device, so it needs the
- * lane order on (the default); the host never waits for it.  live_max is
- * 0 .. 32,768 (default 32,768; 0 = by channel count only).  Bits are the
+ * The choice is made on the device, per launch: both mappings are enqueued,
+ * each gated on the live count the lane-order sort counted there (so it
+ * needs the lane order on, the default), and the host never reads the
+ * count.  live_max >= 0 (default 32,768, where the four-wave kernel holds
+ * every live channel resident; 0 = by channel count only).  Bits are the
  * same either way. */
 int melpe_engine_set_mw_live_max(melpe_engine *e, int live_max);
+
+/* The mapping the engine's last analysis launch ran, as the device recorded
+ * it: 1 = one lane per channel, 4 = four waves per 64 channels, 0 = none
+ * (no live channel).  Waits for the engine's enqueued calls. */
+int melpe_engine_last_ana_waves(melpe_engine *e);
 
 /* Per-channel state records, for checkpoint / resume and for moving channels
  * between engines or GPUs (e.g. re-balancing ragged streams).  which: 1 =

@@ -41,6 +41,7 @@ def load_library(path=None):
         "melpe_engine_set_lane_order": (i32, [vp, i32]),
         "melpe_engine_set_ana_waves": (i32, [vp, i32]),
         "melpe_engine_set_mw_live_max": (i32, [vp, i32]),
+        "melpe_engine_last_ana_waves": (i32, [vp]),
         "melpe_engine_state_bytes": (ctypes.c_long, [i32]),
         "melpe_engine_export": (i32, [vp, i32, i32, i32, vp]),
         "melpe_engine_import": (i32, [vp, i32, i32, i32, vp]),
@@ -233,6 +234,13 @@ class MelpeEngine:
         channels run the four-wave analysis (0 = off; results are the same
         either way)"""
         _check(self.lib.melpe_engine_set_mw_live_max(self.h, int(live_max)))
+
+    def last_ana_waves(self):
+        """the mapping the last analysis launch ran, recorded on the device:
+        1 lane per channel, 4 four waves per 64 channels, 0 none"""
+        r = self.lib.melpe_engine_last_ana_waves(self.h)
+        _check(r if r < 0 else 0)
+        return r
 
     def reset_dev(self, d_mask=None, which=3, stream=None):
         """reset enqueued on `stream` (ordered with the *_dev calls on it)"""

@@ -70,13 +70,13 @@ int kl_npp(EncState *enc, int16_t *sp, int frames, int stride, const uint8_t *ac
 	   int rate1200, hipStream_t s);
 int kl_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active, int n, hipStream_t s);
 int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
-	       const int *perm, const int *nlive, int16_t *res, hipStream_t s);
+	       const int *perm, const int *nlive, int16_t *res, AnaGate gate, hipStream_t s);
 int kl_enc_harm(EncState *enc, const int16_t *res, const uint8_t *active, int n, const int *perm,
-		const int *nlive, hipStream_t s);
+		const int *nlive, AnaGate gate, hipStream_t s);
 int kl_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active, int n, const int *perm,
-		const int *nlive, hipStream_t s);
+		const int *nlive, AnaGate gate, hipStream_t s);
 int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active, int n,
-		  const int *perm, const int *nlive, int nw, uint32_t *lqbuf, hipStream_t s);
+		  const int *perm, const int *nlive, int nw, uint32_t *lqbuf, AnaGate gate, hipStream_t s);
 size_t kl_enc_ana_mw_lq_words(int n);
 int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto, hipStream_t s);
 int kl_npp_warm(int n, hipStream_t s);
@@ -265,7 +265,53 @@ __global__ __launch_bounds__(WAVE) void k_modulate_state(ModemState *st, const u
 /* Demodulate (modem.h, modem/modem.c:186): one lane per channel, `calls`
  * successive calls as rx.c:294-297 makes them (pos advances by the return
  * value, data persists); a call that would read past the channel's stride
- * returns -1 and stops the channel */
+ * returns -1 and stops the channel.
+ *
+ * Each lane reads its own row, so a direct read of the stream is a 2-byte
+ * load whose 64 lanes touch 64 different rows -- ~1,900 of them per call.
+ * Instead the samples of up to DEMOD_CALLS calls are staged once into the
+ * lane's private segment with 16-byte loads, and the calls read them from
+ * there, where the hardware interleaves the 64 lanes' copies per dword: the
+ * same-index reads of a wave are one contiguous 256-byte access. */
+#define DEMOD_CALLS 15	/* calls per staged window (one packet time) */
+#define DEMOD_ADV_MAX (MODEM_BLOCK_SAMPLES + 8)	/* a call's largest return (q <= 8) */
+#define DEMOD_WIN (((DEMOD_CALLS - 1) * DEMOD_ADV_MAX + MODEM_LOOKAHEAD + 8 + 7) & ~7)
+
+struct DemodLane {
+	uint8_t guard[FLAT_GUARD_BYTES];
+	ModemState S;
+	alignas(16) int16_t w[DEMOD_WIN];
+};
+
+/* w[sh + i] = src[i], i < n, where sh = the samples before src in its
+ * 16-byte line: whole lines by dwordx4 (each starts at or after the line
+ * that holds src[0], and ends at or before src[n]), the last partial line
+ * sample by sample, so nothing past src[n - 1] is read */
+__device__ __forceinline__ int demod_stage(int16_t *w, const int16_t *src, int n)
+{
+	const int sh = (int) (((uintptr_t) src & 15) >> 1);
+	/* pointer arithmetic on src (not an integer cast) keeps the global
+	 * address space, so these are global_ loads, not FLAT */
+	const v4u32 *g = (const v4u32 *) (src - sh);
+	v4u32 *d = (v4u32 *) w;
+	const int full = (sh + n) >> 3;
+	int k = 0;
+	for (; k + 8 <= full; k += 8) {	/* eight loads in flight, then the stores */
+		v4u32 t[8];
+#pragma unroll
+		for (int j = 0; j < 8; j++)
+			t[j] = g[k + j];
+#pragma unroll
+		for (int j = 0; j < 8; j++)
+			d[k + j] = t[j];
+	}
+	for (; k < full; k++)
+		d[k] = g[k];
+	for (int i = full * 8 - sh; i < n; i++)
+		w[sh + i] = src[i];
+	return sh;
+}
+
 __global__ __launch_bounds__(WAVE) void k_demodulate(ModemState *st, const int16_t *pcm, long stride,
 						     int32_t *pos, uint8_t *data, uint8_t *out,
 						     int32_t *ret, int channels, int calls,
@@ -274,27 +320,42 @@ __global__ __launch_bounds__(WAVE) void k_demodulate(ModemState *st, const int16
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (c >= channels || (active && !active[c]))
 		return;
-	ModemState S = st[c];
+	DemodLane L;
+	PIN_FRAME(L);
+	L.S = st[c];
 	uint8_t d[12];
 	for (int i = 0; i < 12; i++)
 		d[i] = data[12L * c + i];
 	int32_t p = pos[c];
 	const int16_t *x = pcm + (long) c * stride;
-	for (int k = 0; k < calls; k++) {
-		int32_t r = -1;
+	int32_t r = 0;
+	for (int k0 = 0; k0 < calls && r >= 0; k0 += DEMOD_CALLS) {
+		const int nk = calls - k0 < DEMOD_CALLS ? calls - k0 : DEMOD_CALLS;
+		/* the window: from p, the lookahead of the chunk's last call at
+		 * the largest advance per call, never past the row */
+		long base = 0;
 		if (p >= 0 && p + MODEM_LOOKAHEAD <= stride) {
-			r = modem_demod(&S, x + p, d);
-			p += r;
+			long end = (long) p + (long) (nk - 1) * DEMOD_ADV_MAX + MODEM_LOOKAHEAD;
+			if (end > stride)
+				end = stride;
+			base = p - demod_stage(L.w, x + p, (int) (end - p));
 		}
-		if (out)
-			for (int i = 0; i < 12; i++)
-				out[((long) c * calls + k) * 12 + i] = d[i];
-		if (ret)
-			ret[(long) c * calls + k] = r;
-		if (r < 0)
-			break;
+		for (int k = k0; k < k0 + nk; k++) {
+			r = -1;
+			if (p >= 0 && p + MODEM_LOOKAHEAD <= stride) {
+				r = modem_demod(&L.S, L.w + (p - base), d);
+				p += r;
+			}
+			if (out)
+				for (int i = 0; i < 12; i++)
+					out[((long) c * calls + k) * 12 + i] = d[i];
+			if (ret)
+				ret[(long) c * calls + k] = r;
+			if (r < 0)
+				break;
+		}
 	}
-	st[c] = S;
+	st[c] = L.S;
 	pos[c] = p;
 	for (int i = 0; i < 12; i++)
 		data[12L * c + i] = d[i];
@@ -447,7 +508,8 @@ struct BinBuf {
 	int *perm = nullptr;	/* [C] lane -> channel */
 	uint8_t *key = nullptr;	/* [C] class of each channel (0xff: not live) */
 	/* [0, NBIN) counts, [NBIN, 2 NBIN) next slot of each class, [2 NBIN]
-	 * the live count */
+	 * the live count, [2 NBIN + 1] the mapping the last analysis launch ran
+	 * (AnaGate tag: 1 lane, 4 four-wave; 0 none yet) */
 	unsigned *ctl = nullptr;
 	/* The buffers are one per engine and direction, but *_dev calls may
 	 * come on different streams: the sort of a call waits for the kernel
@@ -459,7 +521,7 @@ struct BinBuf {
 
 static hipError_t bin_alloc(BinBuf *b, int channels)
 {
-	size_t pb = sizeof(int) * (size_t) channels, cb = sizeof(unsigned) * (2 * NBIN + 1);
+	size_t pb = sizeof(int) * (size_t) channels, cb = sizeof(unsigned) * (2 * NBIN + 4);
 	char *p = nullptr;
 	hipError_t er = hipMalloc(&p, pb + cb + (size_t) channels);
 	if (er != hipSuccess)
@@ -472,7 +534,7 @@ static hipError_t bin_alloc(BinBuf *b, int channels)
 	b->perm = (int *) p;
 	b->ctl = (unsigned *) (p + pb);
 	b->key = (uint8_t *) (p + pb + cb);
-	return hipSuccess;
+	return hipMemset(b->ctl, 0, cb);
 }
 
 /* the class of one record, from its last superframe: the voiced frames
@@ -536,6 +598,7 @@ __global__ void k_bin_scan(BinBuf b)
 			acc += b.ctl[k];
 		}
 		b.ctl[2 * NBIN] = acc;
+		b.ctl[2 * NBIN + 1] = 0;	/* the mapping tag: the launch that runs sets it */
 	}
 }
 
@@ -623,6 +686,7 @@ struct melpe_engine {
 	hipStream_t stream = nullptr;	/* the device's engine stream (g_dev_stream), shared */
 	hipEvent_t ev0 = nullptr, ev1 = nullptr;
 	hipEvent_t ev_in = nullptr, ev_out = nullptr;	/* EngineCall's hops to and from the engine stream */
+	hipEvent_t ev_host = nullptr;	/* host_finish: the end of a host call's own work */
 	EncState *d_enc = nullptr;
 	DecState *d_dec = nullptr;
 	synth_state *d_syn = nullptr;
@@ -637,12 +701,6 @@ struct melpe_engine {
 	/* the live-count mapping (ana_launch): a superframe with at most this
 	 * many live channels runs the multi-wave kernel (0: off) */
 	int mw_live_max = MW_MAX_CHANNELS;
-	/* the live count of the latest analysis launch whose readback has
-	 * landed (pinned host word, copied after the lane-order sort) */
-	int *h_live = nullptr;
-	hipEvent_t live_ev = nullptr;
-	bool live_pending = false;
-	int last_live = -1;	/* -1: none seen yet */
 	size_t scratch_need = 0;	/* bytes of scratch the largest launch takes */
 	int16_t *d_res = nullptr;	/* the split lane analysis' windowed residuals (C x NF x LPC_FRAME) */
 	/* one event per stream this engine's *_dev calls have used, recorded
@@ -711,42 +769,39 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 	const int *perm = on ? b.perm : nullptr;
 	const int *nlive = on ? (const int *) (b.ctl + 2 * NBIN) : nullptr;
 	int nw = ana_waves_for(e);
+	AnaGate all;
+	all.tag = (int *) (b.ctl + 2 * NBIN + 1);
 	/* Above MW_MAX_CHANNELS the engine runs the lane kernels -- unless few
-	 * channels are live (ragged streams, BASELINE config 5).  The count is
-	 * on the device (the lane-order sort counted it); the host takes the
-	 * latest one whose readback has landed, typically the previous
-	 * superframe's, so it never waits.  Either mapping gives the same bits
-	 * for any live count (the four-wave kernel grid-strides over every live
-	 * slot), so a stale count only costs speed. */
-	const bool auto_live = nw == 1 && on && e->ana_waves == 0 && ana_nw_env() < 0 &&
-			       e->mw_live_max > 0 && harm_split();
-	if (auto_live && e->live_pending && hipEventQuery(e->live_ev) == hipSuccess) {
-		e->last_live = *e->h_live;
-		e->live_pending = false;
+	 * channels are live (ragged streams, BASELINE config 5).  The live count
+	 * is on the device (the lane-order sort counted it), so the choice is
+	 * made there: both mappings are enqueued, each gated on the count, and
+	 * the one whose range holds it runs (the other's waves leave at once).
+	 * No host readback, so host run-ahead cannot make the choice stale.
+	 * Either mapping gives the same bits (the four-wave kernel grid-strides
+	 * over every live slot). */
+	const bool dual = nw == 1 && on && e->ana_waves == 0 && ana_nw_env() < 0 &&
+			  e->mw_live_max > 0 && harm_split();
+	AnaGate lane = all, mw = all;
+	if (dual) {
+		lane.lo = e->mw_live_max;
+		mw.hi = e->mw_live_max;
 	}
-	if (auto_live && e->last_live >= 0 && e->last_live <= e->mw_live_max)
-		nw = 4;
-	int rc;
-	if (nw == 1 && harm_split()) {
-		/* lane-per-channel analysis up to the Fourier magnitudes, the
-		 * magnitudes with a wave per channel, then the packing (k_harm.hip) */
-		rc = kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, e->d_res, s);
-		if (rc == 0)
-			rc = kl_enc_harm(e->d_enc, e->d_res, d_act, e->channels, perm, nlive, s);
-		if (rc == 0)
-			rc = kl_enc_tail(e->d_enc, d_bits, d_act, e->channels, perm, nlive, s);
-	} else {
-		rc = nw == 1 ? kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nullptr, s)
-			     : kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nw,
-					     e->d_lq, s);
-	}
-	if (rc == 0 && auto_live && !e->live_pending) {
-		/* this launch's live count, for a later launch's choice */
-		er = hipMemcpyAsync(e->h_live, b.ctl + 2 * NBIN, sizeof(int), hipMemcpyDeviceToHost, s);
-		if (er == hipSuccess)
-			er = hipEventRecord(e->live_ev, s);
-		rc = (int) er;
-		e->live_pending = rc == 0;
+	int rc = 0;
+	if (dual || nw == 4)
+		rc = kl_enc_ana_mw(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, 4, e->d_lq, mw, s);
+	if (rc == 0 && nw == 1) {
+		if (harm_split()) {
+			/* lane-per-channel analysis up to the Fourier magnitudes,
+			 * the magnitudes with a wave per channel, then the packing
+			 * (k_harm.hip) */
+			rc = kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, e->d_res, lane, s);
+			if (rc == 0)
+				rc = kl_enc_harm(e->d_enc, e->d_res, d_act, e->channels, perm, nlive, lane, s);
+			if (rc == 0)
+				rc = kl_enc_tail(e->d_enc, d_bits, d_act, e->channels, perm, nlive, lane, s);
+		} else {
+			rc = kl_enc_ana(e->d_enc, d_sp, d_bits, d_act, e->channels, perm, nlive, nullptr, lane, s);
+		}
 	}
 	if (rc == 0 && on)
 		rc = (int) bin_release(b, s);
@@ -860,6 +915,22 @@ static int engine_wait(melpe_engine *e)
 	return 0;
 }
 #define ENGINE_WAIT(e) do { if (int _r = engine_wait(e)) return _r; } while (0)
+/* a host-side call (the *_host calls, reset, export / import, synth_seed)
+ * holds the engine's lock for its whole body: it stages data through the
+ * engine's shared buffers (d_mask, d_pcm, d_bits, d_npp), which another
+ * thread's call on the same engine would otherwise overwrite or reallocate
+ * under it.  (The lock is recursive: ENGINE_WAIT and EngineCall take it
+ * again inside.) */
+#define HOST_LOCK(e) std::lock_guard<std::recursive_mutex> _host_lk((e)->mu)
+/* the host waits for the work this call enqueued on the engine stream (an
+ * event recorded after it), not for work other engines enqueue later */
+static int host_finish(melpe_engine *e)
+{
+	HIPCHK(hipEventRecord(e->ev_host, e->stream));
+	HIPCHK(hipEventSynchronize(e->ev_host));
+	return 0;
+}
+#define HOST_FINISH(e) do { if (int _r = host_finish(e)) return _r; } while (0)
 /* one *_dev call of an engine: holds the engine's lock (the host-side
  * bookkeeping -- marks, the lane-order buffers -- is shared by the calls of
  * every thread) and records the stream's mark when it ends */
@@ -867,6 +938,7 @@ struct EngineCall {
 	melpe_engine *e;
 	hipStream_t user, run;
 	std::lock_guard<std::recursive_mutex> lk;
+	bool finished = false;
 	EngineCall(melpe_engine *e_, hipStream_t s_) : e(e_), user(s_), run(s_), lk(e_->mu)
 	{
 		/* the call's kernels run on the device's engine stream, ordered
@@ -881,8 +953,23 @@ struct EngineCall {
 		    hipStreamWaitEvent(e->stream, e->ev_in, 0) == hipSuccess)
 			run = e->stream;
 	}
+	/* the hop back to the caller's stream and the call's mark; an entry
+	 * point returns its result, so a failed hop (the caller's later work
+	 * would not be ordered after the kernels) is reported */
+	int finish()
+	{
+		finished = true;
+		if (run != user) {
+			HIPCHK(hipEventRecord(e->ev_out, run));
+			HIPCHK(hipStreamWaitEvent(user, e->ev_out, 0));
+		}
+		return engine_mark(e, user);
+	}
+	/* early error returns: the same steps, best effort */
 	~EngineCall()
 	{
+		if (finished)
+			return;
 		if (run != user && hipEventRecord(e->ev_out, run) == hipSuccess)
 			hipStreamWaitEvent(user, e->ev_out, 0);
 		engine_mark(e, user);
@@ -924,9 +1011,6 @@ static int engine_reserve(melpe_engine *e)
 		return fail("melpe_engine_create: multi-wave score rows", er);
 	}
 	const int mw = e->channels < MW_MAX_CHANNELS ? e->channels : MW_MAX_CHANNELS;
-	if ((er = hipHostMalloc((void **) &e->h_live, sizeof(int), hipHostMallocDefault)) != hipSuccess ||
-	    (er = hipEventCreateWithFlags(&e->live_ev, hipEventDisableTiming)) != hipSuccess)
-		return fail("melpe_engine_create: live-count readback", er);
 	/* The runtime keeps a queue's scratch between dispatches only below its
 	 * scratch limit threshold; above it the allocation is made for the
 	 * dispatch and given back.  Raise the threshold (never lower it) to
@@ -985,6 +1069,7 @@ int melpe_engine_create(melpe_engine **out, int device, int channels)
 	CREATE_STEP(hipEventCreate(&e->ev1));
 	CREATE_STEP(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
 	CREATE_STEP(hipEventCreateWithFlags(&e->ev_out, hipEventDisableTiming));
+	CREATE_STEP(hipEventCreateWithFlags(&e->ev_host, hipEventDisableTiming));
 	CREATE_STEP(hipMalloc(&e->d_enc, sizeof(EncState) * (size_t) channels));
 	CREATE_STEP(hipMalloc(&e->d_dec, sizeof(DecState) * (size_t) channels));
 	CREATE_STEP(hipMalloc(&e->d_syn, sizeof(synth_state) * (size_t) channels));
@@ -1022,11 +1107,22 @@ int melpe_engine_set_lane_order(melpe_engine *e, int on)
 
 int melpe_engine_set_mw_live_max(melpe_engine *e, int live_max)
 {
-	if (!e || live_max < 0 || live_max > MW_MAX_CHANNELS)
-		return fail_msg("melpe_engine_set_mw_live_max: 0 .. 32768 live channels");
+	if (!e || live_max < 0)
+		return fail_msg("melpe_engine_set_mw_live_max: a live-channel count >= 0");
 	std::lock_guard<std::recursive_mutex> lk(e->mu);
 	e->mw_live_max = live_max;
 	return 0;
+}
+
+int melpe_engine_last_ana_waves(melpe_engine *e)
+{
+	if (!e)
+		return fail_msg("melpe_engine_last_ana_waves: no engine");
+	DEVGUARD(e->device);
+	ENGINE_WAIT(e);
+	int v = 0;
+	HIPCHK(hipMemcpy(&v, e->bin_enc.ctl + 2 * NBIN + 1, sizeof(int), hipMemcpyDeviceToHost));
+	return v;
 }
 
 int melpe_engine_set_ana_waves(melpe_engine *e, int waves)
@@ -1042,8 +1138,8 @@ int melpe_engine_destroy(melpe_engine *e)
 	if (!e)
 		return 0;
 	DevGuard dg(e->device);
-	if (e->stream)
-		hipStreamSynchronize(e->stream);
+	/* this engine's enqueued calls, not the whole shared stream */
+	engine_wait(e);
 	hipFree(e->d_npp);
 	hipFree(e->d_enc);
 	hipFree(e->d_dec);
@@ -1055,10 +1151,6 @@ int melpe_engine_destroy(melpe_engine *e)
 	hipFree(e->bin_dec.perm);
 	hipFree(e->d_lq);
 	hipFree(e->d_res);
-	if (e->h_live)
-		hipHostFree(e->h_live);
-	if (e->live_ev)
-		hipEventDestroy(e->live_ev);
 	for (auto &m : e->marks)
 		hipEventDestroy(m.second);
 	if (e->bin_enc.done)
@@ -1073,6 +1165,8 @@ int melpe_engine_destroy(melpe_engine *e)
 		hipEventDestroy(e->ev_in);
 	if (e->ev_out)
 		hipEventDestroy(e->ev_out);
+	if (e->ev_host)
+		hipEventDestroy(e->ev_host);
 	delete e;
 	return 0;
 }
@@ -1104,7 +1198,7 @@ int melpe_engine_reset_dev(melpe_engine *e, const void *d_mask, int which, void 
 	k_reset<<<grid_for(e->channels), WAVE, 0, s>>>(
 		e->d_enc, e->d_dec, (const uint8_t *) d_mask, e->channels, which);
 	HIPCHK(hipGetLastError());
-	return 0;
+	return _call.finish();
 }
 
 int melpe_engine_reset(melpe_engine *e, const uint8_t *mask_host, int which)
@@ -1112,6 +1206,7 @@ int melpe_engine_reset(melpe_engine *e, const uint8_t *mask_host, int which)
 	if (!e || which < 1 || which > 3)
 		return fail_msg("melpe_engine_reset: bad arguments");
 	DEVGUARD(e->device);
+	HOST_LOCK(e);
 	/* ordered after every *_dev call of this engine already enqueued, on
 	 * any stream: those read and write the same channel records */
 	ENGINE_WAIT(e);
@@ -1122,7 +1217,7 @@ int melpe_engine_reset(melpe_engine *e, const uint8_t *mask_host, int which)
 	k_reset<<<grid_for(e->channels), WAVE, 0, e->stream>>>(e->d_enc, e->d_dec, m,
 								  e->channels, which);
 	HIPCHK(hipGetLastError());
-	HIPCHK(hipStreamSynchronize(e->stream));
+	HOST_FINISH(e);
 	return 0;
 }
 
@@ -1136,7 +1231,7 @@ static int npp_launch(melpe_engine *e, int16_t *d_sp, int frames, int stride,
 	ev_begin(e, s);
 	HIPCHK((hipError_t) kl_npp(e->d_enc, d_sp, frames, stride, d_act, e->channels, rate1200, s));
 	ev_end(e, s, sync);
-	return 0;
+	return _call.finish();
 }
 
 int melpe_npp_dev(melpe_engine *e, void *d_sp, int frames, int stride, const void *d_active,
@@ -1153,6 +1248,7 @@ int melpe_npp_host(melpe_engine *e, int16_t *sp, int frames, int stride, const u
 	if (!e || !sp || stride <= 0)
 		return fail_msg("melpe_npp_host: bad arguments");
 	DEVGUARD(e->device);
+	HOST_LOCK(e);
 	ENGINE_WAIT(e);
 	size_t bytes = sizeof(int16_t) * (size_t) stride * e->channels;
 	if (e->npp_bytes < bytes) {
@@ -1171,7 +1267,9 @@ int melpe_npp_host(melpe_engine *e, int16_t *sp, int frames, int stride, const u
 		if (!rc) {
 			hipError_t er = hipMemcpyAsync(sp, d, bytes, hipMemcpyDeviceToHost, e->stream);
 			if (er == hipSuccess)
-				er = hipStreamSynchronize(e->stream);
+				er = hipEventRecord(e->ev_host, e->stream);
+				if (er == hipSuccess)
+					er = hipEventSynchronize(e->ev_host);
 			if (er != hipSuccess)
 				rc = fail("npp copy back", er);
 		}
@@ -1188,7 +1286,7 @@ static int encode_launch(melpe_engine *e, unsigned char *d_bits, int16_t *d_sp,
 	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, d_sp, d_act, e->channels, s));
 	HIPCHK((hipError_t) ana_launch(e, d_sp, d_bits, d_act, s));
 	ev_end(e, s, sync);
-	return 0;
+	return _call.finish();
 }
 
 int melpe_encode_dev(melpe_engine *e, void *d_bits, void *d_sp, const void *d_active,
@@ -1209,7 +1307,7 @@ int melpe_encode_npp_dev(melpe_engine *e, void *d_sp, const void *d_active, void
 	ENGINE_CALL(e, s);
 	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, (int16_t *) d_sp, (const uint8_t *) d_active,
 				       e->channels, s));
-	return 0;
+	return _call.finish();
 }
 
 int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const void *d_active,
@@ -1222,7 +1320,7 @@ int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const 
 	ENGINE_CALL(e, s);
 	HIPCHK((hipError_t) ana_launch(e, (const int16_t *) d_sp, (uint8_t *) d_bits,
 				       (const uint8_t *) d_active, s));
-	return 0;
+	return _call.finish();
 }
 
 int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const uint8_t *active)
@@ -1230,6 +1328,7 @@ int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const u
 	if (!e || !bits || !sp)
 		return fail_msg("melpe_encode_host: null argument");
 	DEVGUARD(e->device);
+	HOST_LOCK(e);
 	ENGINE_WAIT(e);
 	size_t pb = sizeof(int16_t) * BLOCK * (size_t) e->channels;
 	size_t bb = (size_t) 11 * e->channels;
@@ -1245,7 +1344,7 @@ int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const u
 		return rc;
 	HIPCHK(hipMemcpyAsync(sp, e->d_pcm, pb, hipMemcpyDeviceToHost, e->stream));
 	HIPCHK(hipMemcpyAsync(bits, e->d_bits, bb, hipMemcpyDeviceToHost, e->stream));
-	HIPCHK(hipStreamSynchronize(e->stream));
+	HOST_FINISH(e);
 	return 0;
 }
 
@@ -1257,7 +1356,7 @@ static int decode_launch(melpe_engine *e, int16_t *d_sp, const unsigned char *d_
 	ev_begin(e, s);
 	HIPCHK((hipError_t) dec_launch(e, d_sp, d_bits, d_act, s));
 	ev_end(e, s, sync);
-	return 0;
+	return _call.finish();
 }
 
 int melpe_decode_dev(melpe_engine *e, void *d_sp, const void *d_bits, const void *d_active,
@@ -1275,6 +1374,7 @@ int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
 	if (!e || !bits || !sp)
 		return fail_msg("melpe_decode_host: null argument");
 	DEVGUARD(e->device);
+	HOST_LOCK(e);
 	ENGINE_WAIT(e);
 	size_t pb = sizeof(int16_t) * BLOCK * (size_t) e->channels;
 	size_t bb = (size_t) 11 * e->channels;
@@ -1289,7 +1389,7 @@ int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
 	if (rc)
 		return rc;
 	HIPCHK(hipMemcpyAsync(sp, e->d_pcm, pb, hipMemcpyDeviceToHost, e->stream));
-	HIPCHK(hipStreamSynchronize(e->stream));
+	HOST_FINISH(e);
 	return 0;
 }
 
@@ -1305,7 +1405,7 @@ static int encode24_launch(melpe_engine *e, unsigned char *d_bits, int16_t *d_sp
 	HIPCHK((hipError_t) kl_npp(e->d_enc, d_sp, 1, MELPE_FRAME_SAMPLES, d_act, e->channels, 0, s));
 	HIPCHK((hipError_t) kl_enc24(e->d_enc, d_sp, d_bits, d_act, e->channels, s));
 	ev_end(e, s, sync);
-	return 0;
+	return _call.finish();
 }
 
 int melpe_encode2400_dev(melpe_engine *e, void *d_bits, void *d_sp, const void *d_active,
@@ -1329,7 +1429,7 @@ int melpe_decode2400_dev(melpe_engine *e, void *d_sp, const void *d_bits, const 
 	HIPCHK((hipError_t) kl_dec24(e->d_dec, (int16_t *) d_sp, (const uint8_t *) d_bits,
 				     (const uint8_t *) d_active, e->channels, s));
 	ev_end(e, s, false);
-	return 0;
+	return _call.finish();
 }
 
 int melpe_encode2400_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const uint8_t *active)
@@ -1337,6 +1437,7 @@ int melpe_encode2400_host(melpe_engine *e, unsigned char *bits, int16_t *sp, con
 	if (!e || !bits || !sp)
 		return fail_msg("melpe_encode2400_host: null argument");
 	DEVGUARD(e->device);
+	HOST_LOCK(e);
 	ENGINE_WAIT(e);
 	size_t pb = sizeof(int16_t) * MELPE_FRAME_SAMPLES * (size_t) e->channels;
 	size_t bb = (size_t) MELPE_R24_BYTES * e->channels;
@@ -1352,7 +1453,7 @@ int melpe_encode2400_host(melpe_engine *e, unsigned char *bits, int16_t *sp, con
 		return rc;
 	HIPCHK(hipMemcpyAsync(sp, e->d_pcm, pb, hipMemcpyDeviceToHost, e->stream));
 	HIPCHK(hipMemcpyAsync(bits, e->d_bits, bb, hipMemcpyDeviceToHost, e->stream));
-	HIPCHK(hipStreamSynchronize(e->stream));
+	HOST_FINISH(e);
 	return 0;
 }
 
@@ -1362,6 +1463,7 @@ int melpe_decode2400_host(melpe_engine *e, int16_t *sp, const unsigned char *bit
 	if (!e || !bits || !sp)
 		return fail_msg("melpe_decode2400_host: null argument");
 	DEVGUARD(e->device);
+	HOST_LOCK(e);
 	ENGINE_WAIT(e);
 	size_t pb = sizeof(int16_t) * MELPE_FRAME_SAMPLES * (size_t) e->channels;
 	size_t bb = (size_t) MELPE_R24_BYTES * e->channels;
@@ -1374,7 +1476,7 @@ int melpe_decode2400_host(melpe_engine *e, int16_t *sp, const unsigned char *bit
 		HIPCHK(hipMemcpyAsync(e->d_pcm, sp, pb, hipMemcpyHostToDevice, e->stream));
 	HIPCHK((hipError_t) kl_dec24(e->d_dec, e->d_pcm, e->d_bits, m, e->channels, e->stream));
 	HIPCHK(hipMemcpyAsync(sp, e->d_pcm, pb, hipMemcpyDeviceToHost, e->stream));
-	HIPCHK(hipStreamSynchronize(e->stream));
+	HOST_FINISH(e);
 	return 0;
 }
 
@@ -1404,6 +1506,7 @@ int melpe_engine_export(melpe_engine *e, int which, int first, int count, void *
 	if (!host_out && count)
 		return fail_msg("melpe_engine_export: null buffer");
 	DEVGUARD(e->device);
+	HOST_LOCK(e);
 	ENGINE_WAIT(e);
 	HIPCHK(hipMemcpy(host_out, base + rec * first, rec * count, hipMemcpyDeviceToHost));
 	return 0;
@@ -1427,6 +1530,7 @@ int melpe_engine_import(melpe_engine *e, int which, int first, int count, const 
 					" is not a state record of this library's layout");
 	}
 	DEVGUARD(e->device);
+	HOST_LOCK(e);
 	ENGINE_WAIT(e);
 	HIPCHK(hipMemcpy(base + rec * first, host_in, rec * count, hipMemcpyHostToDevice));
 	return 0;
@@ -1437,10 +1541,11 @@ int melpe_synth_seed(melpe_engine *e, uint32_t run_seed, uint32_t first_channel)
 	if (!e)
 		return fail_msg("null engine");
 	DEVGUARD(e->device);
+	HOST_LOCK(e);
 	k_synth_seed<<<grid_for(e->channels), WAVE, 0, e->stream>>>(e->d_syn, run_seed,
 								      first_channel, e->channels);
 	HIPCHK(hipGetLastError());
-	HIPCHK(hipStreamSynchronize(e->stream));
+	HOST_FINISH(e);
 	return 0;
 }
 
@@ -1454,7 +1559,7 @@ int melpe_synth_dev(melpe_engine *e, void *d_sp, int samples, void *hip_stream)
 	k_synth<<<grid_for(e->channels), WAVE, 0, s>>>(
 		e->d_syn, (int16_t *) d_sp, samples, e->channels);
 	HIPCHK(hipGetLastError());
-	return 0;
+	return _call.finish();
 }
 
 int melpe_synth_host(uint32_t run_seed, uint32_t channel, int16_t *out, int samples)

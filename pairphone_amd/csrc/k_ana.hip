@@ -24,17 +24,25 @@ struct AnaLane {
 template <int MODE>
 __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits,
 						  const uint8_t *active, int n, const int *perm,
-						  const int *nlive, int16_t *res)
+						  const int *nlive, int16_t *res, AnaGate gate)
 {
 	/* lane g runs channel perm[g] when the engine ordered the live channels
-	 * by pitch class (engine.hip, MELPE_BIN), else channel g under the mask */
+	 * by pitch class (engine.hip, MELPE_BIN), else channel g under the mask;
+	 * the whole launch stands down unless the live count is the gate's
+	 * (engine.hip ana_launch enqueues this and the four-wave kernel) */
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (perm) {
-		if (c >= *nlive)
+		const int L = *nlive;
+		if (!gate.open(L))
+			return;
+		gate.mark(c == 0, 1);
+		if (c >= L)
 			return;
 		c = perm[c];
-	} else if (c >= n || (active && !active[c])) {
-		return;
+	} else {
+		gate.mark(c == 0, 1);
+		if (c >= n || (active && !active[c]))
+			return;
 	}
 	AnaLane L;
 	PIN_FRAME(L);
@@ -79,12 +87,14 @@ static unsigned ana_lds_bytes(void)
 }
 
 extern "C" int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
-			  int n, const int *perm, const int *nlive, int16_t *res, hipStream_t s)
+			  int n, const int *perm, const int *nlive, int16_t *res, AnaGate gate, hipStream_t s)
 {
 	if (res)
-		k_enc_ana<1><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res);
+		k_enc_ana<1><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res,
+									 gate);
 	else
-		k_enc_ana<0><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res);
+		k_enc_ana<0><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res,
+									 gate);
 	return (int) hipGetLastError();
 }
 
@@ -106,6 +116,7 @@ extern "C" size_t kl_ana_private(void)
 
 extern "C" int kl_ana_warm(int n, hipStream_t s)
 {
-	k_enc_ana<1><<<grid_for(n), WAVE, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
+	k_enc_ana<1><<<grid_for(n), WAVE, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+						 AnaGate{});
 	return (int) hipGetLastError();
 }

@@ -72,7 +72,7 @@ template <int NW>
 __global__ __launch_bounds__(WAVE * NW, MELPE_MW_WAVES) void k_enc_ana_mw(EncState *enc, const int16_t *sp,
 									    uint8_t *bits, const uint8_t *active,
 									    int n, const int *perm, const int *nlive,
-									    uint32_t *lqbuf)
+									    uint32_t *lqbuf, AnaGate gate)
 {
 	__shared__ int16_t xs[XS_WORDS * WAVE];
 	const int w = threadIdx.x / WAVE, t = threadIdx.x % WAVE;
@@ -81,6 +81,11 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_MW_WAVES) void k_enc_ana_mw(EncSta
 	 * however many there are (engine.hip ana_launch picks this kernel from
 	 * a live count that may be a superframe old) */
 	const int count = perm ? *nlive : n;
+	/* the engine enqueues this and the lane kernels, each gated on the
+	 * live count: uniform per launch, so every wave leaves before a barrier */
+	if (perm && !gate.open(count))
+		return;
+	gate.mark(blockIdx.x == 0 && threadIdx.x == 0, NW);
 	for (int grp = blockIdx.x; grp * WAVE < count; grp += gridDim.x) {
 	int c = grp * WAVE + t;
 	bool live;
@@ -157,12 +162,13 @@ extern "C" size_t kl_enc_ana_mw_lq_words(int n)
 
 extern "C" int kl_enc_ana_mw(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
 			     int n, const int *perm, const int *nlive, int nw, uint32_t *lqbuf,
-			     hipStream_t s)
+			     AnaGate gate, hipStream_t s)
 {
 	/* 4 waves per 64 channels (2 measured no better at any channel count
 	 * and cost a third more compile time; ana_mw.h supports any count) */
 	if (nw == 4)
-		k_enc_ana_mw<4><<<mw_grid(n), WAVE * 4, 0, s>>>(enc, sp, bits, active, n, perm, nlive, lqbuf);
+		k_enc_ana_mw<4><<<mw_grid(n), WAVE * 4, 0, s>>>(enc, sp, bits, active, n, perm, nlive, lqbuf,
+								gate);
 	else
 		return (int) hipErrorInvalidValue;
 	return (int) hipGetLastError();
@@ -177,6 +183,6 @@ extern "C" size_t kl_ana_mw_private(void)
 extern "C" int kl_ana_mw_warm(int n, hipStream_t s)
 {
 	k_enc_ana_mw<4><<<mw_grid(n), WAVE * 4, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr,
-							nullptr);
+							nullptr, AnaGate{});
 	return (int) hipGetLastError();
 }

@@ -142,11 +142,12 @@ MD void wv_find_harm(const int16_t v[4], int16_t *fsmag, Word16 pitch, uint32_t 
  * lane order) or channel g under the mask; the three frames in order */
 __global__ __launch_bounds__(WAVE) void k_enc_harm(EncState *enc, const int16_t *res,
 						   const uint8_t *active, int n, const int *perm,
-						   const int *nlive)
+						   const int *nlive, AnaGate gate)
 {
 	int c = blockIdx.x;
 	if (perm) {
-		if (c >= *nlive)
+		const int L = *nlive;
+		if (!gate.open(L) || c >= L)
 			return;
 		c = perm[c];
 	} else if (c >= n || (active && !active[c])) {
@@ -176,9 +177,9 @@ __global__ __launch_bounds__(WAVE) void k_enc_harm(EncState *enc, const int16_t 
 }
 
 extern "C" int kl_enc_harm(EncState *enc, const int16_t *res, const uint8_t *active, int n,
-			   const int *perm, const int *nlive, hipStream_t s)
+			   const int *perm, const int *nlive, AnaGate gate, hipStream_t s)
 {
-	k_enc_harm<<<n, WAVE, 0, s>>>(enc, res, active, n, perm, nlive);
+	k_enc_harm<<<n, WAVE, 0, s>>>(enc, res, active, n, perm, nlive, gate);
 	return (int) hipGetLastError();
 }
 
@@ -190,11 +191,12 @@ struct TailLane {
 };
 
 __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active,
-						   int n, const int *perm, const int *nlive)
+						   int n, const int *perm, const int *nlive, AnaGate gate)
 {
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (perm) {
-		if (c >= *nlive)
+		const int L = *nlive;
+		if (!gate.open(L) || c >= L)
 			return;
 		c = perm[c];
 	} else if (c >= n || (active && !active[c])) {
@@ -219,9 +221,9 @@ __global__ __launch_bounds__(WAVE, 4) void k_enc_tail(EncState *enc, uint8_t *bi
 }
 
 extern "C" int kl_enc_tail(EncState *enc, uint8_t *bits, const uint8_t *active, int n,
-			   const int *perm, const int *nlive, hipStream_t s)
+			   const int *perm, const int *nlive, AnaGate gate, hipStream_t s)
 {
-	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(enc, bits, active, n, perm, nlive);
+	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(enc, bits, active, n, perm, nlive, gate);
 	return (int) hipGetLastError();
 }
 
@@ -233,7 +235,7 @@ extern "C" size_t kl_harm_private(void)
 
 extern "C" int kl_harm_warm(int n, hipStream_t s)
 {
-	k_enc_harm<<<n, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr);
-	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr);
+	k_enc_harm<<<n, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr, AnaGate{});
+	k_enc_tail<<<grid_for(n), WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr, AnaGate{});
 	return (int) hipGetLastError();
 }

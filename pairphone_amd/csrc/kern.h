@@ -127,6 +127,22 @@ __device__ __forceinline__ void lane_copy_x4(void *dst, const void *src, size_t 
 	}
 #endif
 
+/* The device-side choice of analysis mapping (engine.hip ana_launch): a
+ * launch works only when the live count L its lane-order sort counted lies
+ * in (lo, hi], and the launch that works writes its mapping (waves per 64
+ * channels: 1 lane, 4 four-wave) into *tag.  The default is always open and
+ * writes nothing. */
+struct AnaGate {
+	int lo = -1, hi = 0x7fffffff;
+	int *tag = nullptr;
+	__device__ bool open(int L) const { return L > lo && L <= hi; }
+	__device__ void mark(bool leader, int waves) const
+	{
+		if (tag && leader)
+			*tag = waves;
+	}
+};
+
 static inline unsigned grid_for(int n)
 {
 	return (unsigned) ((n + WAVE - 1) / WAVE);

@@ -33,6 +33,9 @@
 #define MODEM_FN static inline
 #endif
 
+/* dword view of int16 sample rows (aliases them) */
+typedef uint32_t modem_u32a __attribute__((__may_alias__));
+
 #define MODEM_BITS 90
 #define MODEM_PKT_SAMPLES 3240	/* 90 bits x 36 samples at 48 kHz */
 #define MODEM_BLOCK_SAMPLES 216	/* one Demodulate call: 6 bits */
@@ -139,21 +142,41 @@ MODEM_FN int modem_demod(ModemState *S, const int16_t *frame, uint8_t *data)
 #endif
 	const int16_t *sp = frame + 9;
 	int q = 0;
-	/* carrier phase: |x[k] - x[k+18]| summed over 24 periods per offset */
+	/* carrier phase: |x[k] - x[k+18]| summed over 24 periods per offset.
+	 * Integer sums, so the order is free: period by period, the period's
+	 * 54 samples read as 27 sample pairs (dword loads from the even sample
+	 * at or below sp, realigned by one sample when sp is odd), the 36
+	 * offsets' sums kept in registers. */
 	{
-		int best = 0;
-		for (int j = 0; j < 36; j++) {
-			int e = 0;
-			for (int i = 0; i < 24; i++) {
-				int k = i * 36 + j;
-				int d = sp[k] - sp[k + 18];
-				e += d < 0 ? -d : d;
+		int e[36];
+		for (int j = 0; j < 36; j++)
+			e[j] = 0;
+		const int odd = (int) (((uintptr_t) sp >> 1) & 1);
+		/* the even sample at or below sp: 4-byte aligned (int16 rows) */
+		const modem_u32a *bw = (const modem_u32a *) (sp - odd);
+		for (int i = 0; i < 24; i++) {
+			uint32_t dw[28], v[27];
+			for (int t = 0; t < 28; t++) {
+				/* the 28th dword (odd starts only) is within the
+				 * window: sp[881] is the last sample read below */
+				dw[t] = (t < 27 || odd) ? bw[18 * i + t] : 0u;
 			}
-			if (e > best) {
-				best = e;
-				q = j;
+			for (int t = 0; t < 27; t++)
+				v[t] = odd ? (dw[t] >> 16) | (dw[t + 1] << 16) : dw[t];
+			for (int j = 0; j < 36; j++) {
+				const uint32_t a = v[j >> 1], c = v[(j + 18) >> 1];
+				const int x0 = (int16_t) ((j & 1) ? a >> 16 : a);
+				const int x1 = (int16_t) ((j & 1) ? c >> 16 : c);
+				const int d = x0 - x1;
+				e[j] += d < 0 ? -d : d;
 			}
 		}
+		int best = 0;
+		for (int j = 0; j < 36; j++)
+			if (e[j] > best) {
+				best = e[j];
+				q = j;
+			}
 	}
 	S->f180 = fmul_d(S->f180, 0.9);
 	if (q > 17) {

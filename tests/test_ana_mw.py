@@ -192,9 +192,11 @@ def test_mw_gpu_mapping_alternates_between_superframes():
     assert not bad, "bitstream mismatch on %d channels, first %s" % (len(bad), bad[:8])
 
 
-def _gpu_encode_masked(C, masks, live_max, waves, seed):
+def _gpu_encode_masked(C, masks, live_max, waves, seed, choice=None):
     """C channels under per-superframe activity masks [nsf, C]; returns bits
-    [nsf, C, 11] (0xAB where a channel was inactive)"""
+    [nsf, C, 11] (0xAB where a channel was inactive); `choice`, a list,
+    receives the mapping each superframe's analysis ran (the device's
+    record, after each superframe)"""
     import torch
     from pairphone_amd import MelpeEngine
     dev = torch.device("cuda", 0)
@@ -210,6 +212,8 @@ def _gpu_encode_masked(C, masks, live_max, waves, seed):
     for k in range(nsf):
         eng.synth_dev(pcm.data_ptr(), 540, s)
         eng.encode_dev(bits[k].data_ptr(), pcm.data_ptr(), m[k].data_ptr(), s)
+        if choice is not None:
+            choice.append(eng.last_ana_waves())
     torch.cuda.synchronize(dev)
     eng.close()
     return bits.cpu().numpy()
@@ -221,15 +225,18 @@ def test_mw_gpu_live_count_pick_ragged():
     ragged masks whose live count crosses 32,768 both ways: with the
     live-count pick on (the default) every superframe with <= 32,768 live
     channels runs k_enc_ana_mw, the others the lane kernels, decided on the
-    device.  Every channel's bits equal the lane kernels' alone (pick off)
-    and the four-wave kernel's alone."""
+    device (both enqueued, each gated on the sort's live count; the device
+    records which ran).  Every channel's bits equal the lane kernels' alone
+    (pick off) and the four-wave kernel's alone."""
     C, nsf = 65536, 10
     rng = np.random.default_rng(12)
     live = [60000, 20000, 32768, 32769, 1000, 45000, 30000, 64, 65536, 16000]
     masks = np.zeros((nsf, C), bool)
     for k, n in enumerate(live):
         masks[k, rng.choice(C, n, replace=False)] = True
-    got = _gpu_encode_masked(C, masks, 32768, 0, 5)
+    choice = []
+    got = _gpu_encode_masked(C, masks, 32768, 0, 5, choice)
+    assert choice == [4 if n <= 32768 else 1 for n in live], choice
     lane = _gpu_encode_masked(C, masks, 0, 0, 5)
     np.testing.assert_array_equal(got, lane)
     mw = _gpu_encode_masked(C, masks, 0, 4, 5)

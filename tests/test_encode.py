@@ -115,6 +115,51 @@ def test_encode_gpu_1024_channels_match_golden():
     assert not badn, "NPP output mismatch on %d channels, first %s" % (len(badn), badn[:8])
 
 
+@pytest.mark.gpu
+def test_encode_host_two_threads_one_engine():
+    """Two host threads calling melpe_encode_host on one engine at once,
+    each on its own half of the channels (disjoint masks): every call holds
+    the engine's lock while it stages PCM, mask and bits through the
+    engine's shared buffers, so each thread gets exactly the bits and NPP
+    output of one engine running all channels alone (ctypes releases the
+    GIL during the calls, so the calls do overlap)."""
+    import threading
+    from pairphone_amd import MelpeEngine
+    g = golden()
+    C, nsf = g["channels"], 40
+    x = signals(g["seed"], C, nsf)
+    eng = MelpeEngine(C)
+    halves = [np.arange(C) % 2 == h for h in (0, 1)]
+    out = [None, None]
+    err = []
+
+    def worker(h):
+        try:
+            xs = x.copy()
+            bits = np.zeros((C, nsf * 11), np.uint8)
+            for k in range(nsf):
+                sp = np.ascontiguousarray(xs[:, k * 540:(k + 1) * 540])
+                bits[:, k * 11:(k + 1) * 11] = eng.encode(sp, active=halves[h])
+                xs[:, k * 540:(k + 1) * 540] = sp
+            out[h] = (bits, xs)
+        except Exception as e:  # noqa: BLE001
+            err.append(e)
+    th = [threading.Thread(target=worker, args=(h,)) for h in (0, 1)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    eng.close()
+    assert not err, err
+    ref = MelpeEngine(C)
+    want, wnpp = run_superframes(ref.encode, x.copy(), nsf)
+    ref.close()
+    for h in (0, 1):
+        bits, npp = out[h]
+        np.testing.assert_array_equal(bits[halves[h]], want[halves[h]])
+        np.testing.assert_array_equal(npp[halves[h]], wnpp[halves[h]])
+
+
 def edge_signals(n):
     rng = np.random.default_rng(5)
     t = np.arange(n)
