@@ -95,6 +95,8 @@ def parse(argv=None):
                     help="config 5 TX front end leg, channels per GPU (0 = skip)")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-side-legs", action="store_true", help="skip crypt and VAD legs")
+    ap.add_argument("--no-host-leg", action="store_true",
+                    help="skip the host-fed (pinned host buffers, PCIe-inclusive) encode leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-channels", type=int, default=128)
     ap.add_argument("--cpu-jobs", type=int, default=0,
@@ -371,6 +373,53 @@ def encode_leg(rig, wl, K, W):
     return timed(rig, [wl.npp, wl.ana], K, W)
 
 
+def host_leg(rig, C, first, K, W, dev_bits, world):
+    """The host-fed form of the headline (melpe/melpe.c:91-99's contract:
+    the caller hands host buffers): the same channels and synthetic input,
+    in pinned host memory, through melpe_encode_host_async -- per superframe
+    the PCM over PCIe to the device, melpe_a, the NPP output (in place, as
+    melpe_a) and the bits back, double-buffered so the copies of superframes
+    k - 1 and k + 1 overlap the kernels of k.  A fresh engine, so its bits
+    must equal the device-resident run's bit for bit."""
+    import torch
+    from pairphone_amd import MelpeEngine
+    eng = MelpeEngine(C, device=rig.dev.index)
+    eng.synth_seed(RUN_SEED, first_channel=first)
+    tmp = torch.empty((C, SF_SAMPLES), dtype=torch.int16, device=rig.dev)
+    t0 = time.perf_counter()
+    pcm_h = torch.empty((W + K, C, SF_SAMPLES), dtype=torch.int16, pin_memory=True)
+    bits_h = torch.zeros((W + K, C, SF_BYTES), dtype=torch.uint8, pin_memory=True)
+    for s in range(W + K):
+        eng.synth_dev(tmp.data_ptr(), SF_SAMPLES, rig.sptr)
+        pcm_h[s].copy_(tmp)
+    rig.sync()
+    log("host leg: %.1f GB of pinned input made in %.1f s" % (pcm_h.numel() * 2 / 1e9,
+                                                               time.perf_counter() - t0))
+    del tmp
+
+    def step(s):
+        eng.encode_host_async(bits_h[s].data_ptr(), pcm_h[s].data_ptr())
+    for s in range(W):
+        step(s)
+    eng.encode_host_wait()
+    rig.sync()
+    rig.barrier()
+    t0 = time.perf_counter()
+    for s in range(W, W + K):
+        step(s)
+    eng.encode_host_wait()
+    dt = rig.max_over_ranks(time.perf_counter() - t0)
+    same = bool(torch.equal(bits_h[W:], dev_bits[W:].cpu()))
+    eng.close()
+    del pcm_h, bits_h
+    return {"value": world * C * K * SF_SECONDS / dt, "unit": "channel-s/s (host buffers in and out)",
+            "ms_per_step": 1e3 * dt / K, "steps": K, "warmup": W,
+            "pcie_bytes_per_step": C * (2 * SF_SAMPLES * 2 + SF_BYTES),
+            "bits_equal_device_resident": same,
+            "how": "melpe_encode_host_async: pinned host PCM [C, 540] in, NPP output and bits "
+                   "out per superframe, two device slots, H2D / kernels / D2H on three streams"}
+
+
 def tx_leg(rig, args, rank, world):
     """BASELINE config 5: the TX front end (tx.c:232-246: VAD gate, then
     melpe_a on the superframes it opens) on ragged streams, per-channel
@@ -446,6 +495,13 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
     enc_kms = npp_kms + ana_kms
     log("encode: %.1f ms/step (k_enc_npp %.1f ms + k_enc_ana %.1f ms)"
         % (1e3 * enc_s / K, npp_kms, ana_kms))
+    hostfed = None
+    if not args.no_host_leg and workload_cls is None:
+        hostfed = host_leg(rig, C, rank * C, K, W, wl.bits, world)
+        hostfed["frac_of_device_resident"] = hostfed["value"] / (world * C * K * SF_SECONDS / enc_s)
+        log("host-fed encode: %.1f ms/step (%.0f%% of device-resident), bits equal: %s"
+            % (hostfed["ms_per_step"], 100 * hostfed["frac_of_device_resident"],
+               hostfed["bits_equal_device_resident"]))
     # end-of-run bitstream gather (the only collective, outside the timed
     # region): every rank's K x C x 11 bytes to every rank, rank 0 keeps them
     from pairphone_amd.shard import gather_bitstreams, channel_range
@@ -544,7 +600,7 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
                    "parallelism": "channel shards, %d GPU(s), no collective" % world},
         "realtime_factor": value / (world * C),
         "roofline": roof, "cpu_baseline": base, "decode": dec, "parity_spot_check": parity,
-        "strong_scaling": strong, "tx_front_end": tx,
+        "strong_scaling": strong, "tx_front_end": tx, "host_fed": hostfed,
         "bitstream_gather": gathered, "voice_crypt": side.get("crypt"), "vad": side.get("vad"),
         "modem": side.get("modem"),
     }

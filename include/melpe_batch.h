@@ -276,6 +276,25 @@ int melpe_demodulate_dev(void *d_state, const void *d_pcm, long stride, void *d_
  * reference's operators. */
 int melpe_ops_eval_dev(int op, const void *d_a, const void *d_b, const void *d_c, void *d_out,
 		       long n, void *hip_stream);
+/* Host-fed pipelined encode: melpe_encode_host's work (PCM in, NPP output
+ * back into sp, bits out) enqueued without waiting.  The engine keeps two
+ * device slots; call k's host-to-device copy, kernels and device-to-host
+ * copy run on three streams, so superframe k's kernels overlap the copies
+ * of superframes k - 1 and k + 1.  bits, sp and active must stay valid and
+ * untouched until melpe_encode_host_wait returns (or two calls later, when
+ * the slot is reused).  For the copies to overlap the kernels the host
+ * buffers must be pinned (hipHostMalloc / hipHostRegister); with pageable
+ * memory the runtime stages them and the host call blocks.  Ordered after
+ * the engine's earlier calls on any stream. */
+int melpe_encode_host_async(melpe_engine *e, unsigned char *bits, int16_t *sp, const uint8_t *active);
+/* Waits for every melpe_encode_host_async call enqueued so far. */
+int melpe_encode_host_wait(melpe_engine *e);
+
+/* Device divide_s over its whole domain (0 <= num <= den < 2^15): d_digest
+ * (32,767 uint64, device) gets, for den = 1 .. 32,767, the sum over every
+ * num of q * (num * 0x9E3779B97F4A7C15 + 1) mod 2^64.  tests/
+ * test_device_ops.py forms the same digests from the reference's divide_s. */
+int melpe_divide_s_sweep_dev(void *d_digest, void *hip_stream);
 /* Device self-test of the sample-stream and exact-correlator helpers the
  * codec kernels use (pairphone_amd/csrc/helpers_eval.h): n lanes, lane i on
  * its own 464 int16 of d_src at the offsets / length d_args[4i .. 4i+2],

@@ -50,6 +50,9 @@ def load_library(path=None):
         "melpe_modulate_dev": (i32, [vp, vp, vp, i32, i32, vp, vp]),
         "melpe_demodulate_dev": (i32, [vp, vp, ctypes.c_long, vp, vp, vp, vp, i32, i32, vp, vp]),
         "melpe_ops_eval_dev": (i32, [i32, vp, vp, vp, vp, ctypes.c_long, vp]),
+        "melpe_divide_s_sweep_dev": (i32, [vp, vp]),
+        "melpe_encode_host_async": (i32, [vp, vp, vp, vp]),
+        "melpe_encode_host_wait": (i32, [vp]),
         "melpe_helpers_eval_dev": (i32, [i32, vp, vp, vp, i32, vp]),
         "melpe_encode_host": (i32, [vp, vp, vp, vp]),
         "melpe_encode_dev": (i32, [vp, vp, vp, vp, vp]),
@@ -276,6 +279,15 @@ class MelpeEngine:
         m = self._mask(active)
         _check(self.lib.melpe_encode_host(self.h, _ptr(bits), _ptr(sp), _ptr(m)))
         return bits
+
+    def encode_host_async(self, bits_ptr, sp_ptr, active_ptr=None):
+        """host-fed pipelined encode (melpe_encode_host_async): host
+        pointers (pinned for overlap) to uint8 [C, 11] bits and int16
+        [C, 540] PCM, valid until encode_host_wait()"""
+        _check(self.lib.melpe_encode_host_async(self.h, bits_ptr, sp_ptr, active_ptr))
+
+    def encode_host_wait(self):
+        _check(self.lib.melpe_encode_host_wait(self.h))
 
     def _raw_encode(self, sp, bits, active):
         """encode with caller-provided output bits (kept for inactive lanes)"""

@@ -391,6 +391,23 @@ __global__ __launch_bounds__(256) void k_ops_eval(int op, const int64_t *A, cons
 	out[i] = r;
 }
 
+/* divide_s over its whole domain, 0 <= num <= den < 2^15 (den >= 1): one
+ * thread per denominator sums q(num) * (num * 0x9E3779B97F4A7C15 + 1) over
+ * every numerator in uint64 arithmetic -- a digest that any wrong quotient
+ * changes (tests/test_device_ops.py forms the same sums from the
+ * reference's divide_s) */
+__global__ __launch_bounds__(256) void k_divide_s_sweep(uint64_t *digest)
+{
+	const int den = blockIdx.x * blockDim.x + threadIdx.x + 1;
+	if (den > 32767)
+		return;
+	uint64_t h = 0;
+	for (int num = 0; num <= den; num++)
+		h += (uint64_t) (uint16_t) divide_s((Word16) num, (Word16) den) *
+		     ((uint64_t) num * 0x9E3779B97F4A7C15ull + 1u);
+	digest[den - 1] = h;
+}
+
 /* device helper self-test (helpers_eval.h): lane i copies its HE_N
  * samples into a private array -- the codec's streams read the private
  * segment, at per-lane alignments -- and runs helper `mode` on it with
@@ -710,6 +727,19 @@ struct melpe_engine {
 	std::recursive_mutex mu;	/* guards marks and the BinBuf bookkeeping */
 	size_t npp_bytes = 0;
 	float last_ms = 0.f;
+	/* the host-fed pipeline (melpe_encode_host_async): two device slots;
+	 * call k uses slot k & 1 -- its H2D on `cin`, its kernels on the
+	 * engine stream, its D2H on `cout`, so superframe k's kernels overlap
+	 * the copies of k - 1 and k + 1 */
+	struct Slot {
+		int16_t *pcm = nullptr;
+		unsigned char *bits = nullptr;
+		uint8_t *mask = nullptr;
+		hipEvent_t loaded = nullptr, done = nullptr, freed = nullptr;
+		bool used = false;
+	} slot[2];
+	hipStream_t cin = nullptr, cout = nullptr;
+	long async_calls = 0;
 };
 
 /*
@@ -1167,6 +1197,18 @@ int melpe_engine_destroy(melpe_engine *e)
 		hipEventDestroy(e->ev_out);
 	if (e->ev_host)
 		hipEventDestroy(e->ev_host);
+	for (auto &sl : e->slot) {
+		hipFree(sl.pcm);
+		hipFree(sl.bits);
+		hipFree(sl.mask);
+		for (hipEvent_t ev : {sl.loaded, sl.done, sl.freed})
+			if (ev)
+				hipEventDestroy(ev);
+	}
+	if (e->cin)
+		hipStreamDestroy(e->cin);
+	if (e->cout)
+		hipStreamDestroy(e->cout);
 	delete e;
 	return 0;
 }
@@ -1345,6 +1387,74 @@ int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const u
 	HIPCHK(hipMemcpyAsync(sp, e->d_pcm, pb, hipMemcpyDeviceToHost, e->stream));
 	HIPCHK(hipMemcpyAsync(bits, e->d_bits, bb, hipMemcpyDeviceToHost, e->stream));
 	HOST_FINISH(e);
+	return 0;
+}
+
+/* the host-fed pipeline's buffers and streams, made at its first call */
+static int async_setup(melpe_engine *e)
+{
+	if (e->cin)
+		return 0;
+	const size_t pb = sizeof(int16_t) * BLOCK * (size_t) e->channels, bb = (size_t) 11 * e->channels;
+	for (auto &sl : e->slot) {
+		HIPCHK(hipMalloc(&sl.pcm, pb));
+		HIPCHK(hipMalloc(&sl.bits, bb));
+		HIPCHK(hipMalloc(&sl.mask, (size_t) e->channels));
+		for (hipEvent_t *ev : {&sl.loaded, &sl.done, &sl.freed})
+			HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+	}
+	HIPCHK(hipStreamCreateWithFlags(&e->cout, hipStreamNonBlocking));
+	HIPCHK(hipStreamCreateWithFlags(&e->cin, hipStreamNonBlocking));
+	return 0;
+}
+
+int melpe_encode_host_async(melpe_engine *e, unsigned char *bits, int16_t *sp, const uint8_t *active)
+{
+	if (!e || !bits || !sp)
+		return fail_msg("melpe_encode_host_async: null argument");
+	DEVGUARD(e->device);
+	HOST_LOCK(e);
+	if (int rc = async_setup(e))
+		return rc;
+	const size_t pb = sizeof(int16_t) * BLOCK * (size_t) e->channels, bb = (size_t) 11 * e->channels;
+	melpe_engine::Slot &sl = e->slot[e->async_calls & 1];
+	/* the slot's previous superframe has left the device (its D2H) */
+	if (sl.used)
+		HIPCHK(hipStreamWaitEvent(e->cin, sl.freed, 0));
+	/* (the copies touch only the slot; the kernels below are ordered after
+	 * the engine's earlier calls by the engine stream itself) */
+	if (active)
+		HIPCHK(hipMemcpyAsync(sl.mask, active, (size_t) e->channels, hipMemcpyHostToDevice, e->cin));
+	HIPCHK(hipMemcpyAsync(sl.pcm, sp, pb, hipMemcpyHostToDevice, e->cin));
+	if (active)	/* inactive channels keep the caller's bits */
+		HIPCHK(hipMemcpyAsync(sl.bits, bits, bb, hipMemcpyHostToDevice, e->cin));
+	HIPCHK(hipEventRecord(sl.loaded, e->cin));
+	/* the kernels on the engine stream, after the slot's H2D */
+	HIPCHK(hipStreamWaitEvent(e->stream, sl.loaded, 0));
+	HIPCHK((hipError_t) kl_enc_npp(e->d_enc, sl.pcm, active ? sl.mask : nullptr, e->channels, e->stream));
+	HIPCHK((hipError_t) ana_launch(e, sl.pcm, sl.bits, active ? sl.mask : nullptr, e->stream));
+	HIPCHK(hipEventRecord(sl.done, e->stream));
+	/* the NPP output (melpe_a's in-place side effect) and the bits back */
+	HIPCHK(hipStreamWaitEvent(e->cout, sl.done, 0));
+	HIPCHK(hipMemcpyAsync(sp, sl.pcm, pb, hipMemcpyDeviceToHost, e->cout));
+	HIPCHK(hipMemcpyAsync(bits, sl.bits, bb, hipMemcpyDeviceToHost, e->cout));
+	HIPCHK(hipEventRecord(sl.freed, e->cout));
+	sl.used = true;
+	e->async_calls++;
+	/* later calls of this engine (and engine_wait) are ordered after this
+	 * one's last copy */
+	return engine_mark(e, e->cout);
+}
+
+int melpe_encode_host_wait(melpe_engine *e)
+{
+	if (!e)
+		return fail_msg("melpe_encode_host_wait: null argument");
+	DEVGUARD(e->device);
+	HOST_LOCK(e);
+	for (auto &sl : e->slot)
+		if (sl.used)
+			HIPCHK(hipEventSynchronize(sl.freed));
 	return 0;
 }
 
@@ -1821,6 +1931,15 @@ int melpe_ops_eval_dev(int op, const void *d_a, const void *d_b, const void *d_c
 	k_ops_eval<<<(unsigned) ((n + 255) / 256), 256, 0, (hipStream_t) hip_stream>>>(
 		op, (const int64_t *) d_a, (const int32_t *) d_b, (const int32_t *) d_c,
 		(int64_t *) d_out, n);
+	HIPCHK(hipGetLastError());
+	return 0;
+}
+
+int melpe_divide_s_sweep_dev(void *d_digest, void *hip_stream)
+{
+	if (!d_digest)
+		return fail_msg("melpe_divide_s_sweep_dev: null argument");
+	k_divide_s_sweep<<<(32767 + 255) / 256, 256, 0, (hipStream_t) hip_stream>>>((uint64_t *) d_digest);
 	HIPCHK(hipGetLastError());
 	return 0;
 }

@@ -153,3 +153,41 @@ def test_device_basic_ops_match_reference():
                 got[i], want[i]))
     assert not bad, "; ".join(bad)
     assert total > 30_000_000
+
+
+def ref_divide_s_digests(ref):
+    """for den = 1 .. 32,767: sum over num = 0 .. den of the reference's
+    divide_s(num, den) * (num * 0x9E3779B97F4A7C15 + 1) mod 2^64, the
+    reference evaluated over all ~537 M pairs in blocks of denominators"""
+    out = np.zeros(32767, np.uint64)
+    mul = np.uint64(0x9E3779B97F4A7C15)
+    for d0 in range(1, 32768, 512):
+        dens = np.arange(d0, min(d0 + 512, 32768), dtype=np.int64)
+        cnt = dens + 1
+        b = np.repeat(dens, cnt)
+        start = np.repeat(np.cumsum(cnt) - cnt, cnt)
+        a = np.arange(len(b), dtype=np.int64) - start
+        q = ref_eval(ref, ID["divide_s"], a, b, None).astype(np.uint64)
+        with np.errstate(over="ignore"):
+            w = q * (a.astype(np.uint64) * mul + np.uint64(1))
+        out[dens - 1] = np.add.reduceat(w, np.cumsum(cnt) - cnt)
+    return out
+
+
+@pytest.mark.gpu
+def test_device_divide_s_exhaustive():
+    """divide_s (device: float reciprocal + integer correction, ops.h) over
+    its whole domain 0 <= num <= den < 2^15 against the reference's
+    (melpe/mathhalf_i.h:175-190): one launch digests each denominator's
+    quotients, the reference's quotients give the same digests"""
+    import torch
+    from pairphone_amd import load_library
+    lib = load_library()
+    ref = ctypes.CDLL(os.path.join(REF_DIR, "libref_ops.so"))
+    dev = torch.device("cuda", 0)
+    d = torch.zeros(32767, dtype=torch.int64, device=dev)
+    assert lib.melpe_divide_s_sweep_dev(d.data_ptr(), torch.cuda.current_stream(dev).cuda_stream) == 0
+    got = d.cpu().numpy().view(np.uint64)
+    want = ref_divide_s_digests(ref)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, "divide_s differs for denominators %s" % (bad[:8] + 1)
