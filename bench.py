@@ -95,6 +95,8 @@ def parse(argv=None):
                     help="config 5 TX front end leg, channels per GPU (0 = skip)")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-side-legs", action="store_true", help="skip crypt and VAD legs")
+    ap.add_argument("--no-duplex", action="store_true",
+                    help="skip the duplex leg (encoder + decoder engines, shared vs own streams)")
     ap.add_argument("--no-host-leg", action="store_true",
                     help="skip the host-fed (pinned host buffers, PCIe-inclusive) encode leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -420,6 +422,59 @@ def host_leg(rig, C, first, K, W, dev_bits, world):
                    "out per superframe, two device slots, H2D / kernels / D2H on three streams"}
 
 
+def duplex_leg(rig, wl, C, K, W):
+    """A duplex link's two directions on one GPU: an encoder engine and a
+    decoder engine of C channels, superframe k encoded on one caller stream
+    while superframe k - 1's bits are decoded on another.  Timed twice,
+    fresh engines each time: with both engines on the device's shared engine
+    stream (the default: one hardware queue, the kernels serialise) and
+    with each on a stream of its own (melpe_engine_set_own_stream: the
+    kernels may overlap).  ms per duplex step either way, and whether the
+    two runs' bits agree."""
+    import torch
+    from pairphone_amd import MelpeEngine
+    out = {}
+    ref_bits = None
+    for mode in ("shared", "own"):
+        wl.regen_pcm()
+        enc, dec = MelpeEngine(C, device=rig.dev.index), MelpeEngine(C, device=rig.dev.index)
+        if mode == "own":
+            enc.set_own_stream(True)
+            dec.set_own_stream(True)
+        sa, sb = torch.cuda.Stream(rig.dev), torch.cuda.Stream(rig.dev)
+        bits = torch.zeros((W + K, C, SF_BYTES), dtype=torch.uint8, device=rig.dev)
+        pcm = torch.empty((C, SF_SAMPLES), dtype=torch.int16, device=rig.dev)
+        evs = [torch.cuda.Event() for _ in range(W + K)]
+
+        def step(s):
+            enc.encode_dev(bits[s].data_ptr(), wl.pcm[s].data_ptr(), None, sa.cuda_stream)
+            evs[s].record(sa)
+            if s > 0:
+                sb.wait_event(evs[s - 1])
+                dec.decode_dev(pcm.data_ptr(), bits[s - 1].data_ptr(), None, sb.cuda_stream)
+        for s in range(W):
+            step(s)
+        rig.sync()
+        t0 = time.perf_counter()
+        for s in range(W, W + K):
+            step(s)
+        rig.sync()
+        out[mode] = 1e3 * (time.perf_counter() - t0) / K
+        if ref_bits is None:
+            ref_bits = bits.cpu()
+        else:
+            out["bits_equal"] = bool(torch.equal(ref_bits, bits.cpu()))
+        enc.close()
+        dec.close()
+        del bits, pcm
+    res = {"ms_per_step_shared_stream": out["shared"], "ms_per_step_own_streams": out["own"],
+           "bits_equal": out["bits_equal"], "channels": C,
+           "step": "encode superframe k (caller stream A) + decode superframe k - 1 (caller stream B)"}
+    log("duplex: %.1f ms/step on the shared engine stream, %.1f ms/step on own streams"
+        % (out["shared"], out["own"]))
+    return res
+
+
 def tx_leg(rig, args, rank, world):
     """BASELINE config 5: the TX front end (tx.c:232-246: VAD gate, then
     melpe_a on the superframes it opens) on ragged streams, per-channel
@@ -519,6 +574,9 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
                "ms_per_step": 1e3 * dec_s / K, "kernel_ms": dec_kms}
         log("decode: %.1f ms/step (kernel %.1f ms)" % (1e3 * dec_s / K, dec_kms))
     cpu_bits = wl.bits[:W + K, :args.cpu_sample_channels].cpu().numpy() if rank == 0 else None
+    duplex = None
+    if not args.no_duplex and workload_cls is None:
+        duplex = duplex_leg(rig, wl, C, K, W)
 
     side = {}
     if not args.no_side_legs:
@@ -600,7 +658,7 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
                    "parallelism": "channel shards, %d GPU(s), no collective" % world},
         "realtime_factor": value / (world * C),
         "roofline": roof, "cpu_baseline": base, "decode": dec, "parity_spot_check": parity,
-        "strong_scaling": strong, "tx_front_end": tx, "host_fed": hostfed,
+        "strong_scaling": strong, "tx_front_end": tx, "host_fed": hostfed, "duplex": duplex,
         "bitstream_gather": gathered, "voice_crypt": side.get("crypt"), "vad": side.get("vad"),
         "modem": side.get("modem"),
     }

@@ -103,6 +103,19 @@ int melpe_engine_set_ana_waves(melpe_engine *e, int waves);
  * same either way. */
 int melpe_engine_set_mw_live_max(melpe_engine *e, int live_max);
 
+/* By default every engine on a device runs its kernels on one internal
+ * stream per device (one hardware queue): the runtime holds kernel scratch
+ * per queue, sized for the largest private segment it has run at the
+ * device's full wave count, and engines each on a queue of their own could
+ * exhaust the scratch pool (a later launch then aborts its queue with
+ * HSA_STATUS_ERROR_OUT_OF_RESOURCES) or make the runtime reclaim one
+ * queue's scratch for another's, hundreds of ms per launch.  With on = 1
+ * this engine gets a stream of its own (its kernels can then overlap other
+ * engines', e.g. an encoder and a decoder of a duplex link); its scratch is
+ * reserved on it here, and the call fails cleanly if it cannot be had.
+ * on = 0 returns to the shared stream.  Waits for the engine's calls. */
+int melpe_engine_set_own_stream(melpe_engine *e, int on);
+
 /* The mapping the engine's last analysis launch ran, as the device recorded
  * it: 1 = one lane per channel, 4 = four waves per 64 channels, 0 = none
  * (no live channel).  Waits for the engine's enqueued calls. */

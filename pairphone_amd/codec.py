@@ -42,6 +42,7 @@ def load_library(path=None):
         "melpe_engine_set_ana_waves": (i32, [vp, i32]),
         "melpe_engine_set_mw_live_max": (i32, [vp, i32]),
         "melpe_engine_last_ana_waves": (i32, [vp]),
+        "melpe_engine_set_own_stream": (i32, [vp, i32]),
         "melpe_engine_state_bytes": (ctypes.c_long, [i32]),
         "melpe_engine_export": (i32, [vp, i32, i32, i32, vp]),
         "melpe_engine_import": (i32, [vp, i32, i32, i32, vp]),
@@ -237,6 +238,11 @@ class MelpeEngine:
         channels run the four-wave analysis (0 = off; results are the same
         either way)"""
         _check(self.lib.melpe_engine_set_mw_live_max(self.h, int(live_max)))
+
+    def set_own_stream(self, on):
+        """run this engine's kernels on a stream (hardware queue) of its own
+        instead of the device's shared engine stream"""
+        _check(self.lib.melpe_engine_set_own_stream(self.h, 1 if on else 0))
 
     def last_ana_waves(self):
         """the mapping the last analysis launch ran, recorded on the device:

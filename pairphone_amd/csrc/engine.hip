@@ -740,6 +740,7 @@ struct melpe_engine {
 	} slot[2];
 	hipStream_t cin = nullptr, cout = nullptr;
 	long async_calls = 0;
+	hipStream_t own = nullptr;	/* melpe_engine_set_own_stream */
 };
 
 /*
@@ -1027,6 +1028,22 @@ const char *melpe_last_error(void)
  *   is held per hardware queue: a caller's own stream may map to another
  *   queue, whose first dispatch reserves it again.)
  */
+/* every codec kernel dispatched once on the engine's stream with the grid
+ * of a real launch and no live channel, and waited for: the runtime sizes
+ * that hardware queue's scratch by the dispatches it sees */
+static int engine_warm(melpe_engine *e)
+{
+	hipError_t er;
+	const int mw = e->channels < MW_MAX_CHANNELS ? e->channels : MW_MAX_CHANNELS;
+	int (*warm[])(int, hipStream_t) = {kl_npp_warm, kl_ana_warm, kl_harm_warm, kl_ana_mw_warm, kl_dec_warm};
+	for (auto f : warm)
+		if ((er = (hipError_t) f(f == kl_ana_mw_warm ? mw : e->channels, e->stream)) != hipSuccess)
+			return fail("melpe_engine: codec kernel scratch could not be reserved", er);
+	if ((er = hipStreamSynchronize(e->stream)) != hipSuccess)
+		return fail("melpe_engine: codec kernel scratch could not be reserved", er);
+	return 0;
+}
+
 static int engine_reserve(melpe_engine *e)
 {
 	DEVGUARD(e->device);
@@ -1067,13 +1084,7 @@ static int engine_reserve(melpe_engine *e)
 		}
 		e->scratch_need = need;
 	}
-	int (*warm[])(int, hipStream_t) = {kl_npp_warm, kl_ana_warm, kl_harm_warm, kl_ana_mw_warm, kl_dec_warm};
-	for (auto f : warm)
-		if ((er = (hipError_t) f(f == kl_ana_mw_warm ? mw : e->channels, e->stream)) != hipSuccess)
-			return fail("melpe_engine_create: codec kernel scratch could not be reserved", er);
-	if ((er = hipStreamSynchronize(e->stream)) != hipSuccess)
-		return fail("melpe_engine_create: codec kernel scratch could not be reserved", er);
-	return 0;
+	return engine_warm(e);
 }
 
 int melpe_engine_create(melpe_engine **out, int device, int channels)
@@ -1124,6 +1135,32 @@ int melpe_engine_create(melpe_engine **out, int device, int channels)
 		return r;
 	}
 	*out = e;
+	return 0;
+}
+
+int melpe_engine_set_own_stream(melpe_engine *e, int on)
+{
+	if (!e)
+		return fail_msg("melpe_engine_set_own_stream: null engine");
+	DEVGUARD(e->device);
+	HOST_LOCK(e);
+	ENGINE_WAIT(e);
+	HIPCHK(hipStreamSynchronize(e->stream));
+	if (on && !e->own) {
+		HIPCHK(hipStreamCreateWithFlags(&e->own, hipStreamNonBlocking));
+		e->stream = e->own;
+		/* the new queue's scratch, had here and not mid-stream */
+		if (int rc = engine_warm(e)) {
+			e->stream = g_dev_stream[e->device];
+			hipStreamDestroy(e->own);
+			e->own = nullptr;
+			return rc;
+		}
+	} else if (!on && e->own) {
+		e->stream = g_dev_stream[e->device];
+		HIPCHK(hipStreamDestroy(e->own));
+		e->own = nullptr;
+	}
 	return 0;
 }
 
@@ -1205,6 +1242,8 @@ int melpe_engine_destroy(melpe_engine *e)
 			if (ev)
 				hipEventDestroy(ev);
 	}
+	if (e->own)
+		hipStreamDestroy(e->own);
 	if (e->cin)
 		hipStreamDestroy(e->cin);
 	if (e->cout)

@@ -194,3 +194,47 @@ def test_single_stream_duplex_matches_reference(tmp_path, ref_tool):
         y.append(m.melpe_s(rx[k * 11:(k + 1) * 11]))
     np.testing.assert_array_equal(np.concatenate(tx), np.fromfile(str(tmp_path / "tx.bits"), np.uint8))
     np.testing.assert_array_equal(np.concatenate(y), np.fromfile(str(tmp_path / "y.pcm"), np.int16))
+
+
+@pytest.mark.gpu
+def test_duplex_encoder_decoder_on_own_streams_match_goldens():
+    """An encoder engine and a decoder engine, each on a stream (hardware
+    queue) of its own (melpe_engine_set_own_stream), driven from two caller
+    streams: superframe k is encoded on one while superframe k - 1's bits
+    are decoded on the other, the decoder's stream waiting only for the
+    bits it reads.  Both outputs match the 1,024-channel goldens (the
+    encoder's bitstream and NPP output, the PCM the reference decodes
+    from it); whether the two engines' kernels overlap is timed by
+    bench.py --duplex."""
+    import torch
+    from pairphone_amd import MelpeEngine
+    ge, gd = enc_golden(), gold("dec_1024.json")
+    C, nsf = ge["channels"], ge["superframes"]
+    dev = torch.device("cuda", 0)
+    x = torch.from_numpy(np.ascontiguousarray(
+        signals(ge["seed"], C, nsf).reshape(C, nsf, 540).transpose(1, 0, 2))).to(dev)
+    enc, dec = MelpeEngine(C), MelpeEngine(C)
+    enc.set_own_stream(True)
+    dec.set_own_stream(True)
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    sa.wait_stream(torch.cuda.current_stream(dev))
+    bits = torch.zeros((nsf, C, 11), dtype=torch.uint8, device=dev)
+    pcm = torch.zeros((nsf, C, 540), dtype=torch.int16, device=dev)
+    for k in range(nsf + 1):
+        if k < nsf:
+            enc.encode_dev(bits[k].data_ptr(), x[k].data_ptr(), None, sa.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(sa)
+        if k > 0:
+            dec.decode_dev(pcm[k - 1].data_ptr(), bits[k - 1].data_ptr(), None, sb.cuda_stream)
+        if k < nsf:
+            sb.wait_event(ev)
+    torch.cuda.synchronize(dev)
+    enc.close()
+    dec.close()
+    b = bits.cpu().numpy().transpose(1, 0, 2).reshape(C, nsf * 11)
+    n = x.cpu().numpy().transpose(1, 0, 2).reshape(C, nsf * 540)
+    p = pcm.cpu().numpy().transpose(1, 0, 2).reshape(C, nsf * 540)
+    assert [c for c in range(C) if sha(b[c]) != ge["bits_sha256"][c]] == []
+    assert [c for c in range(C) if sha(n[c]) != ge["npp_sha256"][c]] == []
+    assert [c for c in range(C) if sha(p[c]) != gd["pcm_sha256"][c]] == []

@@ -160,6 +160,45 @@ def test_encode_host_two_threads_one_engine():
         np.testing.assert_array_equal(npp[halves[h]], wnpp[halves[h]])
 
 
+@pytest.mark.gpu
+def test_encode_host_async_matches_sync():
+    """The host-fed pipeline (melpe_encode_host_async: two device slots,
+    copies and kernels on three streams) against melpe_encode_host, on
+    pinned and on pageable buffers, with a ragged mask on some superframes:
+    the same bits and in-place NPP output"""
+    import torch
+    from pairphone_amd import MelpeEngine
+    g = golden()
+    C, nsf = 256, 12
+    x = signals(g["seed"], C, nsf)
+    rng = np.random.default_rng(3)
+    masks = [None if k % 3 else (rng.random(C) < 0.6).astype(np.uint8) for k in range(nsf)]
+    ref = MelpeEngine(C)
+    want_b = np.zeros((nsf, C, 11), np.uint8)
+    want_p = np.zeros((nsf, C, 540), np.int16)
+    for k in range(nsf):
+        sp = np.ascontiguousarray(x[:, k * 540:(k + 1) * 540])
+        bits = np.full((C, 11), 0xAB, np.uint8)
+        ref._raw_encode(sp, bits, masks[k])
+        want_b[k], want_p[k] = bits, sp
+    ref.close()
+    for pinned in (True, False):
+        eng = MelpeEngine(C)
+        pcm = torch.from_numpy(np.ascontiguousarray(
+            x[:, :nsf * 540].reshape(C, nsf, 540).transpose(1, 0, 2)))
+        bits = torch.full((nsf, C, 11), 0xAB, dtype=torch.uint8)
+        mk = torch.from_numpy(np.stack([m if m is not None else np.ones(C, np.uint8) for m in masks]))
+        if pinned:
+            pcm, bits, mk = pcm.pin_memory(), bits.pin_memory(), mk.pin_memory()
+        for k in range(nsf):
+            eng.encode_host_async(bits[k].data_ptr(), pcm[k].data_ptr(),
+                                  None if masks[k] is None else mk[k].data_ptr())
+        eng.encode_host_wait()
+        eng.close()
+        np.testing.assert_array_equal(bits.numpy(), want_b, err_msg="bits, pinned=%s" % pinned)
+        np.testing.assert_array_equal(pcm.numpy(), want_p, err_msg="NPP output, pinned=%s" % pinned)
+
+
 def edge_signals(n):
     rng = np.random.default_rng(5)
     t = np.arange(n)
