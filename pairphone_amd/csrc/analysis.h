@@ -416,7 +416,7 @@ MD void fp_corrK(const int16_t *pa, const int16_t *pb, int len, Word32 *out)
 /* frac_pch's nine sums as exact plain sums (the caller's bound), on packed
  * pairs: a_j = pa[j], b_j = pb[j], j < len; in q[]: a.a, b.b, a.b, a.b+1,
  * a.b+2, b+1.b+2, b+1.b+1, b+2.b+2, b.b+1.  Reads pa[0 .. len), pb[0 .. len + 2). */
-MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q)
+MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q, int lsh = 0)
 {
 	constexpr int PD = MELPE_XC_PD;
 	int32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -430,6 +430,7 @@ MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q)
 		 * their mids (b_j+1) and wb[st + 1] (b_j+2) */
 		uint32_t wb[5];
 		ps_head<1>(sb, wb);
+		wb[0] = pk_shl16(wb[0], lsh);
 		auto group = [&](const uint32_t *xa, int nst) {
 			#pragma unroll
 			for (int st = 0; st < 4; st++) {
@@ -458,6 +459,11 @@ MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q)
 				uint32_t xa[4];
 				p16c_next4(ca, xa);
 				p16c_next4(cb, &wb[1]);
+				#pragma unroll
+				for (int k = 0; k < 4; k++) {
+					xa[k] = pk_shl16(xa[k], lsh);
+					wb[1 + k] = pk_shl16(wb[1 + k], lsh);
+				}
 				group(xa, 4);
 			}
 		}
@@ -466,12 +472,18 @@ MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q)
 			uint32_t xa[4];
 			ps_pairs4(sa, t, xa);
 			ps_pairs4(sb, 1 + t, &wb[1]);
+			#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				xa[k] = pk_shl16(xa[k], lsh);
+				wb[1 + k] = pk_shl16(wb[1 + k], lsh);
+			}
 			group(xa, T - t);
 		}
 		jt = 2 * T;
 	}
 	for (int j = jt; j < len; j++) {
-		int a = pa[j], x0 = pb[j], x1 = pb[j + 1], x2 = pb[j + 2];
+		const int m = 1 << lsh;
+		int a = pa[j] * m, x0 = pb[j] * m, x1 = pb[j + 1] * m, x2 = pb[j + 2] * m;
 		acc[0] += a * a;
 		acc[1] += x0 * x0;
 		acc[2] += a * x0;
@@ -625,13 +637,20 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 }
 
 /* frac_pch :340 -- fractional pitch refinement and its correlation */
+/* lsh > 0 (range 0 only): sig holds the window before its scaling by
+ * f_pitch_scale, which the caller proved a plain left shift by lsh with no
+ * saturation (bpvc_band_s); every sample is shifted as it is read, so the
+ * scaled window is never written out */
 MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 range,
 		   Word16 pmin, Word16 pmax, Word16 pmin_q7, Word16 pmax_q7, Word16 lmin,
-		   bool exact = false)
+		   bool exact = false, int lsh = 0)
 {
 	PROF_SCOPE(3);
 #if defined(MELPE_OPCOUNT)
 	exact = false;
+#endif
+#if defined(MELPE_DIAG_UNIFORM_PITCH)
+	fpitch = 80 << 7;	/* diagnostics only: every lane at one lag (wrong output) */
 #endif
 	EXACT_STAT(exact ? 3 : 2);
 	Word16 len, cb, ip, corr;
@@ -666,7 +685,7 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 	Word32 msq = 0, m2 = 0, cm1 = 0, c0 = 0, c1 = 0, tt1 = 0, tt = 0, t1t1 = 0, tt1m = 0;
 	if (exact) {
 		int32_t q[9];
-		fp_sums9(&sig[cb], &sig[cb + ip - 1], len, q);
+		fp_sums9(&sig[cb], &sig[cb + ip - 1], len, q, lsh);
 		msq = 2 * q[0];
 		m2 = 2 * q[1];
 		cm1 = 2 * q[2];
@@ -678,7 +697,7 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 		tt1m = 2 * q[8];
 	} else {
 		const int16_t *pa = &sig[cb], *pb = &sig[cb + ip - 1];
-		int16_t b0 = pb[0], b1 = pb[1];
+		int16_t b0 = (int16_t) (pb[0] * (1 << lsh)), b1 = (int16_t) (pb[1] * (1 << lsh));
 		auto step = [&](int16_t a, int16_t b2) {
 			msq = L_mac(msq, a, a);
 			m2 = L_mac(m2, b0, b0);
@@ -699,12 +718,12 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 		int j = 0;
 		#pragma unroll 4
 		for (int k = 0; k < np; k++, j += 2) {
-			uint32_t x = p16_next(ra), y = p16_next(rb);
+			uint32_t x = pk_shl16(p16_next(ra), lsh), y = pk_shl16(p16_next(rb), lsh);
 			step(lo16(x), lo16(y));
 			step(hi16(x), hi16(y));
 		}
 		for (; j < len; j++)
-			step(pa[j], pb[j + 2]);
+			step((int16_t) (pa[j] * (1 << lsh)), (int16_t) (pb[j + 2] * (1 << lsh)));
 	}
 	/* census: the reference's two L_v_magsq and six L_v_inner calls */
 	OPC_ADD(OP_L_mac, -len);
@@ -713,8 +732,12 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 	OPC_ADD(OP_add, 12);
 	OPC_ADD(OP_L_shl, 8);
 	Word32 ttm = m2;	/* sum of b_j^2, j < len */
-	m2 = L_mac(m2, sig[cb + ip - 1 + len], sig[cb + ip - 1 + len]);
-	m2 = L_mac(m2, sig[cb + ip + len], sig[cb + ip + len]);
+	{
+		const int m = 1 << lsh;
+		const int16_t u = (int16_t) (sig[cb + ip - 1 + len] * m), v = (int16_t) (sig[cb + ip + len] * m);
+		m2 = L_mac(m2, u, u);
+		m2 = L_mac(m2, v, v);
+	}
 	Word16 s1a = norm_s(extract_h(msq));
 	Word16 s1b = norm_s(extract_h(m2));
 	Word16 s = add(s1a, s1b);
@@ -1100,6 +1123,36 @@ MN void bpvc_band_s(BandState *B, const int16_t *sp, int i, Word16 pitch, int16_
 	const int fi = i * (BPF_ORD / 2) * 3;
 	bool ex;
 	int64_t e = bp_window(B->fsp, sp, w, TB(bpf_den) + fi, TB(bpf_num) + fi, B->delin, B->delout);
+	if (e <= (int64_t) LW_MAX_) {
+		/* f_pitch_scale (pit_lib.c:178-203) without its pass over the
+		 * window: with the energy e = sum 2x^2 within 32 bits its scale is
+		 * a left shift by lsh = norm_l(e) >> 1, and every scaled sample
+		 * fits (2 (x 2^lsh)^2 <= e 2^(2 lsh) < 2^31), as does the scaled
+		 * window's energy e 4^lsh, so the exact correlators apply.  The
+		 * window stays unscaled; frac_pch and envelope shift each sample
+		 * as they read it. */
+		const int lsh = shr(norm_l((Word32) e), 1);
+		sc = (Word16) -lsh;
+		frac_pch(&sb[BPF_ORD + PITCHMAX], bpvci, pitch, 0, PITCHMIN, PITCHMAX, PITCHMIN_Q7,
+			 PITCHMAX_Q7, 160, true, lsh);
+		t = shr(B->env2, sc);
+		B->env2 = shr((int16_t) (w[FRAME - 1] * (1 << lsh)), (Word16) -sc);
+		v_equ_shr(&sb[BPF_ORD - ENV_ORD], B->env, sc, ENV_ORD);
+		e = envelope_e(w, t, w, PITCH_FR, lsh);
+		v_equ_shr(B->env, &sb[BPF_ORD + FRAME - ENV_ORD], (Word16) -sc, ENV_ORD);
+		if (e <= (int64_t) LW_MAX_) {
+			frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, pitch, 0, PITCHMIN, PITCHMAX, PITCHMIN_Q7,
+				 PITCHMAX_Q7, 160, true, shr(norm_l((Word32) e), 1));
+		} else {
+			f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
+			frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, pitch, 0, PITCHMIN, PITCHMAX, PITCHMIN_Q7,
+				 PITCHMAX_Q7, 160, ex);
+		}
+		pcorr = sub(pcorr, 1638);
+		if (pcorr > *bpvci)
+			*bpvci = pcorr;
+		return;
+	}
 	sc = f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
 	frac_pch(&sb[BPF_ORD + PITCHMAX], bpvci, pitch, 0, PITCHMIN, PITCHMAX, PITCHMIN_Q7,
 		 PITCHMAX_Q7, 160, ex);
@@ -1764,6 +1817,9 @@ MD void fc_corr_any(const int16_t *in, int hp, int win, Word40 *A)
 MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 {
 	PROF_SCOPE(46);
+#if defined(MELPE_DIAG_UNIFORM_PITCH)
+	pitch = 80;	/* diagnostics only: every lane at one lag (wrong output) */
+#endif
 	Word16 lp = sub(pitch, 5), hp = add(pitch, 5);
 	if (lp < MINPITCH)
 		lp = MINPITCH;

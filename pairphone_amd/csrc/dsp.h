@@ -105,6 +105,20 @@ MD int32_t sdot2_sat(uint32_t a, uint32_t b, int32_t c)
 }
 
 /* the pair one sample later: (lo's high half, hi's low half) */
+/* both int16 halves of v shifted left by s (0 <= s < 16), each in its own
+ * half (v_pk_lshlrev_b16); callers guarantee no half overflows */
+MD uint32_t pk_shl16(uint32_t v, int s)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+	typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+	u16x2 x = __builtin_bit_cast(u16x2, v);
+	u16x2 y = x << (u16x2) {(uint16_t) s, (uint16_t) s};
+	return __builtin_bit_cast(uint32_t, y);
+#else
+	return ((uint32_t) (uint16_t) ((v & 0xffffu) << s)) | ((uint32_t) (uint16_t) ((v >> 16) << s) << 16);
+#endif
+}
+
 MD uint32_t pair_mid(uint32_t hi, uint32_t lo)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -830,14 +844,17 @@ MN void envelope(const int16_t *in, int16_t prev_in, int16_t *out, int n)
 }
 
 /* envelope, returning the exact energy (sum of L_mult(y, y)) of what it
- * wrote, for f_pitch_scale_e (bpvc_ana) */
-MD int64_t envelope_e(const int16_t *in, int16_t prev_in, int16_t *out, int n)
+ * wrote, for f_pitch_scale_e (bpvc_ana); lsh > 0: the input is in[i]
+ * scaled up by 2^lsh, the caller having proved no sample overflows
+ * (bpvc_band_s) */
+MD int64_t envelope_e(const int16_t *in, int16_t prev_in, int16_t *out, int n, int lsh = 0)
 {
 	PROF_SCOPE(48);
 	Word16 pa = abs_s(prev_in), y1 = out[-1], y2 = out[-2];
 	int64_t e = 0;
+	const int m = 1 << lsh;
 	v_batch(in, out, n, [&](int, int16_t x) {
-		Word16 ca = abs_s(x);
+		Word16 ca = abs_s((int16_t) (x * m));
 		Word32 acc = L_shr(L_deposit_h(sub(ca, pa)), 5);
 		acc = L_mac(acc, 31565, y1);
 		acc = L_mac(acc, -15415, y2);
