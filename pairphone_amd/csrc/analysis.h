@@ -416,7 +416,7 @@ MD void fp_corrK(const int16_t *pa, const int16_t *pb, int len, Word32 *out)
 /* frac_pch's nine sums as exact plain sums (the caller's bound), on packed
  * pairs: a_j = pa[j], b_j = pb[j], j < len; in q[]: a.a, b.b, a.b, a.b+1,
  * a.b+2, b+1.b+2, b+1.b+1, b+2.b+2, b.b+1.  Reads pa[0 .. len), pb[0 .. len + 2). */
-MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q, int lsh = 0)
+MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q)
 {
 	constexpr int PD = MELPE_XC_PD;
 	int32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -430,7 +430,6 @@ MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q, int 
 		 * their mids (b_j+1) and wb[st + 1] (b_j+2) */
 		uint32_t wb[5];
 		ps_head<1>(sb, wb);
-		wb[0] = pk_shl16(wb[0], lsh);
 		auto group = [&](const uint32_t *xa, int nst) {
 			#pragma unroll
 			for (int st = 0; st < 4; st++) {
@@ -459,11 +458,6 @@ MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q, int 
 				uint32_t xa[4];
 				p16c_next4(ca, xa);
 				p16c_next4(cb, &wb[1]);
-				#pragma unroll
-				for (int k = 0; k < 4; k++) {
-					xa[k] = pk_shl16(xa[k], lsh);
-					wb[1 + k] = pk_shl16(wb[1 + k], lsh);
-				}
 				group(xa, 4);
 			}
 		}
@@ -472,18 +466,12 @@ MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q, int 
 			uint32_t xa[4];
 			ps_pairs4(sa, t, xa);
 			ps_pairs4(sb, 1 + t, &wb[1]);
-			#pragma unroll
-			for (int k = 0; k < 4; k++) {
-				xa[k] = pk_shl16(xa[k], lsh);
-				wb[1 + k] = pk_shl16(wb[1 + k], lsh);
-			}
 			group(xa, T - t);
 		}
 		jt = 2 * T;
 	}
 	for (int j = jt; j < len; j++) {
-		const int m = 1 << lsh;
-		int a = pa[j] * m, x0 = pb[j] * m, x1 = pb[j + 1] * m, x2 = pb[j + 2] * m;
+		int a = pa[j], x0 = pb[j], x1 = pb[j + 1], x2 = pb[j + 2];
 		acc[0] += a * a;
 		acc[1] += x0 * x0;
 		acc[2] += a * x0;
@@ -499,8 +487,10 @@ MD void fp_sums9(const int16_t *pa, const int16_t *pb, int len, int32_t *q, int 
 }
 
 /* find_pitch :240 -- normalised autocorrelation lag search, lags upper..lower */
+/* lsh > 0 (exact only): sig holds the window before f_pitch_scale's left
+ * shift by lsh, which the caller proved exact (see frac_pch) */
 MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upper, Word16 len,
-		     bool exact = false)
+		     bool exact = false, int lsh = 0)
 {
 	PROF_SCOPE(2);
 #if defined(MELPE_OPCOUNT)
@@ -516,9 +506,12 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 	 * which every lag block below reads inside (also the unused lags of a
 	 * last partial block), so each L_mac chain is the plain sum */
 	Word32 c00, cTT;
+	/* sums of the scaled samples: the plain sums times 4^lsh */
+	const int32_t sm = 2 << (2 * lsh);
+	const int qm = 1 << lsh;
 	if (exact) {
-		c00 = 2 * magsq_pairs(&sig[cb], len);
-		cTT = 2 * magsq_pairs(&sig[cb + upper], len);
+		c00 = sm * magsq_pairs(&sig[cb], len);
+		cTT = sm * magsq_pairs(&sig[cb + upper], len);
 		OPC_ADD(OP_L_mac, 0);
 	} else {
 		c00 = L_v_magsq(&sig[cb], len, 0, 1);
@@ -535,7 +528,7 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 			int32_t raw[12];
 			xcorr_pairs<12, FpLags<12>, false>(&sig[cb0], &sig[cb0 + 6 + upper - 11], len, raw);
 			for (int k = 0; k < 12; k++)
-				blk12[k] = 2 * raw[k];
+				blk12[k] = sm * raw[k];
 		} else {
 			fp_corrK<12>(&sig[cb0], &sig[cb0 + 6 + upper - 11], len, blk12);
 		}
@@ -556,10 +549,10 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 			const int16_t *pa = &sig[cb0 + n / 2], *pb = &sig[cb0 + upper - 1 - n / 2];
 			#pragma unroll
 			for (int k = 0; k < 4; k++) {
-				qa[k] = pa[k];
-				qal[k] = pa[k + len];
-				qb[k] = pb[-k];
-				qbl[k] = pb[len - k];
+				qa[k] = (int16_t) (pa[k] * qm);
+				qal[k] = (int16_t) (pa[k + len] * qm);
+				qb[k] = (int16_t) (pb[-k] * qm);
+				qbl[k] = (int16_t) (pb[len - k] * qm);
 			}
 		}
 		if (one) {
@@ -572,7 +565,7 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 				int32_t raw[8];
 				xcorr_pairs<8, FpLags<8>, false>(&sig[c_n0], &sig[b0], len, raw);
 				for (int k = 0; k < 8; k++)
-					blk[k] = 2 * raw[k];
+					blk[k] = sm * raw[k];
 			} else {
 				fp_corr8(&sig[c_n0], &sig[b0], len, blk);
 			}
@@ -667,7 +660,7 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 		len = ip;
 		if (len < lmin)
 			len = lmin;
-		fpitch = shl(find_pitch(sig, &corr, lo, hi, len, exact), 7);
+		fpitch = shl(find_pitch(sig, &corr, lo, hi, len, exact, lsh), 7);
 	}
 	ip = shift_r(fpitch, -7);
 	if (ip >= pmax)
@@ -685,16 +678,19 @@ MN Word16 frac_pch(const int16_t *sig, Word16 *pcorr, Word16 fpitch, Word16 rang
 	Word32 msq = 0, m2 = 0, cm1 = 0, c0 = 0, c1 = 0, tt1 = 0, tt = 0, t1t1 = 0, tt1m = 0;
 	if (exact) {
 		int32_t q[9];
-		fp_sums9(&sig[cb], &sig[cb + ip - 1], len, q, lsh);
-		msq = 2 * q[0];
-		m2 = 2 * q[1];
-		cm1 = 2 * q[2];
-		c0 = 2 * q[3];
-		c1 = 2 * q[4];
-		tt1 = 2 * q[5];
-		tt = 2 * q[6];
-		t1t1 = 2 * q[7];
-		tt1m = 2 * q[8];
+		fp_sums9(&sig[cb], &sig[cb + ip - 1], len, q);
+		/* the sums of the samples scaled up by 2^lsh: the plain sums times
+		 * 4^lsh, exactly (the caller's bound holds for the scaled ones) */
+		const int32_t m = 2 << (2 * lsh);
+		msq = m * q[0];
+		m2 = m * q[1];
+		cm1 = m * q[2];
+		c0 = m * q[3];
+		c1 = m * q[4];
+		tt1 = m * q[5];
+		tt = m * q[6];
+		t1t1 = m * q[7];
+		tt1m = m * q[8];
 	} else {
 		const int16_t *pa = &sig[cb], *pb = &sig[cb + ip - 1];
 		int16_t b0 = (int16_t) (pb[0] * (1 << lsh)), b1 = (int16_t) (pb[1] * (1 << lsh));
@@ -1096,13 +1092,17 @@ MN void bpvc_band0(EncAna *E, const int16_t *speech, const int16_t *fpitch, int1
 	const int16_t *sp = &speech[PITCH_FR - FRAME - PITCHMAX];
 	int16_t *w = &sb[BPF_ORD];
 	int64_t e = bp_window(B->fsp, sp, w, TB(bpf_den), TB(bpf_num), B->delin, B->delout);
-	bool ex;
-	f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
+	bool ex = true;
+	int lsh = 0;
+	if (e <= (int64_t) LW_MAX_)	/* the scale read lazily, as in bpvc_band_s */
+		lsh = shr(norm_l((Word32) e), 1);
+	else
+		f_pitch_scale_e(w, w, PITCH_FR, e, &ex);
 	*pitch = frac_pch(&sb[BPF_ORD + PITCHMAX], bpvc0, fpitch[0], 5, PITCHMIN, PITCHMAX,
-			  PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
+			  PITCHMIN_Q7, PITCHMAX_Q7, 160, ex, lsh);
 	for (int i = 1; i < 2; i++) {	/* NUM_PITCHES */
 		t = frac_pch(&sb[BPF_ORD + PITCHMAX], &pcorr, fpitch[i], 5, PITCHMIN, PITCHMAX,
-			     PITCHMIN_Q7, PITCHMAX_Q7, 160, ex);
+			     PITCHMIN_Q7, PITCHMAX_Q7, 160, ex, lsh);
 		if (pcorr > *bpvc0) {
 			*pitch = t;
 			*bpvc0 = pcorr;

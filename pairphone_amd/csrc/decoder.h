@@ -93,18 +93,25 @@ MD Word32 magsq_shr(const int16_t *a, int n, Word16 sh)
 	return acc;
 }
 
-MN void scale_adj(DecState *D, int16_t *sp, Word16 gain, int len, Word16 over, Word16 inv_over)
+/* scale_adj; msq0 >= 0: the first energy (L_v_magsq of sp >> 4), already
+ * summed by the caller (syn_chain); out: where the scaled samples go (sp
+ * itself, or the caller's next buffer, which saves a copy pass) */
+MN void scale_adj(DecState *D, int16_t *sp, Word16 gain, int len, Word16 over, Word16 inv_over,
+		  Word32 msq0 = -1, int16_t *out = nullptr)
 {
 	PROF_SCOPE(21);
 	Word16 sh = 4, t;
+	if (!out)
+		out = sp;
 #if defined(MELPE_OPCOUNT)
 	/* census build: the reference's passes */
 	int16_t tb[PITCHMAX + 8];
 	v_equ_shr(tb, sp, sh, len);
 	Word32 msq = L_v_magsq(tb, len, 0, 1);
+	(void) msq0;
 #else
 	/* L_v_magsq(tb, len, 0, 1) of tb = sp >> 4: its final shift is 0 */
-	Word32 msq = magsq_shr(sp, len, sh);
+	Word32 msq = msq0 >= 0 ? msq0 : magsq_shr(sp, len, sh);
 #endif
 	if (msq) {
 		t = sub(norm_l(msq), 1);
@@ -139,12 +146,12 @@ MN void scale_adj(DecState *D, int16_t *sp, Word16 gain, int len, Word16 over, W
 		t = extract_h(L_shl(L_mult(t, inv_over), 1));
 		Word32 i2 = L_mult(scale, t);
 		Word32 s = extract_h(L_add(i1, i2));
-		sp[i - 1] = extract_h(L_shl(L_mult(sp[i - 1], (Word16) s), 2));
+		out[i - 1] = extract_h(L_shl(L_mult(sp[i - 1], (Word16) s), 2));
 	}
 #if defined(MELPE_OPCOUNT)
 	v_scale_shl(&sp[over - 1], scale, (int16_t) (len - over + 1), 2);
 #else
-	v_batch(&sp[over - 1], &sp[over - 1], len - over + 1, [scale](int, int16_t x) {
+	v_batch(&sp[over - 1], &out[over - 1], len - over + 1, [scale](int, int16_t x) {
 		return (int16_t) extract_h(L_shl(L_mult(x, scale), 2));	/* v_scale_shl :462 */
 	});
 #endif
@@ -1343,6 +1350,102 @@ MN void postfilt(DecState *D, int16_t *sp, const int16_t *prev_lsf, const int16_
 /* ------------------------------------------------------------------ */
 /* R24: the reference's rate == RATE2400 frame (melp_syn.c:213: the
  * unvoiced-frame parameter override is 1200 bps only) */
+/* One pitch period's synthesis filters (melp_syn.c:395-428) in one pass
+ * over its samples, in place on s[0 .. len): v_scale(pulse_gain), lpc_syn
+ * (ase_den, memory ase_del), zerflt(ase_num; its history the same ase_del),
+ * zerflt_Q(tilt, memory tilt_del), lpc_syn(lpc, memory lpc_del).  Filter k
+ * at sample i needs only filter k-1's samples <= i and its own past, so
+ * interleaving them sample by sample equals the reference's five in-place
+ * passes; each sample's L_mac / L_msu chain is the reference's, in its tap
+ * order.  The delay lines ride in registers (no history copies through
+ * scratch), the inputs come a block ahead.  Returns the first energy of
+ * scale_adj (L_v_magsq of the outputs >> 4), summed as they leave.
+ * DBL: no coefficient is MIN16, so L_mac / L_msu are a 24-bit multiply by
+ * the doubled coefficient and one clamped add (2c fits; 2xc cannot clamp). */
+template <bool DBL>
+MD Word32 syn_chain_t(DecState *D, int16_t *s, int len, Word16 pulse_gain, const int16_t *aden,
+		      const int16_t *anum, const int16_t *tilt, const int16_t *lpc)
+{
+	int32_t cd[LPC_ORD], cn[LPC_ORD + 1], cl[LPC_ORD], ct0, ct1;
+	int16_t w[LPC_ORD], v[LPC_ORD];	/* y2[i-1-k] (lpc_syn 1 / zerflt), y5[i-1-k] */
+#pragma unroll
+	for (int k = 0; k < LPC_ORD; k++) {
+		cd[k] = DBL ? 2 * (int32_t) aden[k] : aden[k];
+		cl[k] = DBL ? 2 * (int32_t) lpc[k] : lpc[k];
+		w[k] = D->ase_del[LPC_ORD - 1 - k];
+		v[k] = D->lpc_del[LPC_ORD - 1 - k];
+	}
+#pragma unroll
+	for (int k = 0; k <= LPC_ORD; k++)
+		cn[k] = DBL ? 2 * (int32_t) anum[k] : anum[k];
+	ct0 = DBL ? 2 * (int32_t) tilt[0] : tilt[0];
+	ct1 = DBL ? 2 * (int32_t) tilt[1] : tilt[1];
+	int16_t y3p = D->tilt_del[0];
+	Word32 e = 0;
+	auto msu = [&](Word32 acc, int16_t x, int32_t c) {
+		return DBL ? sat_sub32(acc, (int32_t) x * c) : L_msu(acc, x, (Word16) c);
+	};
+	auto mac = [&](Word32 acc, int16_t x, int32_t c) {
+		return DBL ? sat_add32(acc, (int32_t) x * c) : L_mac(acc, x, (Word16) c);
+	};
+	v_batch(s, s, len, [&](int, int16_t x0) {
+		const int16_t x1 = mult(x0, pulse_gain);
+		/* lpc_syn(aden): y2 */
+		Word32 acc = L_shr(L_deposit_h(x1), 3);
+#pragma unroll
+		for (int i = LPC_ORD; i > 0; i--)
+			acc = msu(acc, w[i - 1], cd[i - 1]);
+		const int16_t y2 = r_ound(L_shl(acc, 3));
+		/* zerflt(anum, Q12): y3 over y2[i .. i-10] */
+		acc = mac(0, y2, cn[0]);
+#pragma unroll
+		for (int j = 1; j <= LPC_ORD; j++)
+			acc = mac(acc, w[j - 1], cn[j]);
+		const int16_t y3 = r_ound(L_shl(acc, 3));
+#pragma unroll
+		for (int k = LPC_ORD - 1; k > 0; k--)
+			w[k] = w[k - 1];
+		w[0] = y2;
+		/* zerflt_Q(tilt, order 1, Q15): y4 */
+		acc = mac(mac(0, y3, ct0), y3p, ct1);
+		const int16_t y4 = r_ound(acc);
+		y3p = y3;
+		/* lpc_syn(lpc): y5 */
+		acc = L_shr(L_deposit_h(y4), 3);
+#pragma unroll
+		for (int i = LPC_ORD; i > 0; i--)
+			acc = msu(acc, v[i - 1], cl[i - 1]);
+		const int16_t y5 = r_ound(L_shl(acc, 3));
+#pragma unroll
+		for (int k = LPC_ORD - 1; k > 0; k--)
+			v[k] = v[k - 1];
+		v[0] = y5;
+		const Word16 t = shr(y5, 4);	/* scale_adj's first energy */
+		e = L_mac(e, t, t);
+		return y5;
+	});
+#pragma unroll
+	for (int k = 0; k < LPC_ORD; k++) {
+		D->ase_del[k] = w[LPC_ORD - 1 - k];
+		D->lpc_del[k] = v[LPC_ORD - 1 - k];
+	}
+	D->tilt_del[0] = y3p;
+	return e;
+}
+
+MD Word32 syn_chain(DecState *D, int16_t *s, int len, Word16 pulse_gain, const int16_t *aden,
+		    const int16_t *anum, const int16_t *tilt, const int16_t *lpc)
+{
+	bool dbl = tilt[0] != SW_MIN_ && tilt[1] != SW_MIN_;
+	for (int k = 0; k < LPC_ORD; k++)
+		dbl &= aden[k] != SW_MIN_ && lpc[k] != SW_MIN_;
+	for (int k = 0; k <= LPC_ORD; k++)
+		dbl &= anum[k] != SW_MIN_;
+	if (wave_all(dbl))
+		return syn_chain_t<true>(D, s, len, pulse_gain, aden, anum, tilt, lpc);
+	return syn_chain_t<false>(D, s, len, pulse_gain, aden, anum, tilt, lpc);
+}
+
 template <bool R24>
 MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 {
@@ -1469,6 +1572,16 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 		interp_array(prev->fs_mag, par->fs_mag, &fs_real[1], intfact, NUM_HARM);
 		}
 		harm_syn_pitch(D, fs_real, &sb[BEGIN], fc, len);
+#if !defined(MELPE_OPCOUNT)
+		{
+			/* the filter chain in one pass, then scale_adj writing the
+			 * period straight into the frame's run */
+			Word32 e0 = syn_chain(D, &sb[BEGIN], len, pulse_gain, ase_den, ase_num, tilt_cof, &lpc[1]);
+			scale_adj(D, &sb[BEGIN], gain, len, 10, 26214, e0, &pre[DISP_ORD + sb0 - sb_start]);
+			D->syn_begin = add(sb0, len);
+			continue;
+		}
+#endif
 		v_scale(&sb[BEGIN], pulse_gain, len);
 		v_copy(&sb[BEGIN - LPC_ORD], D->ase_del, LPC_ORD);
 		lpc_syn(&sb[BEGIN], &sb[BEGIN], ase_den, LPC_ORD, len);

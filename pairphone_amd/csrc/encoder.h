@@ -47,6 +47,30 @@ MD void ana_first(EncAna *E)
 MN Word16 global_pitch(const int16_t *speech, int16_t *sb, int16_t *delin, int16_t *delout)
 {
 	Word16 dontcare;
+#if !defined(MELPE_OPCOUNT)
+	/* the copy, the lowpass (memories kept after FRAME samples) and
+	 * f_pitch_scale's energy in one pass, as bpvc_ana's windows; with the
+	 * energy within 32 bits the scale is read lazily (frac_pch) */
+	{
+		int64_t e = 0;
+		auto acc = [&](int, int16_t y) { e += L_mult(y, y); };
+		iir3_s_io(&speech[PITCH_BEG], &sb[LPF_ORD], TB(lpf_den), TB(lpf_num), delin, delout, FRAME, acc);
+		int16_t tin[6], tout[6];
+		v_copy(tin, delin, 6);
+		v_copy(tout, delout, 6);
+		iir3_s_io(&speech[PITCH_BEG + FRAME], &sb[LPF_ORD + FRAME], TB(lpf_den), TB(lpf_num), tin, tout,
+			  PITCH_FR - FRAME, acc);
+		bool ex = true;
+		int lsh = 0;
+		if (e <= (int64_t) LW_MAX_)
+			lsh = shr(norm_l((Word32) e), 1);
+		else
+			f_pitch_scale_e(&sb[LPF_ORD], &sb[LPF_ORD], PITCH_FR, e, &ex);
+		Word16 p = find_pitch(&sb[LPF_ORD + PITCH_FR / 2], &dontcare, 2 * PITCHMIN, PITCHMAX,
+				      PITCHMAX, ex, lsh);
+		return shl(p, 7);
+	}
+#endif
 	v_copy(&sb[LPF_ORD], &speech[PITCH_BEG], PITCH_FR);
 	iir3_s(&sb[LPF_ORD], TB(lpf_den), TB(lpf_num), delin, delout, PITCH_FR, FRAME);
 	bool ex;

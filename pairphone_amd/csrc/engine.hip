@@ -519,11 +519,12 @@ static int stage_get(int dev, size_t bytes, void **out)
  * output is the same bit for bit; the order within a class follows the
  * atomics and is not reproducible, which nothing depends on.
  */
-#define NBIN 128
-static_assert(NBIN < 0xff, "class ids and the not-live mark 0xff must fit the uint8 keys");
+#define NBIN 640	/* the largest class count of any key (MELPE_BIN_KEY 3: 4 x 141) */
+#define NOT_LIVE 0xffff	/* the key of a channel that is not live */
+static_assert(NBIN < NOT_LIVE, "class ids and the not-live mark must fit the uint16 keys");
 struct BinBuf {
 	int *perm = nullptr;	/* [C] lane -> channel */
-	uint8_t *key = nullptr;	/* [C] class of each channel (0xff: not live) */
+	uint16_t *key = nullptr;	/* [C] class of each channel (NOT_LIVE: not live) */
 	/* [0, NBIN) counts, [NBIN, 2 NBIN) next slot of each class, [2 NBIN]
 	 * the live count, [2 NBIN + 1] the mapping the last analysis launch ran
 	 * (AnaGate tag: 1 lane, 4 four-wave; 0 none yet) */
@@ -539,8 +540,9 @@ struct BinBuf {
 static hipError_t bin_alloc(BinBuf *b, int channels)
 {
 	size_t pb = sizeof(int) * (size_t) channels, cb = sizeof(unsigned) * (2 * NBIN + 4);
+	const size_t kb = sizeof(uint16_t) * (size_t) channels;
 	char *p = nullptr;
-	hipError_t er = hipMalloc(&p, pb + cb + (size_t) channels);
+	hipError_t er = hipMalloc(&p, pb + cb + kb);
 	if (er != hipSuccess)
 		return er;
 	er = hipEventCreateWithFlags(&b->done, hipEventDisableTiming);
@@ -550,7 +552,7 @@ static hipError_t bin_alloc(BinBuf *b, int channels)
 	}
 	b->perm = (int *) p;
 	b->ctl = (unsigned *) (p + pb);
-	b->key = (uint8_t *) (p + pb + cb);
+	b->key = (uint16_t *) (p + pb + cb);
 	return hipMemset(b->ctl, 0, cb);
 }
 
@@ -571,7 +573,13 @@ __device__ __forceinline__ int bin_class(const char *rec, int off_par, int off_u
 	int b;
 	if (mode == 1) {
 		b = ((p[0] + p[1] + p[2]) / 3 - 20) / 2;
-		return b < 0 ? 0 : (b > NBIN - 1 ? NBIN - 1 : b);
+		return b < 0 ? 0 : (b > 127 ? 127 : b);
+	}
+	if (mode == 3 || mode == 4) {	/* voiced count x last pitch in 1- / 2-sample steps */
+		const int step = mode == 3 ? 1 : 2, nc = 141 / step + 1;
+		b = (p[NF - 1] - 20) / step;
+		b = b < 0 ? 0 : (b > nc - 1 ? nc - 1 : b);
+		return nv * nc + b;
 	}
 	if (mode == 2) {
 		b = (p[NF - 1] - 20) / 5;
@@ -593,12 +601,12 @@ __global__ __launch_bounds__(256) void k_bin_count(const char *rec, size_t strid
 	__syncthreads();
 	int c = blockIdx.x * blockDim.x + threadIdx.x;
 	if (c < n) {
-		int k = 0xff;
+		int k = NOT_LIVE;
 		if (!active || active[c]) {
 			k = bin_class(rec + (size_t) c * stride, off_par, off_uv, mode);
 			atomicAdd(&cnt[k], 1u);
 		}
-		b.key[c] = (uint8_t) k;
+		b.key[c] = (uint16_t) k;
 	}
 	__syncthreads();
 	for (int k = threadIdx.x; k < NBIN; k += blockDim.x)
@@ -626,16 +634,16 @@ __global__ __launch_bounds__(256) void k_bin_scatter(int n, BinBuf b)
 		cnt[k] = 0;
 	__syncthreads();
 	int c = blockIdx.x * blockDim.x + threadIdx.x;
-	int k = c < n ? b.key[c] : 0xff;
+	int k = c < n ? b.key[c] : NOT_LIVE;
 	unsigned r = 0;
-	if (k != 0xff)
+	if (k != NOT_LIVE)
 		r = atomicAdd(&cnt[k], 1u);
 	__syncthreads();
 	for (int j = threadIdx.x; j < NBIN; j += blockDim.x)
 		if (cnt[j])
 			base[j] = atomicAdd(&b.ctl[NBIN + j], cnt[j]);
 	__syncthreads();
-	if (k != 0xff)
+	if (k != NOT_LIVE)
 		b.perm[base[k] + r] = c;
 }
 
