@@ -558,11 +558,12 @@ static hipError_t bin_alloc(BinBuf *b, int channels)
 
 /* the class of one record, from its last superframe: the voiced frames
  * (quant_par uv_flag, 0 = voiced) and the pitch (Q7) of its frames.
- * Default: voiced count x last pitch in 3-sample steps (128 classes).
- * MELPE_BIN_KEY (diagnostics) 1 = mean pitch in 2-sample steps, 2 = voiced
- * count x last pitch in 5-sample steps; on MI355X at 262,144 channels the
- * default was best for both kernels (k_enc_ana 39.8 / 41.5 / 39.9 ms,
- * k_decode 19.0 / 19.2 / 19.2 ms, profiles/r02_binkey_{vp3,mean2,vp5}_*). */
+ * MELPE_BIN_KEY: 3 (default) = voiced count x last pitch in 1-sample steps
+ * (568 classes), 4 = the same in 2-sample steps, 0 = in 3-sample steps (the
+ * round-2 key), 1 = mean pitch in 2-sample steps, 2 = voiced count x last
+ * pitch in 5-sample steps.  Round 5, MI355X, 262,144 channels, two runs
+ * each (profiles/r05_s_keys.txt): k_decode 8.52 -> 8.39 ms and the analysis
+ * 31.11 -> 31.01 ms from key 0 to key 3. */
 __device__ __forceinline__ int bin_class(const char *rec, int off_par, int off_uv, int mode)
 {
 	const int16_t *uv = (const int16_t *) (rec + off_uv);
@@ -664,7 +665,7 @@ static int bin_key_mode(void)
 	static int v = -1;
 	if (v < 0) {
 		const char *s = getenv("MELPE_BIN_KEY");
-		v = s ? atoi(s) : 0;
+		v = s ? atoi(s) : 3;
 	}
 	return v;
 }
