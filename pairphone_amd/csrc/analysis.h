@@ -28,11 +28,20 @@ MD void dc_rmv(const int16_t *in, int16_t *out, int16_t *din, int16_t *dhi,
 	iir3_d(in, out, TB(dc_den), TB(dc_num), din, dhi, dlo, n);
 }
 
-/* remove_dc :261 */
-MN void remove_dc(const int16_t *in, int16_t *out, int16_t len)
+/* remove_dc's offset from the sample sum (an L_add chain of int16 over at
+ * most PIT_COR_LEN terms: never clamps) */
+MD Word16 remove_dc_off(Word32 sum, int16_t len)
 {
 	Word16 up = sub(15, norm_s(len));
 	Word16 pdown = shl(1, sub(up, 1));
+	sum = L_shr(sum, up);
+	Word16 off = mult(extract_l(sum), divide_s(pdown, len));
+	return shl(off, 1);
+}
+
+/* remove_dc :261 */
+MN void remove_dc(const int16_t *in, int16_t *out, int16_t len)
+{
 	Word32 sum = 0;
 	P16 r;
 	int np = p16_open(r, in, len);
@@ -45,26 +54,17 @@ MN void remove_dc(const int16_t *in, int16_t *out, int16_t len)
 	}
 	for (; i < len; i++)
 		sum = L_add(sum, L_deposit_l(in[i]));
-	sum = L_shr(sum, up);
-	Word16 off = mult(extract_l(sum), divide_s(pdown, len));
-	off = shl(off, 1);
-	np = p16_open(r, in, len);
-	i = 0;
-	#pragma unroll 4
-	for (int k = 0; k < np; k++, i += 2) {
-		uint32_t x = p16_next(r);
-		out[i] = sub(lo16(x), off);
-		out[i + 1] = sub(hi16(x), off);
-	}
-	for (; i < len; i++)
-		out[i] = sub(in[i], off);
+	const Word16 off = remove_dc_off(sum, len);
+	v_batch(in, out, len, [off](int, int16_t x) { return sub(x, off); });
 }
 
 /* gain_ana :311 -- pitch-adaptive RMS in dB (Q8) */
 MN Word16 gain_ana(const int16_t *sig, Word16 pitch, Word16 minlen, Word16 maxlen)
 {
 	PROF_SCOPE(23);
+#if defined(MELPE_OPCOUNT)
 	int16_t tb[PITCHMAX * 2 + 8];
+#endif
 	Word16 pq6 = shr(pitch, 1);
 	Word16 tmin = shl(minlen, 6);
 	Word16 fl = pq6;
@@ -75,8 +75,15 @@ MN Word16 gain_ana(const int16_t *sig, Word16 pitch, Word16 minlen, Word16 maxle
 		len = shr(len, 1);
 	Word16 beg = negate(shr(len, 1));
 	Word16 sc = 3;
+#if defined(MELPE_OPCOUNT)
 	v_equ_shr(tb, &sig[beg], sc, len);
 	Word32 e = L_v_magsq(tb, len, 0, 1);
+#else
+	/* both energies straight from sig with the shift applied per sample
+	 * (magsq_shr): the same L_mac chains as L_v_magsq over the shifted
+	 * copies, without writing them */
+	Word32 e = magsq_shr(&sig[beg], len, sc);
+#endif
 	if (e) {
 		sc = sub(sc, shr(norm_l(e), 1));
 		if (sc < 0)
@@ -84,12 +91,16 @@ MN Word16 gain_ana(const int16_t *sig, Word16 pitch, Word16 minlen, Word16 maxle
 	} else {
 		sc = 0;
 	}
+	Word16 g, t1, t2;
+#if defined(MELPE_OPCOUNT)
 	if (sc)
 		v_equ_shr(tb, &sig[beg], sc, len);
 	else
 		v_copy(tb, &sig[beg], len);
-	Word16 g, t1, t2;
 	e = L_v_magsq(tb, len, 0, 0);
+#else
+	e = L_shr(magsq_shr(&sig[beg], len, sc), 1);
+#endif
 	if (sc) {
 		t1 = L_log10_fxp(e, 0);
 		t2 = L_log10_fxp(L_deposit_l(len), 0);
@@ -1054,6 +1065,49 @@ MD int64_t bp_window(int16_t *hist, const int16_t *sp, int16_t *w, const int16_t
 	PROF_SCOPE(47);
 	const int H = PITCH_FR - FRAME;	/* 141 */
 	int64_t e = 0;
+#if MELPE_VBATCH_PAIRS
+	/* hist and w dword-aligned: both moved two samples per access */
+	{
+		const u32_alias *hs = reinterpret_cast<const u32_alias *>(hist);
+		u32_alias *wd = reinterpret_cast<u32_alias *>(w);
+		int k = 0;
+		#pragma unroll 1
+		for (; k + 8 <= H / 2; k += 8) {
+			uint32_t v[8];
+			#pragma unroll
+			for (int q = 0; q < 8; q++)
+				v[q] = hs[k + q];
+			#pragma unroll
+			for (int q = 0; q < 8; q++) {
+				wd[k + q] = v[q];
+				e += L_mult(lo16(v[q]), lo16(v[q])) + (int64_t) L_mult(hi16(v[q]), hi16(v[q]));
+			}
+		}
+		for (; k < H / 2; k++) {
+			const uint32_t v = hs[k];
+			wd[k] = v;
+			e += L_mult(lo16(v), lo16(v)) + (int64_t) L_mult(hi16(v), hi16(v));
+		}
+		const int16_t v = hist[H - 1];
+		w[H - 1] = v;
+		e += L_mult(v, v);
+	}
+	/* the new history written back in pairs as it is produced */
+	uint32_t pend = 0;
+	iir3_s_io(sp, w + H, den, num, din, dout, FRAME, [&](int n, int16_t y) {
+		e += L_mult(y, y);
+		const int m = n - (FRAME - H);
+		if (m >= 0) {
+			if (m & 1)
+				reinterpret_cast<u32_alias *>(hist)[m >> 1] = pend | ((uint32_t) (uint16_t) y << 16);
+			else if (m == H - 1)
+				hist[m] = y;
+			else
+				pend = (uint16_t) y;
+		}
+	});
+	return e;
+#else
 	int k = 0;
 	#pragma unroll 1
 	for (; k + 8 <= H; k += 8) {	/* eight loads issued together */
@@ -1078,6 +1132,7 @@ MD int64_t bp_window(int16_t *hist, const int16_t *sp, int16_t *w, const int16_t
 			hist[n - (FRAME - H)] = y;
 	});
 	return e;
+#endif
 }
 
 /* band 0 of bpvc_ana (melp_sub.c:104-135): the lowest band's window, the
@@ -1086,7 +1141,7 @@ MD int64_t bp_window(int16_t *hist, const int16_t *sp, int16_t *w, const int16_t
 MN void bpvc_band0(EncAna *E, const int16_t *speech, const int16_t *fpitch, int16_t *bpvc0,
 		   Word16 *pitch)
 {
-	int16_t sb[BPF_ORD + PITCH_FR];
+	alignas(4) int16_t sb[BPF_ORD + PITCH_FR];	/* w = sb + BPF_ORD dword-aligned */
 	Word16 pcorr, t;
 	BandState *B = &E->band[0];
 	const int16_t *sp = &speech[PITCH_FR - FRAME - PITCHMAX];
@@ -1117,7 +1172,7 @@ MN void bpvc_band0(EncAna *E, const int16_t *speech, const int16_t *fpitch, int1
  * PITCHMAX for bpvc_ana's `speech`). */
 MN void bpvc_band_s(BandState *B, const int16_t *sp, int i, Word16 pitch, int16_t *bpvci)
 {
-	int16_t sb[BPF_ORD + PITCH_FR];
+	alignas(4) int16_t sb[BPF_ORD + PITCH_FR];	/* w = sb + BPF_ORD dword-aligned */
 	Word16 pcorr, t, sc;
 	int16_t *w = &sb[BPF_ORD];
 	const int fi = i * (BPF_ORD / 2) * 3;
@@ -1380,7 +1435,7 @@ struct CpLags {
 MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
 {
 	PROF_SCOPE(32);
-	int16_t pb[PIT_COR_LEN];
+	alignas(4) int16_t pb[PIT_COR_LEN];
 	const int PW = PIT_COR_LEN - MAXPITCH;	/* 73 */
 	remove_dc(in, pb, PIT_COR_LEN);
 	Word40 r0 = 0, rk = 0, A = 0;
@@ -1686,6 +1741,34 @@ MN Word16 pitLookahead(PitTrack *pt, int num)
 /* ------------------------------------------------------------------ */
 
 /* zeroCrosCount :404 */
+#if !defined(MELPE_OPCOUNT)
+/* zeroCrosCount given the subframe's sample sum: the signs of sp[i] - off
+ * taken as the samples are read (pairs), the dc-free copy never written */
+MN Word16 zeroCrosCount_s(const int16_t *sp, Word32 sum)
+{
+	const Word16 off = remove_dc_off(sum, PIT_SUBFRAME);
+	Word16 cnt = 0;
+	int ps = sub(sp[0], off) >= 0 ? 1 : -1;
+	auto step = [&](int16_t x) {
+		int cs = sub(x, off) >= 0 ? 1 : -1;
+		cnt += ps + cs == 0;
+		ps = cs;
+	};
+	P16 r;
+	int np = p16_open(r, sp + 1, PIT_SUBFRAME - 1);
+	int i = 1;
+	#pragma unroll 4
+	for (int k = 0; k < np; k++, i += 2) {
+		uint32_t x = p16_next(r);
+		step(lo16(x));
+		step(hi16(x));
+	}
+	for (; i < PIT_SUBFRAME; i++)
+		step(sp[i]);
+	return divide_s(cnt, PIT_SUBFRAME);
+}
+#endif
+
 MN Word16 zeroCrosCount(const int16_t *sp)
 {
 	int16_t d[PIT_SUBFRAME];
@@ -1939,8 +2022,12 @@ MN void classify(EncAna *E, const int16_t *in, ClassParam *cs, const int16_t *ac
 	PROF_SCOPE(6);
 	/* so[2..222): the band-passed signal frac_cor reads; so[2..132) is
 	 * the previous call's tail (back_sigbuf) except on the first call */
-	int16_t so[BPF_ORD / 3 + PIT_COR_LEN];
+	alignas(4) int16_t so[BPF_ORD / 3 + PIT_COR_LEN];	/* so + 2 dword-aligned */
+#if defined(MELPE_OPCOUNT)
 	int16_t insp[PIT_SUBFRAME];
+#else
+	int16_t *insp = nullptr;
+#endif
 	const bool first = !E->cls.cls_started;
 	const int KEEP = PIT_COR_LEN - PIT_SUBFRAME;	/* 130 */
 	const int16_t *x;
@@ -1999,6 +2086,7 @@ MN void classify(EncAna *E, const int16_t *in, ClassParam *cs, const int16_t *ac
 
 	Word16 mx = 0, t1, t2, sh1 = 0;
 	Word32 L1, L2 = 0;
+#if defined(MELPE_OPCOUNT)
 	for (int i = 0; i < PIT_SUBFRAME; i++) {
 		t1 = abs_s(in[i]);
 		if (mx < t1)
@@ -2015,6 +2103,45 @@ MN void classify(EncAna *E, const int16_t *in, ClassParam *cs, const int16_t *ac
 		L1 = L_v_magsq(insp, PIT_SUBFRAME, 0, 0);
 		sh1 = 6;
 	}
+#else
+	/* one pass over the subframe (pairs) for the peak, the sum of |x|, both
+	 * energy candidates (the L_mac chains of x^2 and of (x >> 3)^2, each in
+	 * index order as L_v_magsq over in / insp) and zeroCrosCount's sample
+	 * sum; the samples are read once more for the zero crossings */
+	(void) insp;
+	Word32 q0 = 0, q3 = 0, S = 0;
+	{
+		auto step = [&](int16_t x) {
+			t1 = abs_s(x);
+			mx = mx < t1 ? t1 : mx;
+			L2 += t1;	/* <= 90 * 32768: L_add never clamps */
+			S += x;
+			q0 = L_mac(q0, x, x);
+			const Word16 u = shr(x, 3);
+			q3 = L_mac(q3, u, u);
+		};
+		P16 r;
+		int np = p16_open(r, in, PIT_SUBFRAME);
+		int i = 0;
+		#pragma unroll 3
+		for (int k = 0; k < np; k++, i += 2) {
+			uint32_t x = p16_next(r);
+			step(lo16(x));
+			step(hi16(x));
+		}
+		for (; i < PIT_SUBFRAME; i++)
+			step(in[i]);
+	}
+	if (mx == 0) {
+		L1 = 0;
+	} else if (mx <= 4884) {
+		L1 = L_shr(q0, 1);
+		sh1 = 0;
+	} else {
+		L1 = L_shr(q3, 1);
+		sh1 = 6;
+	}
+#endif
 	while (L1 > SW_MAX_) {
 		L1 = L_shr(L1, 2);
 		sh1 = add(sh1, 2);
@@ -2026,7 +2153,11 @@ MN void classify(EncAna *E, const int16_t *in, ClassParam *cs, const int16_t *ac
 		t2 = extract_l(L_shr(L_mult(617, sh1), 1));
 		cs->subEnergy = add(t1, t2);
 	}
+#if defined(MELPE_OPCOUNT)
 	cs->zeroCrosRate = zeroCrosCount(in);
+#else
+	cs->zeroCrosRate = zeroCrosCount_s(in, S);
+#endif
 	if (L2 == 0) {
 		cs->peakiness = 2048;
 	} else {

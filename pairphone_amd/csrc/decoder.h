@@ -70,29 +70,6 @@ MN void noise_sup(int16_t *gain, Word16 ng, Word16 max_noise, Word16 max_att, Wo
 
 /* scale_adj :768 -- match the period's energy to the target gain with a
  * SCALEOVER-sample cross-fade from the previous scale */
-/* L_mac chain of shr(a[i], sh) squared, i = 0 .. n-1: L_v_magsq of the
- * shifted copy the reference builds (v_equ_shr then L_v_magsq, its final
- * shift left to the caller), read straight from a[] in pairs */
-MD Word32 magsq_shr(const int16_t *a, int n, Word16 sh)
-{
-	Word32 acc = 0;
-	P16 ra;
-	int np = p16_open(ra, a, n);
-	int i = 0;
-#pragma unroll 8
-	for (int k = 0; k < np; k++, i += 2) {
-		uint32_t x = p16_next(ra);
-		const Word16 t0 = shr(lo16(x), sh), t1 = shr(hi16(x), sh);
-		acc = L_mac(acc, t0, t0);
-		acc = L_mac(acc, t1, t1);
-	}
-	for (; i < n; i++) {
-		const Word16 t = shr(a[i], sh);
-		acc = L_mac(acc, t, t);
-	}
-	return acc;
-}
-
 /* scale_adj; msq0 >= 0: the first energy (L_v_magsq of sp >> 4), already
  * summed by the caller (syn_chain); out: where the scaled samples go (sp
  * itself, or the caller's next buffer, which saves a copy pass) */

@@ -437,6 +437,31 @@ MD int32_t magsq_pairs(const int16_t *p, int n)
 	return acc0 + acc1;
 }
 
+/* L_mac chain of shr(a[i], sh) squared, i = 0 .. n-1, read straight from
+ * a[] in pairs: L_v_magsq (mat_lib.c:358) of the shifted copy the reference
+ * builds with v_equ_shr, without writing it; equal to L_v_magsq(tb, n, 0,
+ * 1) (final shift 0), and to L_v_magsq(tb, n, 0, 0) once shifted right by 1
+ * (decoder scale_adj, analysis gain_ana) */
+MD Word32 magsq_shr(const int16_t *a, int n, Word16 sh)
+{
+	Word32 acc = 0;
+	P16 ra;
+	int np = p16_open(ra, a, n);
+	int i = 0;
+#pragma unroll 8
+	for (int k = 0; k < np; k++, i += 2) {
+		uint32_t x = p16_next(ra);
+		const Word16 t0 = shr(lo16(x), sh), t1 = shr(hi16(x), sh);
+		acc = L_mac(acc, t0, t0);
+		acc = L_mac(acc, t1, t1);
+	}
+	for (; i < n; i++) {
+		const Word16 t = shr(a[i], sh);
+		acc = L_mac(acc, t, t);
+	}
+	return acc;
+}
+
 /* ------------------------------------------------------------------ */
 /* vectors: melpe/mat_lib.c                                           */
 /* ------------------------------------------------------------------ */
@@ -500,10 +525,76 @@ MD void v_map(int16_t *d, const int16_t *s, int n, F f)
  * the same array, or out lies below in (a shift down: every in[j] is read
  * before out[j] can overwrite it); a copy upward into an overlapping range
  * runs element by element, as the reference's forward loop. */
+#ifndef MELPE_VBATCH_PAIRS
+#define MELPE_VBATCH_PAIRS 1
+#endif
 template <int B = 8, class F>
 MD void v_batch(const int16_t *in, int16_t *out, int n, F f)
 {
 	int i = 0;
+#if MELPE_VBATCH_PAIRS
+	/* Paired form: the private segment is interleaved per dword across the
+	 * wave, so a 2-byte access costs the vector memory pipeline as much as a
+	 * 4-byte one.  Inputs come two per dword (P16, any alignment), B / 2
+	 * dwords a block ahead; outputs go out as dwords after a one-sample head
+	 * when out starts at an odd sample.  Same order of f calls, same
+	 * overlap rules (reads run ahead of writes by at least a block). */
+	if (n >= 2 * B + 1 && !(out > in && out < in + n)) {
+		constexpr int Q = B / 2;
+		if ((reinterpret_cast<uintptr_t>(out) >> 1) & 1) {
+			out[0] = f(0, in[0]);
+			i = 1;
+		}
+		P16 r;
+		const int np = p16_open(r, in + i, n - i);
+		u32_alias *dw = reinterpret_cast<u32_alias *>(out + i);
+		if (np >= 2 * Q) {
+			uint32_t v[Q];
+			#pragma unroll
+			for (int q = 0; q < Q; q++)
+				v[q] = p16_next(r);
+			int k = 0;
+			#pragma unroll 1
+			for (; k + 2 * Q <= np; k += Q) {
+				uint32_t nv[Q];
+				#pragma unroll
+				for (int q = 0; q < Q; q++)
+					nv[q] = p16_next(r);
+				#pragma unroll
+				for (int q = 0; q < Q; q++) {
+					const uint32_t y0 = (uint16_t) f(i + 2 * q, lo16(v[q]));
+					const uint32_t y1 = (uint16_t) f(i + 2 * q + 1, hi16(v[q]));
+					dw[k + q] = y0 | (y1 << 16);
+				}
+				i += 2 * Q;
+				#pragma unroll
+				for (int q = 0; q < Q; q++)
+					v[q] = nv[q];
+			}
+			#pragma unroll
+			for (int q = 0; q < Q; q++) {
+				const uint32_t y0 = (uint16_t) f(i + 2 * q, lo16(v[q]));
+				const uint32_t y1 = (uint16_t) f(i + 2 * q + 1, hi16(v[q]));
+				dw[k + q] = y0 | (y1 << 16);
+			}
+			i += 2 * Q;
+			k += Q;
+			for (; k < np; k++, i += 2) {
+				const uint32_t x = p16_next(r);
+				const uint32_t y0 = (uint16_t) f(i, lo16(x));
+				const uint32_t y1 = (uint16_t) f(i + 1, hi16(x));
+				dw[k] = y0 | (y1 << 16);
+			}
+		} else {
+			for (int k = 0; k < np; k++, i += 2) {
+				const uint32_t x = p16_next(r);
+				const uint32_t y0 = (uint16_t) f(i, lo16(x));
+				const uint32_t y1 = (uint16_t) f(i + 1, hi16(x));
+				dw[k] = y0 | (y1 << 16);
+			}
+		}
+	}
+#else
 	if (n >= 2 * B && !(out > in && out < in + n)) {
 		int16_t v[B];
 		#pragma unroll
@@ -527,6 +618,7 @@ MD void v_batch(const int16_t *in, int16_t *out, int n, F f)
 			out[i + q] = f(i + q, v[q]);
 		i += B;
 	}
+#endif
 	for (; i < n; i++)
 		out[i] = f(i, in[i]);
 }
