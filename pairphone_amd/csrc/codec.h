@@ -27,6 +27,16 @@ MD void derive_all(DerivedTables *d)
 	derive_idft_cos(d);
 }
 
+/* g_lspgrid from the derived cosine grid (host side: the device copy is in
+ * constant memory) */
+static inline void derive_lspgrid(const int16_t *lsp_cos, int16_t *grid)
+{
+	for (int b = 0; b < LSPGRID_BLOCKS; b++)
+		for (int u = 0; u < 8; u++)
+			for (int k = 1; k <= 5; k++)
+				grid[40 * b + 5 * u + k - 1] = lsp_cos[(k * (8 * b + u)) & 511];
+}
+
 }  // namespace mlp
 
 #endif

@@ -1911,8 +1911,38 @@ MN void lsp_to_freq(const int16_t *lsp, int16_t *freq, int order)
 	 * independent of the data, so the polynomial values of 8 grid points
 	 * are formed first (their 40 table loads issued together), then the
 	 * sign-change scan walks them in order. */
+#if !defined(MELPE_OPCOUNT)
+	/* order 10: the block's 40 grid values from g_lspgrid, twenty dwords
+	 * at a wave-uniform address (scalar loads), and the five coefficients
+	 * held in registers */
+	const bool grid = p2 == 5;
+	int16_t cf[6];
+	#pragma unroll
+	for (int j = 0; j < 6; j++)
+		cf[j] = j <= p2 ? lsp[j] : (int16_t) 0;
+#endif
 	for (int i0 = 0; i0 <= 256; i0 += 8) {
 		Word32 accs[8];
+#if !defined(MELPE_OPCOUNT)
+		if (grid) {
+			const u32_alias *gw = reinterpret_cast<const u32_alias *>(g_lspgrid) + 5 * (i0 >> 1);
+			uint32_t w[20];
+			#pragma unroll
+			for (int q = 0; q < 20; q++)
+				w[q] = gw[q];
+			#pragma unroll
+			for (int u = 0; u < 8; u++) {
+				Word32 acc = L_mult(cf[5], 8192);
+				#pragma unroll
+				for (int k = 1; k <= 5; k++) {
+					const int n = 5 * u + k - 1;
+					const Word16 c = (n & 1) ? hi16(w[n >> 1]) : lo16(w[n >> 1]);
+					acc = L_add(acc, L_shr(L_mult(cf[5 - k], c), 1));
+				}
+				accs[u] = acc;
+			}
+		} else
+#endif
 		#pragma unroll
 		for (int u = 0; u < 8; u++) {
 			int i = i0 + u;

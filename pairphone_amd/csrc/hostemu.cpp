@@ -58,6 +58,7 @@ int emu_load_tables(const char *path)
 	if (n != MELPE_TABLE_WORDS)
 		return -2;
 	derive_all(&g_der);
+	derive_lspgrid(g_der.lsp_cos, g_lspgrid);
 	return 0;
 }
 

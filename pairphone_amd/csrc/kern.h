@@ -101,6 +101,11 @@ __device__ __forceinline__ void lane_copy_x4(void *dst, const void *src, size_t 
 		k_derive_##name<<<1, WAVE>>>();                                 \
 		MELPE_CHK(hipGetLastError());                                   \
 		MELPE_CHK(hipDeviceSynchronize());                              \
+		int16_t lc_[512], grid_[LSPGRID_BLOCKS * 40];                   \
+		MELPE_CHK(hipMemcpyFromSymbol(lc_, HIP_SYMBOL(g_der), sizeof(lc_), \
+					      offsetof(DerivedTables, lsp_cos))); \
+		derive_lspgrid(lc_, grid_);                                     \
+		MELPE_CHK(hipMemcpyToSymbol(HIP_SYMBOL(g_lspgrid), grid_, sizeof(grid_))); \
 		return 0;                                                       \
 	}                                                                       \
 	MELPE_TU_PROF(name)

@@ -28,6 +28,10 @@ MN void vq_lspw(int16_t *w, const int16_t *lsp, const int16_t *lpc, int order)
 	w[9] = mult(w[9], 5242);
 }
 
+#ifndef MELPE_SROW
+#define MELPE_SROW 7
+#endif
+
 /* vq_enc, melpe/vq_lib.c:474 -- full search, first minimum wins */
 template <int ORDER>
 MN Word32 vq_enc(const int16_t *cb, const int16_t *u_in, int levels, int16_t *uhat,
@@ -41,6 +45,42 @@ MN Word32 vq_enc(const int16_t *cb, const int16_t *u_in, int levels, int16_t *uh
 	int16_t best = 0;
 	Word32 dmin = LW_MAX_;
 	const int16_t *p = cb;
+#if !defined(MELPE_OPCOUNT)
+	/* rows of an even order at an even table offset: ORDER / 2 dwords at a
+	 * wave-uniform address (scalar loads), the next row's issued before
+	 * this one is scored */
+	if ((MELPE_SROW & 1) && !(ORDER & 1) && !((cb - g_tab) & 1)) {
+		uint32_t rw[ORDER / 2 + 1];
+		const u32_alias *r0 = reinterpret_cast<const u32_alias *>(cb);
+		#pragma unroll
+		for (int q = 0; q < ORDER / 2; q++)
+			rw[q] = r0[q];
+		for (int i = 0; i < levels; i++) {
+			int16_t x[ORDER + 1];
+			#pragma unroll
+			for (int q = 0; q < ORDER / 2; q++) {
+				x[2 * q] = lo16(rw[q]);
+				x[2 * q + 1] = hi16(rw[q]);
+			}
+			const int in = i + 1 < levels ? i + 1 : i;
+			const u32_alias *rn = reinterpret_cast<const u32_alias *>(cb + in * ORDER);
+			#pragma unroll
+			for (int q = 0; q < ORDER / 2; q++)
+				rw[q] = rn[q];
+			Word32 d = 0;
+			#pragma unroll
+			for (int j = 0; j < ORDER; j++) {
+				Word16 t = sub(u[j], x[j]);
+				d = L_mac(d, t, t);
+			}
+			if (d < dmin) {
+				dmin = d;
+				best = (int16_t) i;
+			}
+		}
+		p = nullptr;
+	} else
+#endif
 	for (int i = 0; i < levels; i++) {
 		Word32 d = 0;
 #pragma unroll
@@ -138,6 +178,38 @@ MN void wvq1(const int16_t *tgt_in, const int16_t *wt_in, const int16_t *cb, int
 		if (o_lane != uo || cbsize != un)
 			continue;
 		const int16_t *ucb = g_tab + uo;
+#if !defined(MELPE_OPCOUNT)
+		if ((MELPE_SROW & 2) && DIM == 3 && !(uo & 1)) {
+			/* row i at sample 3i: the two dwords holding it, at a
+			 * wave-uniform address (scalar loads), the next row's issued
+			 * before this one is scored; the row starts in the low half
+			 * for even i.  Every term is scored: the terms are
+			 * non-negative and L_add monotone, so the reference's early
+			 * exit never changes whether the entry is kept. */
+			const u32_alias *cw = reinterpret_cast<const u32_alias *>(ucb);
+			uint32_t r0 = cw[0], r1 = cw[1];
+			for (int i = 0; i < un; i++) {
+				const bool odd = i & 1;
+				int16_t x[3];
+				x[0] = odd ? hi16(r0) : lo16(r0);
+				x[1] = odd ? lo16(r1) : hi16(r0);
+				x[2] = odd ? hi16(r1) : lo16(r1);
+				const int in = i + 1 < un ? i + 1 : i;
+				const int d0 = (3 * in) >> 1;
+				r0 = cw[d0];
+				r1 = cw[d0 + 1];
+				Word32 err = 0;
+				#pragma unroll
+				for (int j = 0; j < 3; j++) {
+					Word16 t = sub(tgt[j], x[j]);
+					Word32 v = L_add(err, L_shr(L_mult(t, t), 2));
+					err = wt[j] > 0 ? v : err;
+				}
+				wvq1_push(err, i, index, dist, maxd, maxi, cand);
+			}
+			break;
+		}
+#endif
 		for (int i = 0; i < un; i++)
 			wvq1_push(wvq1_err<DIM>(tgt, wt, ucb + i * DIM, maxd), i, index, dist, maxd, maxi,
 				  cand);
@@ -288,6 +360,42 @@ MN void gain_vq(EncAna *E, MelpParam *par)
 	Word32 minErr = LW_MAX_;
 	int16_t idx = 0;
 	Word16 b = 0;
+#if !defined(MELPE_OPCOUNT)
+	/* rows of six at an even offset: three dwords at a wave-uniform address
+	 * (scalar loads), the next row's issued before this one is scored.
+	 * Every row is scored whole: the terms are non-negative and L_add
+	 * monotone, so the reference's skip after the first term (:380) never
+	 * changes which row wins. */
+	static_assert(NF * NUM_GAINFR == 6 && TOFF_gain_vq_cb % 2 == 0, "gain_vq rows as dwords");
+	if (MELPE_SROW & 4) {
+		const u32_alias *cw = reinterpret_cast<const u32_alias *>(cb);
+		uint32_t r[3] = {cw[0], cw[1], cw[2]};
+		for (int i = 0; i < 1024; i++) {
+			int16_t x[6];
+			#pragma unroll
+			for (int q = 0; q < 3; q++) {
+				x[2 * q] = lo16(r[q]);
+				x[2 * q + 1] = hi16(r[q]);
+			}
+			const int in = i + 1 < 1024 ? i + 1 : i;
+			#pragma unroll
+			for (int q = 0; q < 3; q++)
+				r[q] = cw[3 * in + q];
+			Word32 err = 0;
+			#pragma unroll
+			for (int j = 0; j < 6; j++) {
+				Word16 t = sub(tg[j], x[j]);
+				err = L_add(err, L_shr(L_mult(t, t), 3));
+			}
+			if (err < minErr) {
+				minErr = err;
+				idx = (int16_t) i;
+			}
+		}
+		b = 0;
+	}
+	if (!(MELPE_SROW & 4))
+#endif
 	for (int i = 0; i < 1024; i++) {
 		Word16 t = sub(tg[0], cb[b]);
 		Word32 err = L_add(0, L_shr(L_mult(t, t), 3));
@@ -446,8 +554,42 @@ MD void lspVQ_t(const int16_t *target, const int16_t *weight, int16_t *qout, con
 				if (o_lane != uo || n_lane != un)
 					continue;
 				const int16_t *ucb = g_tab + uo;
+#if !defined(MELPE_OPCOUNT)
+				/* Rows of an even dimension at an even table offset are
+				 * dword-aligned: each row comes as DIM / 2 dwords at a
+				 * wave-uniform address (scalar loads), the next row's
+				 * issued before this one is scored */
+				const bool srow = !(uo & 1);
+				uint32_t rw[DIM / 2];
+				if (srow) {
+					const u32_alias *r0 = reinterpret_cast<const u32_alias *>(ucb);
+					#pragma unroll
+					for (int q = 0; q < DIM / 2; q++)
+						rw[q] = r0[q];
+				}
+#endif
 				for (int e = 0; e < un; e++) {
+#if !defined(MELPE_OPCOUNT)
+					Word16 d;
+					if (srow) {
+						int16_t x[DIM];
+						#pragma unroll
+						for (int q = 0; q < DIM / 2; q++) {
+							x[2 * q] = lo16(rw[q]);
+							x[2 * q + 1] = hi16(rw[q]);
+						}
+						const int en = e + 1 < un ? e + 1 : e;
+						const u32_alias *rn = reinterpret_cast<const u32_alias *>(ucb + en * DIM);
+						#pragma unroll
+						for (int q = 0; q < DIM / 2; q++)
+							rw[q] = rn[q];
+						d = WeightedMSE_t<DIM>(wr, x, ct, maxd);
+					} else {
+						d = WeightedMSE_t<DIM>(wr, ucb + e * DIM, ct, maxd);
+					}
+#else
 					Word16 d = WeightedMSE_t<DIM>(wr, ucb + e * DIM, ct, maxd);
+#endif
 					if (d < maxd) {
 						const int32_t dk = (int32_t) d * 65536;
 						const int32_t nk = dk + ((c1 << 9) | e);

@@ -16,7 +16,7 @@
 #include "ops.h"
 #include "tables_gen.h"
 
-MDEV_TAB int16_t g_tab[MELPE_TABLE_WORDS];
+alignas(16) MDEV_TAB int16_t g_tab[MELPE_TABLE_WORDS];	/* codebooks at even offsets: dword rows */
 #define TB(name) ((const int16_t *) (g_tab + TOFF_##name))
 
 struct DerivedTables {
@@ -33,5 +33,15 @@ struct DerivedTables {
 };
 
 MDEV_CONST DerivedTables g_der;
+
+/* lsp_to_freq's grid values in the order its scan reads them:
+ * g_lspgrid[40 b + 5 u + k - 1] = lsp_cos[(k (8 b + u)) mod 512], grid point
+ * i = 8 b + u, term k = 1..5 (order 10).  Data-independent and read at
+ * wave-uniform addresses, so it lives in constant memory and comes through
+ * scalar loads (a block's 40 values in five dwordx4-sized pieces) instead of
+ * one vector load per value; filled from g_der.lsp_cos after the derivation
+ * (derive_lspgrid), on the host. */
+#define LSPGRID_BLOCKS 33	/* 8 b + u covers the 257 points 0..256 */
+alignas(16) MDEV_TAB int16_t g_lspgrid[LSPGRID_BLOCKS * 40];
 
 #endif
