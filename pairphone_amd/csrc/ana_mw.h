@@ -133,8 +133,21 @@ MD void pv_slice(X &xc, D &db, int v)
 		Word32 maxd = LW_MAX_;
 		int maxi = 0, n = 0;
 		const int lo = v * un / MW_NV, hi = (v + 1) * un / MW_NV;
+#if !defined(MELPE_OPCOUNT)
+		static_assert(NF == 3 && TOFF_pitch_vq_cb_vvv % 2 == 0 && TOFF_pitch_vq_cb_uvv % 2 == 0,
+			      "pitch codebooks as Row3 streams");
+		Row3 rs;
+		if (lo < hi)
+			rs.open(ucb, lo);
+#endif
 		for (int i = lo; i < hi; i++) {
+#if !defined(MELPE_OPCOUNT)
+			int16_t x[3];
+			rs.take(i, i + 1 < hi ? i + 1 : i, x);
+			const Word32 err = wvq1_err3(w.tgt, w.wt, x);
+#else
 			const Word32 err = wvq1_err<NF>(w.tgt, w.wt, ucb + i * NF, maxd);
+#endif
 			if (wvq1_push(err, i, il, dl, maxd, maxi, PITCH_VQ_CAND)) {
 				if (n < PV_CAP) {
 					db.put(v * 2 * PV_CAP + 2 * n, (uint32_t) i);

@@ -441,6 +441,19 @@ MD void lq_vq_slice(X &xc, int b, D &db, int v, int cbs, int size, int nc, int s
 		lk[k] = SW_MAX_;
 	int ns = 0;
 	int c1 = -1;
+#if !defined(MELPE_OPCOUNT)
+	/* the rows as dwords at wave-uniform addresses (scalar loads; the lsf
+	 * codebooks' stages start at even offsets), the next visit's row issued
+	 * before this one is scored */
+	const bool srow = !(cbs & 1);
+	uint32_t rw[DIM / 2];
+	if (srow && lo < hi) {
+		const u32_alias *r0 = reinterpret_cast<const u32_alias *>(g_tab + cbs + (lo % size) * DIM);
+	#pragma unroll
+		for (int i = 0; i < DIM / 2; i++)
+			rw[i] = r0[i];
+	}
+#endif
 	for (int u = lo; u < hi; u++) {
 		const int c = u / size, e = u - c * size;
 		if (c != c1) {
@@ -461,7 +474,27 @@ MD void lq_vq_slice(X &xc, int b, D &db, int v, int cbs, int size, int nc, int s
 			for (int i = 0; i < DIM; i++)
 				ct[i] = sub(tgt[i], cand[i]);
 		}
+#if !defined(MELPE_OPCOUNT)
+		uint32_t pr;
+		if (srow) {
+			int16_t x[DIM];
+	#pragma unroll
+			for (int i = 0; i < DIM / 2; i++) {
+				x[2 * i] = lo16(rw[i]);
+				x[2 * i + 1] = hi16(rw[i]);
+			}
+			const int en = (u + 1 < hi) ? (e + 1 < size ? e + 1 : 0) : e;
+			const u32_alias *rn = reinterpret_cast<const u32_alias *>(g_tab + cbs + en * DIM);
+	#pragma unroll
+			for (int i = 0; i < DIM / 2; i++)
+				rw[i] = rn[i];
+			pr = lq_wmse<DIM>(wr, x, ct);
+		} else {
+			pr = lq_wmse<DIM>(wr, g_tab + cbs + e * DIM, ct);
+		}
+#else
 		const uint32_t pr = lq_wmse<DIM>(wr, g_tab + cbs + e * DIM, ct);
+#endif
 		const int16_t h = (int16_t) (pr & 0xffff), f = (int16_t) (pr >> 16);
 		const Word16 lmax = lk[LSP_VQ_CAND - 1];
 		const Word16 d = (h >= lmax) ? (Word16) SW_MAX_ : f;

@@ -135,6 +135,49 @@ MD Word32 wvq1_err(const int16_t *tgt, const int16_t *wt, const int16_t *row, Wo
 	return err;
 }
 
+/* Rows of a 3-wide codebook at an even table offset, read through the
+ * two dwords that hold row i (row i starts in the low half for even i) at
+ * wave-uniform addresses (scalar loads); take() hands out row i and issues
+ * the loads of the next row wanted.  Reads at most one sample past the
+ * codebook's last row, inside g_tab. */
+struct Row3 {
+	const u32_alias *cw;
+	uint32_t r0, r1;
+	MM void open(const int16_t *cb, int i)
+	{
+		cw = reinterpret_cast<const u32_alias *>(cb);
+		const int d = (3 * i) >> 1;
+		r0 = cw[d];
+		r1 = cw[d + 1];
+	}
+	MM void take(int i, int in, int16_t *x)
+	{
+		const bool odd = i & 1;
+		x[0] = odd ? hi16(r0) : lo16(r0);
+		x[1] = odd ? lo16(r1) : hi16(r0);
+		x[2] = odd ? hi16(r1) : lo16(r1);
+		const int d = (3 * in) >> 1;
+		r0 = cw[d];
+		r1 = cw[d + 1];
+	}
+};
+
+/* wvq1's distortion of a row held in registers, every weighted term summed:
+ * the terms are non-negative and L_add monotone, so the reference's early
+ * exit (wvq1_err) never changes whether the entry is kept, and a kept
+ * entry's sum is the full one either way */
+MD Word32 wvq1_err3(const int16_t *tgt, const int16_t *wt, const int16_t *x)
+{
+	Word32 err = 0;
+	#pragma unroll
+	for (int j = 0; j < 3; j++) {
+		Word16 t = sub(tgt[j], x[j]);
+		Word32 v = L_add(err, L_shr(L_mult(t, t), 2));
+		err = wt[j] > 0 ? v : err;
+	}
+	return err;
+}
+
 /* wvq1's update with entry i: it replaces the slot holding the current
  * maximum, then the linear rescan finds the new one (first slot wins).
  * Returns whether the entry was kept. */
@@ -180,32 +223,12 @@ MN void wvq1(const int16_t *tgt_in, const int16_t *wt_in, const int16_t *cb, int
 		const int16_t *ucb = g_tab + uo;
 #if !defined(MELPE_OPCOUNT)
 		if ((MELPE_SROW & 2) && DIM == 3 && !(uo & 1)) {
-			/* row i at sample 3i: the two dwords holding it, at a
-			 * wave-uniform address (scalar loads), the next row's issued
-			 * before this one is scored; the row starts in the low half
-			 * for even i.  Every term is scored: the terms are
-			 * non-negative and L_add monotone, so the reference's early
-			 * exit never changes whether the entry is kept. */
-			const u32_alias *cw = reinterpret_cast<const u32_alias *>(ucb);
-			uint32_t r0 = cw[0], r1 = cw[1];
+			Row3 rs;
+			rs.open(ucb, 0);
 			for (int i = 0; i < un; i++) {
-				const bool odd = i & 1;
 				int16_t x[3];
-				x[0] = odd ? hi16(r0) : lo16(r0);
-				x[1] = odd ? lo16(r1) : hi16(r0);
-				x[2] = odd ? hi16(r1) : lo16(r1);
-				const int in = i + 1 < un ? i + 1 : i;
-				const int d0 = (3 * in) >> 1;
-				r0 = cw[d0];
-				r1 = cw[d0 + 1];
-				Word32 err = 0;
-				#pragma unroll
-				for (int j = 0; j < 3; j++) {
-					Word16 t = sub(tgt[j], x[j]);
-					Word32 v = L_add(err, L_shr(L_mult(t, t), 2));
-					err = wt[j] > 0 ? v : err;
-				}
-				wvq1_push(err, i, index, dist, maxd, maxi, cand);
+				rs.take(i, i + 1 < un ? i + 1 : i, x);
+				wvq1_push(wvq1_err3(tgt, wt, x), i, index, dist, maxd, maxi, cand);
 			}
 			break;
 		}
