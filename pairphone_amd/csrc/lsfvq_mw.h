@@ -608,14 +608,22 @@ MD void lq_interp_slice(X &xc, int b, int v)
 	for (int c = lo; c < hi; c++) {
 		const int k = c >> 4, i = c & 15;
 		Word32 err = 0;
+		/* the pattern's 20 coefficients as ten dwords at a wave-uniform
+		 * address (scalar loads; inpCoef at an even offset) */
+		const u32_alias *ic32 = reinterpret_cast<const u32_alias *>(ic + i * 20);
+		uint32_t fw[10];
+	#pragma unroll
+		for (int q = 0; q < 10; q++)
+			fw[q] = ic32[q];
+	#pragma unroll
 		for (int j = 0; j < LPC_ORD; j++) {
 			const Word16 qp = xc.get(b + XL_IP_QPLSP + j);
 			const Word16 lc = xc.get(b + XL_IP_LCAND + k * LPC_ORD + j);
-			Word16 f = ic[i * 20 + j];
+			Word16 f = (j & 1) ? hi16(fw[j >> 1]) : lo16(fw[j >> 1]);
 			Word32 acc = L_mult(f, qp);
 			acc = L_mac(acc, sub(16384, f), lc);
 			acc = L_sub(acc, L_shl(L_deposit_l(xc.get(b + XL_IP_LSP + j)), 15));
-			f = ic[i * 20 + j + LPC_ORD];
+			f = ((j + LPC_ORD) & 1) ? hi16(fw[(j + LPC_ORD) >> 1]) : lo16(fw[(j + LPC_ORD) >> 1]);
 			Word32 bcc = L_mult(f, qp);
 			bcc = L_mac(bcc, sub(16384, f), lc);
 			bcc = L_sub(bcc, L_shl(L_deposit_l(xc.get(b + XL_IP_LSP + LPC_ORD + j)), 15));

@@ -821,27 +821,41 @@ MN void lsf_vq_u(EncAna *E, MelpParam *par, Word16 uvc)
 					acc = L_sub(acc, L_shl(L_deposit_l(lcand[k][j]), 15));
 					e3 = L_add(e3, lsf_werr(acc, wgt[2][j]));
 				}
-				/* four patterns at a time: their chains in registers */
+				/* four patterns at a time: their chains in registers; j
+				 * in pairs, the coefficients of both as one dword per
+				 * pattern and half at a wave-uniform address (scalar
+				 * loads: inpCoef sits at an even offset, rows of 20) */
+				static_assert(TOFF_inpCoef % 2 == 0 && LPC_ORD % 2 == 0, "inpCoef dwords");
+				const u32_alias *ic32 = reinterpret_cast<const u32_alias *>(ic);
 				#pragma unroll 1
 				for (int i0 = 0; i0 < 16; i0 += 4) {
 					Word32 errs[4] = {e3, e3, e3, e3};
 					#pragma unroll 1
-					for (int j = 0; j < LPC_ORD; j++) {
-						const Word16 qp = E->qplsp[j], lc = lcand[k][j];
-						const Word32 l0 = L_shl(L_deposit_l(lsp(0)[j]), 15);
-						const Word32 l1 = L_shl(L_deposit_l(lsp(1)[j]), 15);
-						const Word16 w0 = wgt[0][j], w1 = wgt[1][j];
+					for (int j0 = 0; j0 < LPC_ORD; j0 += 2) {
+						uint32_t fa[4], fb[4];
 						#pragma unroll
 						for (int q = 0; q < 4; q++) {
-							const int i = i0 + q;
-							Word16 f = ic[i * 20 + j];
-							Word32 acc = L_mac(L_mult(f, qp), sub(16384, f), lc);
-							acc = L_sub(acc, l0);
-							f = ic[i * 20 + j + LPC_ORD];
-							Word32 bcc = L_mac(L_mult(f, qp), sub(16384, f), lc);
-							bcc = L_sub(bcc, l1);
-							errs[q] = L_add(errs[q], lsf_werr(acc, w0));
-							errs[q] = L_add(errs[q], lsf_werr(bcc, w1));
+							fa[q] = ic32[((i0 + q) * 20 + j0) >> 1];
+							fb[q] = ic32[((i0 + q) * 20 + j0 + LPC_ORD) >> 1];
+						}
+						#pragma unroll
+						for (int h = 0; h < 2; h++) {
+							const int j = j0 + h;
+							const Word16 qp = E->qplsp[j], lc = lcand[k][j];
+							const Word32 l0 = L_shl(L_deposit_l(lsp(0)[j]), 15);
+							const Word32 l1 = L_shl(L_deposit_l(lsp(1)[j]), 15);
+							const Word16 w0 = wgt[0][j], w1 = wgt[1][j];
+							#pragma unroll
+							for (int q = 0; q < 4; q++) {
+								Word16 f = h ? hi16(fa[q]) : lo16(fa[q]);
+								Word32 acc = L_mac(L_mult(f, qp), sub(16384, f), lc);
+								acc = L_sub(acc, l0);
+								f = h ? hi16(fb[q]) : lo16(fb[q]);
+								Word32 bcc = L_mac(L_mult(f, qp), sub(16384, f), lc);
+								bcc = L_sub(bcc, l1);
+								errs[q] = L_add(errs[q], lsf_werr(acc, w0));
+								errs[q] = L_add(errs[q], lsf_werr(bcc, w1));
+							}
 						}
 					}
 					#pragma unroll

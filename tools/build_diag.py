@@ -6,6 +6,7 @@ pitch-dependent window reads are the same address on every lane; the
 output is wrong by construction).
 
   python tools/build_diag.py <name> <DEFINE> [<DEFINE> ...]
+  MELPE_DIAG_TU=k_ana_mw python tools/build_diag.py ...   (another TU)
 """
 import os
 import shutil
@@ -17,16 +18,17 @@ from pairphone_amd import build as b  # noqa: E402
 
 
 def main(name, defs):
+    tu = os.environ.get("MELPE_DIAG_TU", "k_ana")
     base = os.path.join(ROOT, "build", "obj", "libmelpe_amd")
-    assert os.path.exists(os.path.join(base, "k_ana.o")), "build the product library first"
+    assert os.path.exists(os.path.join(base, tu + ".o")), "build the product library first"
     os.makedirs(os.path.join(ROOT, "build", "var"), exist_ok=True)
     od = os.path.join(ROOT, "build", "obj", name)
     os.makedirs(od, exist_ok=True)
     for f in os.listdir(base):
-        if f.endswith(".o") and f != "k_ana.o":
+        if f.endswith(".o") and f != tu + ".o":
             shutil.copy2(os.path.join(base, f), os.path.join(od, f))
-    b.build_engine(force=True, out=os.path.join(ROOT, "build", "var", name + ".so"), only=("k_ana",),
-                   tus_defs={"k_ana": list(defs)})
+    b.build_engine(force=True, out=os.path.join(ROOT, "build", "var", name + ".so"), only=(tu,),
+                   tus_defs={tu: list(defs)})
 
 
 if __name__ == "__main__":
