@@ -118,6 +118,35 @@ MD uint32_t lq_wmse(const int16_t *w, const int16_t *x, const int16_t *tgt)
 	return lq_pack(h, r_ound(d));
 }
 
+/* lq_wmse when every weight is >= 0 (WeightedMSE_pos's sums, quant.h) */
+template <int DIM>
+MD uint32_t lq_wmse_pos(const int16_t *w, const int16_t *x, const int16_t *tgt)
+{
+	int16_t m[DIM];
+#pragma unroll
+	for (int i = 0; i < DIM; i++) {
+		const int t = sub(x[i], tgt[i]);
+		const int tt = (t * t) >> 15;
+		m[i] = (int16_t) (tt > SW_MAX_ ? SW_MAX_ : tt);
+	}
+	auto pk = [](int16_t lo, int16_t hi) { return (uint32_t) (uint16_t) lo | ((uint32_t) (uint16_t) hi << 16); };
+	auto dbl = [](int32_t S) { return S >= (1 << 30) ? (Word32) LW_MAX_ : (Word32) (2 * S); };
+	constexpr int H = DIM / 2;
+	int32_t S = 0;
+#pragma unroll
+	for (int i = 0; i < H; i += 2) {
+		const bool one = i + 1 >= H;
+		S = sdot2_sat(pk(w[i], one ? (int16_t) 0 : w[i + 1]), pk(m[i], one ? (int16_t) 0 : m[i + 1]), S);
+	}
+	const Word16 h = r_ound(dbl(S));
+#pragma unroll
+	for (int i = H; i < DIM; i += 2) {
+		const bool one = i + 1 >= DIM;
+		S = sdot2_sat(pk(w[i], one ? (int16_t) 0 : w[i + 1]), pk(m[i], one ? (int16_t) 0 : m[i + 1]), S);
+	}
+	return lq_pack(h, r_ound(dbl(S)));
+}
+
 /* ---------------------------------------------------------------- */
 /* leader                                                           */
 /* ---------------------------------------------------------------- */
@@ -569,7 +598,11 @@ MD void lq_vq_slice_g(X &xc, int b, D &db, int v, int cbs, int size, int nc, int
 			x[2 * i] = (int16_t) (w2 & 0xffff);
 			x[2 * i + 1] = (int16_t) (w2 >> 16);
 		}
+#if !defined(MELPE_OPCOUNT) && MELPE_WMSE_POS
+		const uint32_t pr = all ? lq_wmse<DIM>(wr, x, ct) : lq_wmse_pos<DIM>(wr, x, ct);
+#else
 		const uint32_t pr = lq_wmse<DIM>(wr, x, ct);
+#endif
 		const int16_t h = (int16_t) (pr & 0xffff), f = (int16_t) (pr >> 16);
 		const Word16 lmax = lk[LSP_VQ_CAND - 1];
 		const Word16 d = (h >= lmax) ? (Word16) SW_MAX_ : f;

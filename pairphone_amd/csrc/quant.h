@@ -31,6 +31,9 @@ MN void vq_lspw(int16_t *w, const int16_t *lsp, const int16_t *lpc, int order)
 #ifndef MELPE_SROW
 #define MELPE_SROW 7
 #endif
+#ifndef MELPE_WMSE_POS
+#define MELPE_WMSE_POS 1
+#endif
 
 /* vq_enc, melpe/vq_lib.c:474 -- full search, first minimum wins */
 template <int ORDER>
@@ -513,6 +516,43 @@ MD Word16 WeightedMSE_t(const int16_t *w, const int16_t *x, const int16_t *tgt, 
 	return r_ound(d);
 }
 
+/* WeightedMSE_t when every weight is >= 0: each term L_mult(w, m) with
+ * m = mult(t, t) >= 0 is 2 w m exactly (no saturation: w, m < 2^15), so the
+ * saturating L_mac chain is min(MAX32, 2 S) with S the plain sum of w m,
+ * at the half-way point and at the end.  S comes from saturating
+ * v_dot2_i32_i16 (min(MAX32, S) for non-negative products) and 2 S
+ * saturates exactly when S >= 2^30. */
+template <int DIM>
+MD Word16 WeightedMSE_pos(const int16_t *w, const int16_t *x, const int16_t *tgt, Word16 max_dmin)
+{
+	OPC_ADD(OP_shr, 1);
+	int16_t m[DIM + 1];
+#pragma unroll
+	for (int i = 0; i < DIM; i++) {
+		const int t = sub(x[i], tgt[i]);
+		const int tt = (t * t) >> 15;
+		m[i] = (int16_t) (tt > SW_MAX_ ? SW_MAX_ : tt);
+	}
+	m[DIM] = 0;
+	auto pk = [](int16_t lo, int16_t hi) { return (uint32_t) (uint16_t) lo | ((uint32_t) (uint16_t) hi << 16); };
+	auto dbl = [](int32_t S) { return S >= (1 << 30) ? (Word32) LW_MAX_ : (Word32) (2 * S); };
+	constexpr int H = DIM / 2;
+	int32_t S = 0;
+#pragma unroll
+	for (int i = 0; i < H; i += 2) {
+		const bool one = i + 1 >= H;	/* the half's odd last term alone */
+		S = sdot2_sat(pk(w[i], one ? (int16_t) 0 : w[i + 1]), pk(m[i], one ? (int16_t) 0 : m[i + 1]), S);
+	}
+	if (r_ound(dbl(S)) >= max_dmin)
+		return SW_MAX_;
+#pragma unroll
+	for (int i = H; i < DIM; i += 2) {
+		const bool one = i + 1 >= DIM;
+		S = sdot2_sat(pk(w[i], one ? (int16_t) 0 : w[i + 1]), pk(m[i], one ? (int16_t) 0 : m[i + 1]), S);
+	}
+	return r_ound(dbl(S));
+}
+
 /* lspVQ :482 -- M-best multistage search; qout receives the ncPrev best
  * reconstructions (dim each), cb_index their stage indices (tos each).
  * Specialised per dimension (10: the LSF stages, 20: the interpolation
@@ -527,9 +567,15 @@ MD void lspVQ_t(const int16_t *target, const int16_t *weight, int16_t *qout, con
 	int16_t index[LSP_VQ_CAND][LSP_VQ_STAGES], nextIndex[LSP_VQ_CAND][LSP_VQ_STAGES];
 	int16_t cand[LSP_VQ_CAND][2 * LPC_ORD], dMin[LSP_VQ_CAND];
 	int16_t wr[DIM];
+	bool wpos = true;	/* every weight >= 0: WeightedMSE_pos */
 #pragma unroll
-	for (int i = 0; i < DIM; i++)
+	for (int i = 0; i < DIM; i++) {
 		wr[i] = weight[i];
+		wpos &= wr[i] >= 0;
+	}
+#if defined(MELPE_OPCOUNT) || !MELPE_WMSE_POS
+	wpos = false;
+#endif
 	for (int i = 0; i < LSP_VQ_CAND; i++) {
 		v_zero(cand[i], dim);
 		v_zero(index[i], LSP_VQ_STAGES);
@@ -606,7 +652,8 @@ MD void lspVQ_t(const int16_t *target, const int16_t *weight, int16_t *qout, con
 						#pragma unroll
 						for (int q = 0; q < DIM / 2; q++)
 							rw[q] = rn[q];
-						d = WeightedMSE_t<DIM>(wr, x, ct, maxd);
+						d = wpos ? WeightedMSE_pos<DIM>(wr, x, ct, maxd)
+							 : WeightedMSE_t<DIM>(wr, x, ct, maxd);
 					} else {
 						d = WeightedMSE_t<DIM>(wr, ucb + e * DIM, ct, maxd);
 					}
