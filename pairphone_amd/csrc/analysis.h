@@ -1284,11 +1284,41 @@ MN Word16 updateEn(Word16 prev, Word16 ifact, Word16 curr)
 	return add(prev, t);
 }
 
+/* ivfilt's three autocorrelation sums of the updated lp[0 .. PIT_COR_LEN)
+ * (lags 0, 1, 2; each term 2 x y, as L40_mac): 219 terms of at most 2^31
+ * never reach the 40-bit clamp, so the sums are exact integers and may be
+ * formed in any order -- here while lpfilt moves the history down and
+ * writes the new samples, instead of in a pass of their own */
+struct LpAcor {
+	int64_t a0, a1, a2;
+	int16_t h1, h2;	/* the last two samples seen */
+	int n;
+	MM void add(int16_t x)
+	{
+		a0 += 2 * (int64_t) ((int32_t) x * x);
+		if (n >= 1)
+			a1 += 2 * (int64_t) ((int32_t) x * h1);
+		if (n >= 2)
+			a2 += 2 * (int64_t) ((int32_t) x * h2);
+		h2 = h1;
+		h1 = x;
+		n++;
+	}
+};
+
 /* lpfilt :100 */
-MN void lpfilt(const int16_t *in, int16_t *lp, int len)
+MN void lpfilt(const int16_t *in, int16_t *lp, int len, LpAcor *ac = nullptr)
 {
 	const int16_t *lpar = TB(lpar);
 	const Word16 c0 = lpar[0], c1 = lpar[1], c2 = lpar[2], c3 = lpar[3];
+#if !defined(MELPE_OPCOUNT)
+	if (ac)
+		v_batch(&lp[len], lp, PIT_COR_LEN - len, [ac](int, int16_t x) {
+			ac->add(x);
+			return x;
+		});
+	else
+#endif
 	v_copy(lp, &lp[len], PIT_COR_LEN - len);
 	/* the four past outputs in registers (the reference reads them back from
 	 * lp), the inputs a block ahead; the taps in the reference's order */
@@ -1305,23 +1335,49 @@ MN void lpfilt(const int16_t *in, int16_t *lp, int len)
 		y3 = y2;
 		y2 = y1;
 		y1 = o;
+#if !defined(MELPE_OPCOUNT)
+		if (ac)
+			ac->add(o);
+#endif
 		return o;
 	});
 }
 
-/* ivfilt :138 -- 2nd-order inverse filter from 40-bit autocorrelations */
-MN void ivfilt(int16_t *iv, const int16_t *lp, int len)
+/* ivfilt :138 -- 2nd-order inverse filter from 40-bit autocorrelations;
+ * ac: the sums, formed by lpfilt; *dcsum: remove_dc's sample sum of the
+ * updated iv[0 .. PIT_COR_LEN) (an exact int sum), formed while the history
+ * moves down and the new samples are written */
+MN void ivfilt(int16_t *iv, const int16_t *lp, int len, const LpAcor *ac = nullptr,
+	       Word32 *dcsum = nullptr)
 {
 	int16_t rc[3];
 	Word16 pc1, pc2;
+	Word32 dsum = 0;
+#if !defined(MELPE_OPCOUNT)
+	if (ac)
+		v_batch(&iv[len], iv, PIT_COR_LEN - len, [&dsum](int, int16_t x) {
+			dsum += x;
+			return x;
+		});
+	else
+#endif
 	v_copy(iv, &iv[len], PIT_COR_LEN - len);
 	/* the reference's three autocorrelation sums (lags 0, 1, 2) in one pass
 	 * over lp, the samples in pairs (P16); each sum keeps its own chain in
 	 * index order and the same terms */
-	Word40 a0 = L40_mac(0, lp[0], lp[0]);
-	Word40 a1 = L40_mac(0, lp[1], lp[0]);
+	Word40 a0, a1, a2;
+#if !defined(MELPE_OPCOUNT)
+	if (ac) {
+		a0 = ac->a0;
+		a1 = ac->a1;
+		a2 = ac->a2;
+	} else
+#endif
+	{
+	a0 = L40_mac(0, lp[0], lp[0]);
+	a1 = L40_mac(0, lp[1], lp[0]);
 	a0 = L40_mac(a0, lp[1], lp[1]);
-	Word40 a2 = 0;
+	a2 = 0;
 	{
 		int16_t h1 = lp[1], h2 = lp[0];	/* lp[j - 1], lp[j - 2] */
 		auto step = [&](int16_t x) {
@@ -1341,6 +1397,7 @@ MN void ivfilt(int16_t *iv, const int16_t *lp, int len)
 		}
 		for (; j < PIT_COR_LEN; j++)
 			step(lp[j]);
+	}
 	}
 	Word16 sh = norm32(a0);
 	rc[0] = r_ound((Word32) L40_shl(a0, sh));
@@ -1373,9 +1430,13 @@ MN void ivfilt(int16_t *iv, const int16_t *lp, int len)
 			t = L_sub(t, L_mult(pc2, l2));
 			l2 = l1;
 			l1 = x;
-			return r_ound(L_shl(t, 3));
+			const Word16 o = r_ound(L_shl(t, 3));
+			dsum += o;
+			return o;
 		});
 	}
+	if (dcsum)
+		*dcsum = dsum;
 }
 
 /* normalised 40-bit correlation step shared by corPeak and frac_cor:
@@ -1431,13 +1492,19 @@ struct CpLags {
 	static constexpr int ob(int k) { return 4 - (k + 1) / 2; }
 };
 
-/* corPeak :216 */
-MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs)
+/* corPeak :216; dcsum: remove_dc's sample sum of in[0 .. PIT_COR_LEN),
+ * already formed by ivfilt (null: remove_dc forms it) */
+MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs, const Word32 *dcsum = nullptr)
 {
 	PROF_SCOPE(32);
 	alignas(4) int16_t pb[PIT_COR_LEN];
 	const int PW = PIT_COR_LEN - MAXPITCH;	/* 73 */
-	remove_dc(in, pb, PIT_COR_LEN);
+	if (dcsum) {
+		const Word16 off = remove_dc_off(*dcsum, PIT_COR_LEN);
+		v_batch(in, pb, PIT_COR_LEN, [off](int, int16_t x) { return sub(x, off); });
+	} else {
+		remove_dc(in, pb, PIT_COR_LEN);
+	}
 	Word40 r0 = 0, rk = 0, A = 0;
 	Word16 r0s, rks;
 	Word32 Lr0, Lrk;
@@ -1663,9 +1730,17 @@ MN void pitchAuto(EncAna *E, const int16_t *in, PitTrack *pt, ClassParam *cs)
 		v_zero(E->pa.ivbuf, PIT_COR_LEN);
 		E->pa.pauto_started = 1;
 	}
+#if !defined(MELPE_OPCOUNT)
+	LpAcor ac = {0, 0, 0, 0, 0, 0};
+	Word32 dcsum;
+	lpfilt(in, E->pa.lpbuf, PIT_SUBFRAME, &ac);
+	ivfilt(E->pa.ivbuf, E->pa.lpbuf, PIT_SUBFRAME, &ac, &dcsum);
+	corPeak(E->pa.ivbuf, pt, cs, &dcsum);
+#else
 	lpfilt(in, E->pa.lpbuf, PIT_SUBFRAME);
 	ivfilt(E->pa.ivbuf, E->pa.lpbuf, PIT_SUBFRAME);
 	corPeak(E->pa.ivbuf, pt, cs);
+#endif
 }
 
 /* multiCheck :433 */
