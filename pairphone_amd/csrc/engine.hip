@@ -87,6 +87,8 @@ int kl_dec_warm(int n, hipStream_t s);
 size_t kl_ana_private(void);
 size_t kl_ana_mw_private(void);
 size_t kl_harm_private(void);
+size_t kl_harm_wave_private(void);
+size_t kl_npp_private(void);
 size_t kl_dec_private(void);
 int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
 	      const int *perm, const int *nlive,
@@ -1071,17 +1073,29 @@ static int engine_reserve(melpe_engine *e)
 	 * scratch limit threshold; above it the allocation is made for the
 	 * dispatch and given back.  Raise the threshold (never lower it) to
 	 * what this engine's largest launch needs: private bytes per lane x 64
-	 * lanes x the waves of the launch (lane kernels: one per 64 channels;
-	 * the four-wave kernel: 4 per group, at most 512 groups). */
+	 * lanes x the waves of the launch that can be resident at once (lane
+	 * kernels: one per 64 channels; the four-wave kernel: 4 per group, at
+	 * most 512 groups; the wave-per-channel kernels k_enc_npp / k_npp and
+	 * k_enc_harm: one per channel, up to the device's resident waves). */
 	{
 		const size_t lane = kl_ana_private() > kl_harm_private() ? kl_ana_private() : kl_harm_private();
 		const size_t per_wave = (lane > kl_dec_private() ? lane : kl_dec_private()) * WAVE;
 		const size_t mw_wave = kl_ana_mw_private() * WAVE;
+		const size_t ww = kl_npp_private() > kl_harm_wave_private() ? kl_npp_private() : kl_harm_wave_private();
 		const size_t waves = (size_t) (e->channels + WAVE - 1) / WAVE;
 		const size_t mw_waves = 4 * (size_t) ((mw + WAVE - 1) / WAVE);
+		size_t resident = (size_t) e->channels;
+		hipDeviceProp_t prop;
+		if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) {
+			const size_t r = (size_t) prop.multiProcessorCount * (size_t) (prop.maxThreadsPerMultiProcessor / WAVE);
+			if (r > 0 && r < resident)
+				resident = r;
+		}
 		size_t need = per_wave * waves;
 		if (mw_wave * mw_waves > need)
 			need = mw_wave * mw_waves;
+		if (ww * WAVE * resident > need)
+			need = ww * WAVE * resident;
 		size_t cur = 0, mx = 0;
 		if (hipDeviceGetLimit(&cur, hipExtLimitScratchCurrent) == hipSuccess &&
 		    hipDeviceGetLimit(&mx, hipExtLimitScratchMax) == hipSuccess && need > cur) {

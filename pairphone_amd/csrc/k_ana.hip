@@ -110,8 +110,10 @@ extern "C" int kl_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto,
 /* private-segment bytes per lane of the kernel (engine.hip engine_reserve) */
 extern "C" size_t kl_ana_private(void)
 {
-	hipFuncAttributes a;
-	return hipFuncGetAttributes(&a, (const void *) k_enc_ana<1>) == hipSuccess ? a.localSizeBytes : 0;
+	hipFuncAttributes a, b;	/* both forms: MELPE_HARM=0 runs k_enc_ana<0> */
+	size_t x = hipFuncGetAttributes(&a, (const void *) k_enc_ana<1>) == hipSuccess ? a.localSizeBytes : 0;
+	size_t y = hipFuncGetAttributes(&b, (const void *) k_enc_ana<0>) == hipSuccess ? b.localSizeBytes : 0;
+	return x > y ? x : y;
 }
 
 extern "C" int kl_ana_warm(int n, hipStream_t s)

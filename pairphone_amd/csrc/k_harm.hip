@@ -233,6 +233,13 @@ extern "C" size_t kl_harm_private(void)
 	return hipFuncGetAttributes(&a, (const void *) k_enc_tail) == hipSuccess ? a.localSizeBytes : 0;
 }
 
+/* private-segment bytes per lane of k_enc_harm (one wave per channel) */
+extern "C" size_t kl_harm_wave_private(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *) k_enc_harm) == hipSuccess ? a.localSizeBytes : 0;
+}
+
 extern "C" int kl_harm_warm(int n, hipStream_t s)
 {
 	k_enc_harm<<<n, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0, nullptr, nullptr, AnaGate{});

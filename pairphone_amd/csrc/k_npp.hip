@@ -72,6 +72,16 @@ extern "C" int kl_enc_npp(EncState *enc, int16_t *sp, const uint8_t *active, int
 	return (int) hipGetLastError();
 }
 
+/* private-segment bytes per lane of the wave-per-channel NPP kernels
+ * (engine.hip engine_reserve) */
+extern "C" size_t kl_npp_private(void)
+{
+	hipFuncAttributes a, b;
+	size_t x = hipFuncGetAttributes(&a, (const void *) k_enc_npp) == hipSuccess ? a.localSizeBytes : 0;
+	size_t y = hipFuncGetAttributes(&b, (const void *) k_npp) == hipSuccess ? b.localSizeBytes : 0;
+	return x > y ? x : y;
+}
+
 extern "C" int kl_npp_warm(int n, hipStream_t s)
 {
 	k_enc_npp<<<n, WAVE, 0, s>>>(nullptr, nullptr, nullptr, 0);
