@@ -1564,9 +1564,13 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs, const Word32 *d
 	int16_t qa[4], qal[4], qb[4], qbl[4];
 	{
 	PROF_SCOPE(39);
-	for (int i = MAXPITCH - 1; i >= MINPITCH; i--) {
-		int n = MAXPITCH - 1 - i;
-		if ((n & 7) == 0) {
+	/* lag n = MAXPITCH - 1 - i; k8 = n & 7, a compile-time constant in the
+	 * unrolled block loop below, so the block's sums stay in registers
+	 * (indexed by a run-time n & 7 they went through scratch, one store per
+	 * block and one load and wait per lag) */
+	auto lag = [&](int n, int k8) __attribute__((always_inline)) {
+		const int i = MAXPITCH - 1 - n;
+		if (k8 == 0) {
 			#pragma unroll
 			for (int k = 0; k < 4; k++) {
 				qa[k] = pb[lo + k];
@@ -1575,7 +1579,7 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs, const Word32 *d
 				qbl[k] = pb[hi - 1 - k + PW];
 			}
 		}
-		if ((n & 7) == 0 && n + 8 <= NL_BLK) {
+		if (k8 == 0 && n + 8 <= NL_BLK) {
 			const int16_t *pa = &pb[1 + n / 2];
 			const int16_t *pq = &pb[143 - n / 2];
 #if !defined(MELPE_OPCOUNT)
@@ -1647,7 +1651,7 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs, const Word32 *d
 			}
 		}
 		if (n < NL_BLK) {
-			A = blk[n & 7];
+			A = blk[k8];
 			OPC_ADD(OP_L40_mac, PW);	/* census: the reference's per-lag sum */
 		} else {
 			A = 0;
@@ -1659,7 +1663,18 @@ MN void corPeak(const int16_t *in, PitTrack *pt, ClassParam *cs, const Word32 *d
 		peak_insert(tv, tj, (g1 > g2 && g1 > g) ? g1 : (int16_t) 0, (int16_t) (i + 1));
 		g2 = g1;
 		g1 = g;
+	};
+#if !defined(MELPE_OPCOUNT)
+	for (int n0 = 0; n0 < NL; n0 += 8) {
+		#pragma unroll
+		for (int k8 = 0; k8 < 8; k8++)
+			if (n0 + k8 < NL)
+				lag(n0 + k8, k8);
 	}
+#else
+	for (int n = 0; n < NL; n++)
+		lag(n, n & 7);
+#endif
 	peak_insert(tv, tj, (g1 > g2) ? g1 : (int16_t) 0, (int16_t) MINPITCH);
 	}
 	PROF_SCOPE(40);
