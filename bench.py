@@ -93,6 +93,9 @@ def parse(argv=None):
                          "(0 = skip)")
     ap.add_argument("--tx-channels", type=int, default=65536,
                     help="config 5 TX front end leg, channels per GPU (0 = skip)")
+    ap.add_argument("--rt-channels", type=int, default=65536,
+                    help="config 3 round-trip leg (encode + decode per superframe), channels per "
+                         "GPU (0 = skip)")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-side-legs", action="store_true", help="skip crypt and VAD legs")
     ap.add_argument("--no-duplex", action="store_true",
@@ -353,7 +356,12 @@ def cpu_baseline(args, gpu_bits):
     # points stay in the curve)
     top = max(curve, key=lambda p: p["value"])
     quota = cgroup_cpu_quota()
-    base = {"value": top["value"], "unit": "channel-s/s", "cores": top["processes"],
+    # cores = the CPU the processes actually had: the process count, capped
+    # by the cgroup's quota where one is set (more processes than the quota
+    # only time-share those cores)
+    cores = top["processes"] if quota is None else min(top["processes"], int(round(quota)))
+    base = {"value": top["value"], "unit": "channel-s/s", "cores": cores,
+            "processes": top["processes"],
             "kind": "reference", "host_cores_visible": usable, "cgroup_cpu_quota_cores": quota,
             "curve": curve,
             "sample": "channels 0..S-1 x %d superframes (%.1f s of audio each), melpe_a, one "
@@ -472,6 +480,57 @@ def duplex_leg(rig, wl, C, K, W):
            "step": "encode superframe k (caller stream A) + decode superframe k - 1 (caller stream B)"}
     log("duplex: %.1f ms/step on the shared engine stream, %.1f ms/step on own streams"
         % (out["shared"], out["own"]))
+    return res
+
+
+def round_trip_leg(rig, args, rank, world):
+    """BASELINE config 3: the encode + decode round trip (melpe_a then melpe_s
+    with the postfilter, melpe/melpe.c:91-107) of --rt-channels channels per
+    GPU on one engine; one step = k_enc_npp + the analysis + k_decode of one
+    superframe of every channel, each launch timed with HIP events.  After the
+    timed region the bits and the decoded PCM of sampled channels are checked
+    against the reference (oracle/_ref/ref_tool encgen + decgen on the same
+    synthetic channels), on rank 0."""
+    C, K, W = args.rt_channels, args.steps, args.warmup
+    wl = EngineWorkload(rig, C, rank * C, W + K)
+    dt, (npp_kms, ana_kms, dec_kms) = timed(rig, [wl.npp, wl.ana, wl.dec], K, W)
+    res = {"workload": "config 3: %d channels per GPU, melpe_a + melpe_s (with postfilter) "
+                       "per superframe on one engine" % C,
+           "channels_per_gpu": C, "value": world * C * K * SF_SECONDS / dt,
+           "unit": "channel-s/s (encoded and decoded)", "ms_per_step": 1e3 * dt / K,
+           "kernels_ms": {"k_enc_npp": npp_kms, "k_enc_ana": ana_kms, "k_decode": dec_kms}}
+    oc = opcount()
+    if oc:
+        w_ana, _ = w_over(oc, "W_enc_ana", W, W + K)
+        w_npp, _ = w_over(oc, "W_enc_npp", W, W + K)
+        w_dec, _ = w_over(oc, "W_dec", W, W + K)
+        res["roofline_frac"] = {
+            k: w * C / (ms / 1e3) / 1e12 / PEAK_VALU_TOPS
+            for k, w, ms in (("k_enc_npp", w_npp, npp_kms), ("k_enc_ana", w_ana, ana_kms),
+                             ("k_decode", w_dec, dec_kms))}
+        res["roofline_frac"]["step"] = ((w_ana + w_npp + w_dec) * C / dt * K / 1e12
+                                        / PEAK_VALU_TOPS)
+    if rank == 0 and not args.no_cpu_baseline and os.path.exists(REF_TOOL):
+        n = W + K
+        chans = sorted(set([0, C - 1] + [int(c) for c in np.linspace(1, C - 2, 14)]))
+        gb = wl.bits[:, chans].cpu().numpy()
+        go = wl.out[:, chans].cpu().numpy()
+        ok_b = ok_p = True
+        with tempfile.TemporaryDirectory() as tmp:
+            for i, c in enumerate(chans):
+                bp, pp = os.path.join(tmp, "%d.bits" % c), os.path.join(tmp, "%d.pcm" % c)
+                subprocess.run([REF_TOOL, "encgen", str(RUN_SEED), str(c), "1", str(n), bp],
+                               check=True)
+                subprocess.run([REF_TOOL, "decgen", bp, "1", str(n), pp], check=True)
+                rb = np.fromfile(bp, dtype=np.uint8).reshape(n, SF_BYTES)
+                rp = np.fromfile(pp, dtype=np.int16).reshape(n, SF_SAMPLES)
+                ok_b &= bool(np.array_equal(gb[:, i], rb))
+                ok_p &= bool(np.array_equal(go[:, i], rp))
+        res["parity_spot_check"] = {"channels": chans, "superframes": n,
+                                    "bits_equal_reference": ok_b, "pcm_equal_reference": ok_p}
+    wl.close()
+    log("round trip (config 3, %d channels): %.2f ms/step (npp %.2f, analysis %.2f, "
+        "decode %.2f ms)" % (C, res["ms_per_step"], npp_kms, ana_kms, dec_kms))
     return res
 
 
@@ -601,6 +660,10 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
                        "sharding": "shard.channel_range: contiguous, balanced"})
         log("strong (%d total): %.1f ms/step" % (args.total_channels, strong["ms_per_step"]))
 
+    rt = None
+    if args.rt_channels and workload_cls is None:
+        rt = round_trip_leg(rig, args, rank, world)
+
     tx = None
     if args.tx_channels:
         tx = tx_leg(rig, args, rank, world)
@@ -658,7 +721,7 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
                    "parallelism": "channel shards, %d GPU(s), no collective" % world},
         "realtime_factor": value / (world * C),
         "roofline": roof, "cpu_baseline": base, "decode": dec, "parity_spot_check": parity,
-        "strong_scaling": strong, "tx_front_end": tx, "host_fed": hostfed, "duplex": duplex,
+        "strong_scaling": strong, "round_trip": rt, "tx_front_end": tx, "host_fed": hostfed, "duplex": duplex,
         "bitstream_gather": gathered, "voice_crypt": side.get("crypt"), "vad": side.get("vad"),
         "modem": side.get("modem"),
     }

@@ -92,6 +92,15 @@ int melpe_engine_set_lane_order(melpe_engine *e, int on);
  * resident at once; 1 above).  Bits are the same either way. */
 int melpe_engine_set_ana_waves(melpe_engine *e, int waves);
 
+/* Waves per 64 channels of the decoder: 1 = one lane per channel; 2 = the
+ * two-wave decoder, wave A reading the channel and synthesising each
+ * frame's excitation, wave B running the synthesis filters, dispersion and
+ * postfilter one frame behind (for channel counts that would leave SIMDs
+ * idle: available up to 65,536 channels per engine); 0 (default) = chosen
+ * from the channel count (2 up to 65,536 channels, 1 above).  PCM is the
+ * same either way. */
+int melpe_engine_set_dec_waves(melpe_engine *e, int waves);
+
 /* The live-count mapping of the automatic choice above 32,768 channels: a
  * superframe with at most live_max live channels (ragged streams, paused
  * channels) runs the four-wave analysis, more run one lane per channel.
@@ -100,7 +109,9 @@ int melpe_engine_set_ana_waves(melpe_engine *e, int waves);
  * needs the lane order on, the default), and the host never reads the
  * count.  live_max >= 0 (default 32,768, where the four-wave kernel holds
  * every live channel resident; 0 = by channel count only).  Bits are the
- * same either way. */
+ * same either way.  Values above 32,768 are for diagnostics only: the
+ * four-wave kernel then loops over the extra live channels and is slower
+ * than the lane kernel from about 40,960 live (profiles/r05_mw_crossover.jsonl). */
 int melpe_engine_set_mw_live_max(melpe_engine *e, int live_max);
 
 /* By default every engine on a device runs its kernels on one internal
@@ -118,7 +129,8 @@ int melpe_engine_set_own_stream(melpe_engine *e, int on);
 
 /* The mapping the engine's last analysis launch ran, as the device recorded
  * it: 1 = one lane per channel, 4 = four waves per 64 channels, 0 = none
- * (no live channel).  Waits for the engine's enqueued calls. */
+ * (no live channel in the launch since the last lane-order sort).  Waits for
+ * the engine's enqueued calls. */
 int melpe_engine_last_ana_waves(melpe_engine *e);
 
 /* Per-channel state records, for checkpoint / resume and for moving channels
@@ -294,8 +306,9 @@ int melpe_ops_eval_dev(int op, const void *d_a, const void *d_b, const void *d_c
  * device slots; call k's host-to-device copy, kernels and device-to-host
  * copy run on three streams, so superframe k's kernels overlap the copies
  * of superframes k - 1 and k + 1.  bits, sp and active must stay valid and
- * untouched until melpe_encode_host_wait returns (or two calls later, when
- * the slot is reused).  For the copies to overlap the kernels the host
+ * untouched until melpe_encode_host_wait returns (a slot's reuse two calls
+ * later waits on the device only, so the host may not reuse a call's
+ * buffers before the wait).  For the copies to overlap the kernels the host
  * buffers must be pinned (hipHostMalloc / hipHostRegister); with pageable
  * memory the runtime stages them and the host call blocks.  Ordered after
  * the engine's earlier calls on any stream. */

@@ -40,6 +40,7 @@ def load_library(path=None):
         "melpe_engine_reset_dev": (i32, [vp, vp, i32, vp]),
         "melpe_engine_set_lane_order": (i32, [vp, i32]),
         "melpe_engine_set_ana_waves": (i32, [vp, i32]),
+        "melpe_engine_set_dec_waves": (i32, [vp, i32]),
         "melpe_engine_set_mw_live_max": (i32, [vp, i32]),
         "melpe_engine_last_ana_waves": (i32, [vp]),
         "melpe_engine_set_own_stream": (i32, [vp, i32]),
@@ -90,8 +91,16 @@ def load_library(path=None):
         "melpe_s": (None, [vp, vp]),
         "melpe_n": (None, [vp]),
     }
+    # an older build named by MELPE_AMD_LIB (A/B measurements) may lack the
+    # newest entry points; the product library must export every one
+    older = p != LIB_PATH and os.environ.get("MELPE_AMD_LIB") == p
     for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if older:
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     if path is None:
@@ -232,6 +241,12 @@ class MelpeEngine:
         4 waves per channel group (ana_mw.h), 0 = by channel count (results
         are the same either way)"""
         _check(self.lib.melpe_engine_set_ana_waves(self.h, int(waves)))
+
+    def set_dec_waves(self, waves):
+        """waves per 64 channels of the decoder: 1 lane per channel, 2 the
+        two-wave decoder (excitation / filters, up to 65,536 channels), 0 =
+        by channel count (PCM is the same either way)"""
+        _check(self.lib.melpe_engine_set_dec_waves(self.h, int(waves)))
 
     def set_mw_live_max(self, live_max):
         """above 32,768 channels, superframes with at most live_max live

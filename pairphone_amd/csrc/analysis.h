@@ -510,7 +510,6 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 	EXACT_STAT(exact ? 1 : 0);
 	Word16 ip = lower;
 	Word32 max_num = 0, max_den = 1;
-	bool even = true;
 	Word16 cb = negate(shr(add(len, upper), 1));
 	const Word16 cb0 = cb;
 	/* exact: the caller's bound holds over sig[cb0 .. cb0 + upper + len),
@@ -553,10 +552,15 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 	 * of lag n0 + 2k + 1 sig[cb0 + upper - 1 - n0/2 - k] (and + len); each
 	 * register queue moves up by one per update */
 	int16_t qa[4], qal[4], qb[4], qbl[4];
-	for (Word16 i = upper; i >= lower; i--) {
-		int n = upper - i;
+	/* lag i = upper - n; k8 = n & 7 and (for the one-pass search) n itself
+	 * are compile-time constants in the unrolled loops below, so blk[] and
+	 * blk12[] stay in registers (indexed at run time they lived in the
+	 * private segment: a store per block, a load and its wait per lag) */
+	auto lag = [&](int n, int k8) __attribute__((always_inline)) {
+		const Word16 i = upper - n;
+		const bool even = (k8 & 1) == 0;
 		Word32 corr;
-		if ((n & 7) == 0) {
+		if (k8 == 0) {
 			const int16_t *pa = &sig[cb0 + n / 2], *pb = &sig[cb0 + upper - 1 - n / 2];
 			#pragma unroll
 			for (int k = 0; k < 4; k++) {
@@ -567,8 +571,8 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 			}
 		}
 		if (one) {
-			corr = blk12[n];
-		} else if ((n & 7) == 0 && (exact || n + 8 <= nlags)) {
+			corr = blk12[n < 12 ? n : 0];
+		} else if (k8 == 0 && (exact || n + 8 <= nlags)) {
 			/* the block's bases: a at cb_n0, b at cb_(n0+7) + i_(n0+7) */
 			int c_n0 = cb0 + (n + 1) / 2;
 			int b0 = cb0 + (n + 8) / 2 + upper - n - 7;
@@ -583,7 +587,7 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 		}
 		if (one) {
 		} else if (exact || n < (nlags & ~7)) {
-			corr = blk[n & 7];
+			corr = blk[k8];
 			/* census: the reference's L_v_inner tail per lag */
 			OPC_ADD(OP_add, 2);
 			OPC_ADD(OP_sub, 1);
@@ -614,7 +618,6 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 			ip = i;
 		}
 		if (even) {
-			even = false;
 			c00 = L_msu(c00, qa[0], qa[0]);	/* sig[cb], sig[cb + len] */
 			c00 = L_mac(c00, qal[0], qal[0]);
 			cb = add(cb, 1);
@@ -624,7 +627,6 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 				qal[k] = qal[k + 1];
 			}
 		} else {
-			even = true;
 			/* sig[cb + i - 1 + len], sig[cb + i - 1] */
 			cTT = L_msu(cTT, qbl[0], qbl[0]);
 			cTT = L_mac(cTT, qb[0], qb[0]);
@@ -634,7 +636,25 @@ MN Word16 find_pitch(const int16_t *sig, Word16 *pcorr, Word16 lower, Word16 upp
 				qbl[k] = qbl[k + 1];
 			}
 		}
+	};
+#if !defined(MELPE_OPCOUNT)
+	if (one) {
+		#pragma unroll
+		for (int n = 0; n < 12; n++)
+			if (n < nlags)
+				lag(n, n & 7);
+	} else {
+		for (int n0 = 0; n0 < nlags; n0 += 8) {
+			#pragma unroll
+			for (int k8 = 0; k8 < 8; k8++)
+				if (n0 + k8 < nlags)
+					lag(n0 + k8, k8);
+		}
 	}
+#else
+	for (int n = 0; n < nlags; n++)
+		lag(n, n & 7);
+#endif
 	(void) cb;
 	*pcorr = shr(sqrt_fxp(divide_s(extract_l(max_num), extract_l(max_den)), 15), 1);
 	return ip;
@@ -2038,8 +2058,15 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 	fc_corr_any(in, hp, win, blk);
 	/* The r0 / rk updates alternate with the parity of the lag, which
 	 * differs between lanes: one update of the selected side per lag,
-	 * branch-free (the reference's L40_msu / L40_mac pairs, in order). */
-	for (Word16 i = sub(hp, 1); i >= lp; i--) {
+	 * branch-free (the reference's L40_msu / L40_mac pairs, in order).
+	 * Lag i = hp - 1 - n for n < hp - lp <= 10, the loop unrolled so that
+	 * blk[n] is a compile-time index (registers, not the private segment) */
+	const int nl = hp - lp;
+	#pragma unroll
+	for (int n = 0; n < 10; n++) {
+		if (n >= nl)
+			continue;
+		const Word16 i = hp - 1 - n;
 		const bool ev = (i & 1) == 0;	/* i >= MINPITCH > 0 */
 		hi -= !ev;
 		const int ia = ev ? lo : hi;
@@ -2057,7 +2084,7 @@ MN Word16 frac_cor(const int16_t *in, Word16 pitch)
 		rks = ev ? rks : vs;
 		lo += ev;
 		if (blocked) {
-			A = blk[hp - 1 - i];
+			A = blk[n];
 		} else {
 			A = 0;
 			for (int j = lo; j < lo + win; j++)

@@ -1423,15 +1423,19 @@ MD Word32 syn_chain(DecState *D, int16_t *s, int len, Word16 pulse_gain, const i
 	return syn_chain_t<false>(D, s, len, pulse_gain, aden, anum, tilt, lpc);
 }
 
+/* melp_syn's per-frame values (melp_syn.c:160-295): the first-call setup,
+ * the noise estimate, the frame's LPC gain and tilt and the mixing filters'
+ * voicing split.  Shared by the serial form and the two-wave decoder's
+ * excitation side. */
+struct SynFrame {
+	Word16 lpc_gain, cur_tilt;
+	int16_t cur_p[MIX_ORD + 1], cur_n[MIX_ORD + 1];
+};
+
 template <bool R24>
-MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
+MD void syn_frame_begin(DecState *D, MelpParam *par, SynFrame &F)
 {
-	PROF_SCOPE(18);
-	const int BEGIN = DISP_ORD;	/* max(MIX_ORD, DISP_ORD) */
-	int16_t fs_real[PITCHMAX], refc[LPC_ORD], sb[BEGIN + PITCHMAX];
-	int16_t lsf[LPC_ORD], lpc[LPC_ORD + 1], ase_num[LPC_ORD + 1], ase_den[LPC_ORD];
-	int16_t cur_p[MIX_ORD + 1], cur_n[MIX_ORD + 1], pul[MIX_ORD + 1], noi[MIX_ORD + 1];
-	int16_t tilt_cof[2];
+	int16_t refc[LPC_ORD], lpc[LPC_ORD + 1];
 	MelpParam *prev = &D->prev_par;
 	Word16 t1, t2;
 	if (!D->syn_started) {
@@ -1458,123 +1462,110 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 	if (!par->uv_flag && !D->erase)
 		window_Q(par->fs_mag, g_der.w_fs_inv, par->fs_mag, NUM_HARM, 14);
 	lpc_clmp(par->lsf, 409, LPC_ORD);
-	tilt_cof[0] = SW_MAX_;
 	lpc_lsp2pred(par->lsf, &lpc[1], LPC_ORD);
 	Word16 lpc_gain = lpc_pred2refl(&lpc[1], refc, LPC_ORD);
-	lpc_gain = sqrt_fxp(lpc_gain, 15);
-	Word16 cur_tilt = (refc[0] < 0) ? shr(refc[0], 1) : (Word16) 0;
+	F.lpc_gain = sqrt_fxp(lpc_gain, 15);
+	F.cur_tilt = (refc[0] < 0) ? shr(refc[0], 1) : (Word16) 0;
 	t1 = shr(prev->pitch, 1);
 	t2 = add(1536, prev->gain[NUM_GAINFR - 1]);
 	if (par->pitch < t1 && par->gain[0] > t2)
 		prev->pitch = par->pitch;
-	v_zero(cur_p, MIX_ORD + 1);
-	v_zero(cur_n, MIX_ORD + 1);
+	v_zero(F.cur_p, MIX_ORD + 1);
+	v_zero(F.cur_n, MIX_ORD + 1);
 	const int16_t *bpc = TB(bp_cof);
 	for (int i = 0; i < NUM_BANDS; i++) {
 		if (par->bpvc[i] > 8192)
-			v_add(cur_p, bpc + i * (MIX_ORD + 1), MIX_ORD + 1);
+			v_add(F.cur_p, bpc + i * (MIX_ORD + 1), MIX_ORD + 1);
 		else
-			v_add(cur_n, bpc + i * (MIX_ORD + 1), MIX_ORD + 1);
+			v_add(F.cur_n, bpc + i * (MIX_ORD + 1), MIX_ORD + 1);
 	}
-	/* pre[0 .. DISP_ORD): the dispersion history; then the frame's periods
-	 * from syn_begin on, before dispersion (at most FRAME + PITCHMAX) */
-	int16_t pre[DISP_ORD + FRAME + PITCHMAX];
-	const Word16 sb_start = D->syn_begin;
-	v_copy(pre, D->disp_del, DISP_ORD);
-	while (D->syn_begin < FRAME) {
-		Word16 sb0 = D->syn_begin;
-		Word16 len, gain, fc, pulse_gain;
-		{
-		PROF_SCOPE(50);
-		Word16 ifact = divide_s(sb0, FRAME);
-		Word16 gcnt, ifg, intfact;
-		if (sb0 >= 90) {
-			gcnt = 2;
-			ifg = divide_s(sub(sb0, 90), 90);
-		} else {
-			gcnt = 1;
-			ifg = divide_s(sb0, 90);
-		}
-		Word32 La = L_mult(par->gain[gcnt - 1], ifg);
-		Word32 Lb = L_mult(gcnt > 1 ? par->gain[gcnt - 2] : prev->gain[NUM_GAINFR - 1],
-				   sub(SW_MAX_, ifg));
-		gain = extract_h(L_add(La, Lb));
-		t1 = sub(par->gain[NUM_GAINFR - 1], prev->gain[NUM_GAINFR - 1]);
-		if (abs_s(t1) > 1536) {
-			t2 = sub(gain, prev->gain[NUM_GAINFR - 1]);
-			if ((t2 > 0 && t1 < 0) || (t2 < 0 && t1 > 0)) {
-				intfact = 0;
-			} else {
-				t1 = abs_s(t1);
-				t2 = abs_s(t2);
-				intfact = (t2 >= t1) ? (Word16) SW_MAX_ : divide_s(t2, t1);
-			}
-		} else {
-			intfact = ifact;
-		}
-		interp_array(prev->lsf, par->lsf, lsf, intfact, LPC_ORD);
-		lpc_lsp2pred(lsf, &lpc[1], LPC_ORD);
-		Word16 sig_prob = lin_int_bnd(gain, add(D->noise_gain, 3072), add(D->noise_gain, 7680),
-					      0, SW_MAX_);
-		ase_num[0] = 4096;
-		lpc_bwex(&lpc[1], &ase_num[1], mult(sig_prob, 16384), LPC_ORD);
-		lpc_bwex(&lpc[1], ase_den, mult(sig_prob, 26214), LPC_ORD);
-		Word16 if1 = sub(SW_MAX_, intfact);
-		t1 = add(mult(cur_tilt, intfact), mult(D->prev_tilt, if1));
-		tilt_cof[1] = mult(sig_prob, t1);
-		t1 = add(mult(lpc_gain, intfact), mult(D->prev_lpc_gain, if1));
-		Word16 syn_gain = mult(32000, t1);
-		Word16 pitch = add(mult(par->pitch, intfact), mult(prev->pitch, if1));
-		pulse_gain = extract_h(L_shl(L_mult(syn_gain, sqrt_fxp(pitch, 7)), 4));
-		t1 = sqrt_fxp(ifact, 15);
-		interp_array(D->prev_pcof, cur_p, pul, t1, MIX_ORD + 1);
-		interp_array(D->prev_ncof, cur_n, noi, t1, MIX_ORD + 1);
-		Word16 fc_prev = set_fc(prev->bpvc);
-		Word16 fc_cur = set_fc(par->bpvc);
-		t2 = sub(SW_MAX_, t1);
-		fc = add(mult(t1, fc_cur), mult(t2, fc_prev));
-		Word16 jitter = add(mult(par->jitter, ifact), mult(prev->jitter, sub(SW_MAX_, ifact)));
-		gain = mult(26214, gain);	/* X005_Q19 */
-		int16_t r;
-		rand_num(&r, SW_MAX_, 1, &D->seed);
-		t1 = shr(mult(jitter, r), 1);
-		t1 = mult(pitch, sub(16384, t1));
-		len = shift_r(t1, -6);
-		if (len < PITCHMIN)
-			len = PITCHMIN;
-		if (len > PITCHMAX)
-			len = PITCHMAX;
-		v_set(fs_real, 8192, len);
-		fs_real[0] = 0;
-		interp_array(prev->fs_mag, par->fs_mag, &fs_real[1], intfact, NUM_HARM);
-		}
-		harm_syn_pitch(D, fs_real, &sb[BEGIN], fc, len);
-#if !defined(MELPE_OPCOUNT)
-		{
-			/* the filter chain in one pass, then scale_adj writing the
-			 * period straight into the frame's run */
-			Word32 e0 = syn_chain(D, &sb[BEGIN], len, pulse_gain, ase_den, ase_num, tilt_cof, &lpc[1]);
-			scale_adj(D, &sb[BEGIN], gain, len, 10, 26214, e0, &pre[DISP_ORD + sb0 - sb_start]);
-			D->syn_begin = add(sb0, len);
-			continue;
-		}
-#endif
-		v_scale(&sb[BEGIN], pulse_gain, len);
-		v_copy(&sb[BEGIN - LPC_ORD], D->ase_del, LPC_ORD);
-		lpc_syn(&sb[BEGIN], &sb[BEGIN], ase_den, LPC_ORD, len);
-		v_copy(D->ase_del, &sb[BEGIN + len - LPC_ORD], LPC_ORD);
-		zerflt(&sb[BEGIN], ase_num, &sb[BEGIN], LPC_ORD, len);
-		v_copy(&sb[BEGIN - 1], D->tilt_del, 1);
-		v_copy(D->tilt_del, &sb[len + BEGIN - 1], 1);
-		zerflt_Q(&sb[BEGIN], tilt_cof, &sb[BEGIN], 1, len, 15);
-		v_copy(&sb[BEGIN - LPC_ORD], D->lpc_del, LPC_ORD);
-		lpc_syn(&sb[BEGIN], &sb[BEGIN], &lpc[1], LPC_ORD, len);
-		v_copy(D->lpc_del, &sb[len + BEGIN - LPC_ORD], LPC_ORD);
-		scale_adj(D, &sb[BEGIN], gain, len, 10, 26214);
-		/* the period's pre-dispersion samples join the frame's run */
-		v_copy(&pre[DISP_ORD + sb0 - sb_start], &sb[BEGIN], len);
-		D->syn_begin = add(sb0, len);
+}
+
+/* one pitch period's parameters (melp_syn.c:300-394): length, gains, the
+ * synthesis filters' coefficients and the harmonic amplitudes */
+struct SynPer {
+	Word16 len, gain, fc, pulse_gain;
+	int16_t lpc[LPC_ORD + 1], ase_num[LPC_ORD + 1], ase_den[LPC_ORD], tilt_cof[2];
+	int16_t fs_real[PITCHMAX];
+};
+
+MD void syn_period(DecState *D, MelpParam *par, const SynFrame &F, Word16 sb0, SynPer &P)
+{
+	PROF_SCOPE(50);
+	MelpParam *prev = &D->prev_par;
+	int16_t lsf[LPC_ORD], pul[MIX_ORD + 1], noi[MIX_ORD + 1];
+	Word16 t1, t2;
+	Word16 ifact = divide_s(sb0, FRAME);
+	Word16 gcnt, ifg, intfact;
+	if (sb0 >= 90) {
+		gcnt = 2;
+		ifg = divide_s(sub(sb0, 90), 90);
+	} else {
+		gcnt = 1;
+		ifg = divide_s(sb0, 90);
 	}
+	Word32 La = L_mult(par->gain[gcnt - 1], ifg);
+	Word32 Lb = L_mult(gcnt > 1 ? par->gain[gcnt - 2] : prev->gain[NUM_GAINFR - 1],
+			   sub(SW_MAX_, ifg));
+	Word16 gain = extract_h(L_add(La, Lb));
+	t1 = sub(par->gain[NUM_GAINFR - 1], prev->gain[NUM_GAINFR - 1]);
+	if (abs_s(t1) > 1536) {
+		t2 = sub(gain, prev->gain[NUM_GAINFR - 1]);
+		if ((t2 > 0 && t1 < 0) || (t2 < 0 && t1 > 0)) {
+			intfact = 0;
+		} else {
+			t1 = abs_s(t1);
+			t2 = abs_s(t2);
+			intfact = (t2 >= t1) ? (Word16) SW_MAX_ : divide_s(t2, t1);
+		}
+	} else {
+		intfact = ifact;
+	}
+	interp_array(prev->lsf, par->lsf, lsf, intfact, LPC_ORD);
+	lpc_lsp2pred(lsf, &P.lpc[1], LPC_ORD);
+	Word16 sig_prob = lin_int_bnd(gain, add(D->noise_gain, 3072), add(D->noise_gain, 7680),
+				      0, SW_MAX_);
+	P.ase_num[0] = 4096;
+	lpc_bwex(&P.lpc[1], &P.ase_num[1], mult(sig_prob, 16384), LPC_ORD);
+	lpc_bwex(&P.lpc[1], P.ase_den, mult(sig_prob, 26214), LPC_ORD);
+	Word16 if1 = sub(SW_MAX_, intfact);
+	t1 = add(mult(F.cur_tilt, intfact), mult(D->prev_tilt, if1));
+	P.tilt_cof[0] = SW_MAX_;
+	P.tilt_cof[1] = mult(sig_prob, t1);
+	t1 = add(mult(F.lpc_gain, intfact), mult(D->prev_lpc_gain, if1));
+	Word16 syn_gain = mult(32000, t1);
+	Word16 pitch = add(mult(par->pitch, intfact), mult(prev->pitch, if1));
+	P.pulse_gain = extract_h(L_shl(L_mult(syn_gain, sqrt_fxp(pitch, 7)), 4));
+	t1 = sqrt_fxp(ifact, 15);
+	interp_array(D->prev_pcof, F.cur_p, pul, t1, MIX_ORD + 1);
+	interp_array(D->prev_ncof, F.cur_n, noi, t1, MIX_ORD + 1);
+	Word16 fc_prev = set_fc(prev->bpvc);
+	Word16 fc_cur = set_fc(par->bpvc);
+	t2 = sub(SW_MAX_, t1);
+	P.fc = add(mult(t1, fc_cur), mult(t2, fc_prev));
+	Word16 jitter = add(mult(par->jitter, ifact), mult(prev->jitter, sub(SW_MAX_, ifact)));
+	P.gain = mult(26214, gain);	/* X005_Q19 */
+	int16_t r;
+	rand_num(&r, SW_MAX_, 1, &D->seed);
+	t1 = shr(mult(jitter, r), 1);
+	t1 = mult(pitch, sub(16384, t1));
+	Word16 len = shift_r(t1, -6);
+	if (len < PITCHMIN)
+		len = PITCHMIN;
+	if (len > PITCHMAX)
+		len = PITCHMAX;
+	P.len = len;
+	v_set(P.fs_real, 8192, len);
+	P.fs_real[0] = 0;
+	interp_array(prev->fs_mag, par->fs_mag, &P.fs_real[1], intfact, NUM_HARM);
+}
+
+/* the dispersion FIR over the frame's run of periods, the frame's output
+ * and the next frame's start (melp_syn.c:436-447): pre[0 .. DISP_ORD) is
+ * the dispersion history, pre[DISP_ORD ..] the run from sb_start to
+ * D->syn_begin */
+MD void syn_disperse(DecState *D, int16_t *pre, Word16 sb_start, int16_t *out)
+{
 	/* The dispersion FIR (melp_syn.c:436-440) runs per period on the period
 	 * with the previous period's last DISP_ORD pre-dispersion samples as its
 	 * history (disp_del, also when a period is shorter than that): the same
@@ -1583,27 +1574,244 @@ MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
 	 * period count the wave's channels take; each output sample's L_mac
 	 * chain is the reference's.  The run's part past FRAME is the next
 	 * frame's start (sigsave). */
-	{
-		PROF_SCOPE(51);
-		const int total = D->syn_begin - sb_start;
-		v_copy(D->disp_del, &pre[total], DISP_ORD);
-		static_assert(DISP_ORD == 64, "zerflt_Q's unrolled dispersion path (dsp.h)");
-		zerflt_Q(&pre[DISP_ORD], TB(disp_cof), &pre[DISP_ORD], DISP_ORD, total, 15);
-		v_copy(&out[sb_start], &pre[DISP_ORD], FRAME - sb_start);
-		v_copy(D->sigsave, &pre[DISP_ORD + FRAME - sb_start], total - (FRAME - sb_start));
+	PROF_SCOPE(51);
+	const int total = D->syn_begin - sb_start;
+	v_copy(D->disp_del, &pre[total], DISP_ORD);
+	static_assert(DISP_ORD == 64, "zerflt_Q's unrolled dispersion path (dsp.h)");
+	zerflt_Q(&pre[DISP_ORD], TB(disp_cof), &pre[DISP_ORD], DISP_ORD, total, 15);
+	v_copy(&out[sb_start], &pre[DISP_ORD], FRAME - sb_start);
+	v_copy(D->sigsave, &pre[DISP_ORD + FRAME - sb_start], total - (FRAME - sb_start));
+}
+
+/* the frame's parameters become the previous frame's (melp_syn.c:455-468) */
+MD void syn_frame_end(DecState *D, const MelpParam *par, const SynFrame &F)
+{
+	v_copy(D->prev_pcof, F.cur_p, MIX_ORD + 1);
+	v_copy(D->prev_ncof, F.cur_n, MIX_ORD + 1);
+	D->prev_par = *par;
+	D->prev_tilt = F.cur_tilt;
+	D->prev_lpc_gain = F.lpc_gain;
+	D->syn_begin = sub(D->syn_begin, FRAME);
+}
+
+template <bool R24>
+MN void melp_syn(DecState *D, MelpParam *par, int16_t *out)
+{
+	PROF_SCOPE(18);
+	const int BEGIN = DISP_ORD;	/* max(MIX_ORD, DISP_ORD) */
+	int16_t sb[BEGIN + PITCHMAX];
+	SynFrame F;
+	syn_frame_begin<R24>(D, par, F);
+	/* pre[0 .. DISP_ORD): the dispersion history; then the frame's periods
+	 * from syn_begin on, before dispersion (at most FRAME + PITCHMAX) */
+	int16_t pre[DISP_ORD + FRAME + PITCHMAX];
+	const Word16 sb_start = D->syn_begin;
+	v_copy(pre, D->disp_del, DISP_ORD);
+	while (D->syn_begin < FRAME) {
+		const Word16 sb0 = D->syn_begin;
+		SynPer P;
+		syn_period(D, par, F, sb0, P);
+		const Word16 len = P.len;
+		harm_syn_pitch(D, P.fs_real, &sb[BEGIN], P.fc, len);
+#if !defined(MELPE_OPCOUNT)
+		{
+			/* the filter chain in one pass, then scale_adj writing the
+			 * period straight into the frame's run */
+			Word32 e0 = syn_chain(D, &sb[BEGIN], len, P.pulse_gain, P.ase_den, P.ase_num, P.tilt_cof,
+					      &P.lpc[1]);
+			scale_adj(D, &sb[BEGIN], P.gain, len, 10, 26214, e0, &pre[DISP_ORD + sb0 - sb_start]);
+			D->syn_begin = add(sb0, len);
+			continue;
+		}
+#endif
+		v_scale(&sb[BEGIN], P.pulse_gain, len);
+		v_copy(&sb[BEGIN - LPC_ORD], D->ase_del, LPC_ORD);
+		lpc_syn(&sb[BEGIN], &sb[BEGIN], P.ase_den, LPC_ORD, len);
+		v_copy(D->ase_del, &sb[BEGIN + len - LPC_ORD], LPC_ORD);
+		zerflt(&sb[BEGIN], P.ase_num, &sb[BEGIN], LPC_ORD, len);
+		v_copy(&sb[BEGIN - 1], D->tilt_del, 1);
+		v_copy(D->tilt_del, &sb[len + BEGIN - 1], 1);
+		zerflt_Q(&sb[BEGIN], P.tilt_cof, &sb[BEGIN], 1, len, 15);
+		v_copy(&sb[BEGIN - LPC_ORD], D->lpc_del, LPC_ORD);
+		lpc_syn(&sb[BEGIN], &sb[BEGIN], &P.lpc[1], LPC_ORD, len);
+		v_copy(D->lpc_del, &sb[len + BEGIN - LPC_ORD], LPC_ORD);
+		scale_adj(D, &sb[BEGIN], P.gain, len, 10, 26214);
+		/* the period's pre-dispersion samples join the frame's run */
+		v_copy(&pre[DISP_ORD + sb0 - sb_start], &sb[BEGIN], len);
+		D->syn_begin = add(sb0, len);
 	}
+	syn_disperse(D, pre, sb_start, out);
 	/* the reference postfilters the frame inside the loop, in its last
 	 * period (melp_syn.c:448); nothing after it in the loop reads out[] or
 	 * the postfilter state, so the call follows the loop -- where every
 	 * lane of the wave makes it together */
-	postfilt(D, out, prev->lsf, par->lsf);
-	v_copy(D->prev_pcof, cur_p, MIX_ORD + 1);
-	v_copy(D->prev_ncof, cur_n, MIX_ORD + 1);
-	*prev = *par;
-	D->prev_tilt = cur_tilt;
-	D->prev_lpc_gain = lpc_gain;
+	postfilt(D, out, D->prev_par.lsf, par->lsf);
+	syn_frame_end(D, par, F);
+}
+
+#if !defined(MELPE_OPCOUNT)
+/* ------------------------------------------------------------------ */
+/* the two-wave decoder (k_dec2.hip): melp_syn split into the excitation */
+/* side (wave A) and the filter side (wave B) of the same 64 channels     */
+/* ------------------------------------------------------------------ */
+
+/* Per frame, A hands B (through a per-channel buffer of HB_WORDS dwords,
+ * int16 pairs low half first): the period count and the run's length, the
+ * two LSF vectors the postfilter interpolates, each period's length, gains
+ * and filter coefficients, and the run of excitation samples.  A period is
+ * at least PITCHMIN long and the frame's loop starts below FRAME, so a frame
+ * has at most HB_MAXPER periods and a run of at most FRAME + PITCHMAX - 1
+ * samples. */
+#define HB_MAXPER ((FRAME + PITCHMIN - 1) / PITCHMIN)
+enum {
+	HB_NP = 0,	/* periods | run length << 16 */
+	HB_LSF = 1,	/* prev_par.lsf, then par->lsf (clamped): 2 x LPC_ORD / 2 */
+	HB_PER = HB_LSF + LPC_ORD,	/* HB_PW per period */
+	HB_PW = 2 + 3 * LPC_ORD / 2,	/* len | pulse_gain, gain | tilt, ase_den, ase_num[1..], lpc[1..] */
+	HB_EXC = HB_PER + HB_MAXPER * HB_PW,
+	HB_WORDS = HB_EXC + (FRAME + PITCHMAX) / 2,
+};
+static_assert(LPC_ORD % 2 == 0, "coefficient vectors packed in pairs");
+
+MD uint32_t hb_pack(int16_t lo, int16_t hi)
+{
+	return (uint32_t) (uint16_t) lo | ((uint32_t) (uint16_t) hi << 16);
+}
+
+template <class Hb>
+MD void hb_put_vec(Hb &hb, int k, const int16_t *v, int n)
+{
+	for (int i = 0; i < n; i += 2)
+		hb.put(k + i / 2, hb_pack(v[i], v[i + 1]));
+}
+
+template <class Hb>
+MD void hb_get_vec(const Hb &hb, int k, int16_t *v, int n)
+{
+	for (int i = 0; i < n; i += 2) {
+		const uint32_t x = hb.get(k + i / 2);
+		v[i] = lo16(x);
+		v[i + 1] = hi16(x);
+	}
+}
+
+/* wave A's melp_syn: every period's parameters and excitation
+ * (harm_syn_pitch), handed over instead of filtered; the state it moves on
+ * is DecState's excitation side */
+template <class Hb>
+MN void melp_syn_a(DecState *D, MelpParam *par, Hb hb)
+{
+	PROF_SCOPE(18);
+	SynFrame F;
+	syn_frame_begin<false>(D, par, F);
+	alignas(4) int16_t run[FRAME + PITCHMAX + 1];
+	const Word16 sb_start = D->syn_begin;
+	int np = 0;
+	while (D->syn_begin < FRAME) {
+		const Word16 sb0 = D->syn_begin;
+		SynPer P;
+		syn_period(D, par, F, sb0, P);
+		harm_syn_pitch(D, P.fs_real, &run[sb0 - sb_start], P.fc, P.len);
+		const int k = HB_PER + np * HB_PW;
+		hb.put(k, hb_pack(P.len, P.pulse_gain));
+		hb.put(k + 1, hb_pack(P.gain, P.tilt_cof[1]));
+		hb_put_vec(hb, k + 2, P.ase_den, LPC_ORD);
+		hb_put_vec(hb, k + 2 + LPC_ORD / 2, &P.ase_num[1], LPC_ORD);
+		hb_put_vec(hb, k + 2 + LPC_ORD, &P.lpc[1], LPC_ORD);
+		np++;
+		D->syn_begin = add(sb0, P.len);
+	}
+	const int total = D->syn_begin - sb_start;
+	run[total] = 0;
+	hb.put(HB_NP, (uint32_t) np | ((uint32_t) total << 16));
+	hb_put_vec(hb, HB_LSF, D->prev_par.lsf, LPC_ORD);
+	hb_put_vec(hb, HB_LSF + LPC_ORD / 2, par->lsf, LPC_ORD);
+	for (int i = 0; i < total; i += 2)
+		hb.put(HB_EXC + i / 2, hb_pack(run[i], run[i + 1]));
+	syn_frame_end(D, par, F);
+}
+
+/* wave B's melp_syn on A's hand-over: the synthesis filters and scale_adj
+ * per period, the dispersion, the postfilter; the state it moves on is
+ * DecState's filter side (its syn_begin and syn_started are a private
+ * replica of A's, advanced the same way) */
+template <class Hb>
+MN void melp_syn_b(DecState *D, const Hb hb, int16_t *out)
+{
+	PROF_SCOPE(18);
+	if (!D->syn_started) {	/* the filter side of the first call's setup */
+		v_zero(D->disp_del, DISP_ORD);
+		v_zero(D->ase_del, LPC_ORD);
+		v_zero(D->tilt_del, 1);
+		D->syn_started = 1;
+	}
+	const uint32_t h = hb.get(HB_NP);
+	const int np = (int) (h & 0xffff), total = (int) (h >> 16);
+	int16_t prev_lsf[LPC_ORD], cur_lsf[LPC_ORD];
+	hb_get_vec(hb, HB_LSF, prev_lsf, LPC_ORD);
+	hb_get_vec(hb, HB_LSF + LPC_ORD / 2, cur_lsf, LPC_ORD);
+	alignas(4) int16_t run[FRAME + PITCHMAX + 1];
+	/* (reading the run in blocks of 8 dwords, loads issued together, measured
+	 * slower: 3.13 vs 3.02 ms at 32,768 channels, profiles/r06c_*) */
+	for (int i = 0; i < total; i += 2) {
+		const uint32_t x = hb.get(HB_EXC + i / 2);
+		run[i] = lo16(x);
+		run[i + 1] = hi16(x);
+	}
+	int16_t pre[DISP_ORD + FRAME + PITCHMAX];
+	const Word16 sb_start = D->syn_begin;
+	v_copy(pre, D->disp_del, DISP_ORD);
+	int r = 0;
+	for (int p = 0; p < np; p++) {
+		const int k = HB_PER + p * HB_PW;
+		const uint32_t w0 = hb.get(k), w1 = hb.get(k + 1);
+		const Word16 len = lo16(w0), pulse_gain = hi16(w0), gain = lo16(w1);
+		int16_t ase_den[LPC_ORD], ase_num[LPC_ORD + 1], lpc[LPC_ORD], tilt[2];
+		tilt[0] = SW_MAX_;
+		tilt[1] = hi16(w1);
+		ase_num[0] = 4096;
+		hb_get_vec(hb, k + 2, ase_den, LPC_ORD);
+		hb_get_vec(hb, k + 2 + LPC_ORD / 2, &ase_num[1], LPC_ORD);
+		hb_get_vec(hb, k + 2 + LPC_ORD, lpc, LPC_ORD);
+		Word32 e0 = syn_chain(D, &run[r], len, pulse_gain, ase_den, ase_num, tilt, lpc);
+		scale_adj(D, &run[r], gain, len, 10, 26214, e0, &pre[DISP_ORD + r]);
+		r += len;
+	}
+	D->syn_begin = add(sb_start, (Word16) total);
+	syn_disperse(D, pre, sb_start, out);
+	postfilt(D, out, prev_lsf, cur_lsf);
 	D->syn_begin = sub(D->syn_begin, FRAME);
 }
+
+/* The two-wave decoder's phase program for one superframe: phase p (0 ..
+ * NF) has wave A (role 0) read the channel (p = 0) and synthesise frame p's
+ * excitation into buffer p & 1, while wave B (role 1) filters frame p - 1
+ * from buffer (p - 1) & 1 into out (B also lays down the previous
+ * superframe's carried samples at p = 0).  Phases are separated by a
+ * barrier; the buffers are the only data the two waves share. */
+template <class Hb>
+MD void dec2_phase(DecState *D, int16_t *out, Hb hb0, Hb hb1, int role, int p)
+{
+	if (role == 0) {
+		if (p == 0)
+			D->erase = low_rate_chn_read(D);
+		if (p < NF)
+			melp_syn_a(D, &D->par[p], (p & 1) ? hb1 : hb0);
+	} else if (p == 0) {
+		/* syn_begin < PITCHMAX <= BLOCK always, so the reference's
+		 * "impossible" syn_begin > frameSize branch (melp_syn.c:120-125)
+		 * is not restated */
+		if (D->syn_begin > 0)
+			v_copy(out, D->sigsave, D->syn_begin);
+	} else {
+		const int i = p - 1;
+		melp_syn_b(D, (i & 1) ? hb1 : hb0, &out[i * FRAME]);
+		if (D->syn_begin > 0 && i < NF - 1)
+			v_copy(&out[(i + 1) * FRAME], D->sigsave, D->syn_begin);
+	}
+}
+#define DEC2_PHASES (NF + 1)
+#endif
 
 /* synthesis :110 -- melpe_s: D->chbuf (11 bytes) -> 540 samples */
 MN void decode_superframe(DecState *D, int16_t *out)

@@ -84,12 +84,17 @@ int kl_ana_warm(int n, hipStream_t s);
 int kl_harm_warm(int n, hipStream_t s);
 int kl_ana_mw_warm(int n, hipStream_t s);
 int kl_dec_warm(int n, hipStream_t s);
+int kl_dec2_warm(int n, hipStream_t s);
 size_t kl_ana_private(void);
 size_t kl_ana_mw_private(void);
 size_t kl_harm_private(void);
 size_t kl_harm_wave_private(void);
 size_t kl_npp_private(void);
 size_t kl_dec_private(void);
+size_t kl_dec2_private(void);
+size_t kl_decode2_hb_words(int n);
+int kl_decode2(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
+	       const int *perm, const int *nlive, uint32_t *hbuf, hipStream_t s);
 int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active, int n,
 	      const int *perm, const int *nlive,
 	      hipStream_t s);
@@ -707,6 +712,10 @@ static hipError_t bin_release(BinBuf &b, hipStream_t s)
 /* k_enc_ana_mw holds two workgroups (of 4 waves, 64 channels) per CU, so it
  * keeps every workgroup resident up to 512 of them */
 #define MW_MAX_CHANNELS (512 * WAVE)
+/* the two-wave decoder (k_decode2) by default up to this many channels per
+ * engine: 2,048 waves (two per SIMD) at 65,536 channels, where the lane
+ * decoder has one wave per SIMD */
+#define DEC2_MAX_CHANNELS (1024 * WAVE)
 
 struct melpe_engine {
 	int device = 0;
@@ -726,6 +735,8 @@ struct melpe_engine {
 	int lane_order = -1;	/* 1 on, 0 off, -1 the MELPE_BIN default */
 	int ana_waves = 0;	/* waves per 64 channels in k_enc_ana(_mw); 0: by channel count */
 	uint32_t *d_lq = nullptr;	/* k_enc_ana_mw's lsf_vq score rows (engine_reserve) */
+	int dec_waves = 0;	/* waves per 64 channels of the decoder; 0: by channel count */
+	uint32_t *d_hb = nullptr;	/* k_decode2's hand-over buffers (engine_reserve) */
 	/* the live-count mapping (ana_launch): a superframe with at most this
 	 * many live channels runs the multi-wave kernel (0: off) */
 	int mw_live_max = MW_MAX_CHANNELS;
@@ -850,6 +861,23 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 	return rc;
 }
 
+/* Waves per 64 channels of the decoder: 1 = one lane per channel
+ * (k_decode); 2 = the two-wave decoder (k_decode2), for channel counts that
+ * leave SIMDs idle in lane mode.  MELPE_DEC_NW overrides the automatic
+ * choice (diagnostics), not an explicit melpe_engine_set_dec_waves. */
+static int dec_waves_for(melpe_engine *e)
+{
+	static int env = -2;
+	if (env == -2) {
+		const char *v = getenv("MELPE_DEC_NW");
+		env = v ? atoi(v) : -1;
+	}
+	int nw = e->dec_waves ? e->dec_waves : env;
+	if (nw != 1 && nw != 2)
+		nw = e->channels <= DEC2_MAX_CHANNELS ? 2 : 1;
+	return nw == 2 && e->d_hb ? 2 : 1;
+}
+
 static int dec_launch(melpe_engine *e, int16_t *d_sp, const uint8_t *d_bits, const uint8_t *d_act,
 		      hipStream_t s)
 {
@@ -861,8 +889,11 @@ static int dec_launch(melpe_engine *e, int16_t *d_sp, const uint8_t *d_bits, con
 				   d_act, e->channels, s, &on);
 	if (er != hipSuccess)
 		return (int) er;
-	int rc = kl_decode(e->d_dec, d_sp, d_bits, d_act, e->channels, on ? b.perm : nullptr,
-			   on ? (const int *) (b.ctl + 2 * NBIN) : nullptr, s);
+	const int *perm = on ? b.perm : nullptr;
+	const int *nlive = on ? (const int *) (b.ctl + 2 * NBIN) : nullptr;
+	int rc = dec_waves_for(e) == 2
+			 ? kl_decode2(e->d_dec, d_sp, d_bits, d_act, e->channels, perm, nlive, e->d_hb, s)
+			 : kl_decode(e->d_dec, d_sp, d_bits, d_act, e->channels, perm, nlive, s);
 	if (rc == 0 && on)
 		rc = (int) bin_release(b, s);
 	return rc;
@@ -1050,6 +1081,8 @@ static int engine_warm(melpe_engine *e)
 	for (auto f : warm)
 		if ((er = (hipError_t) f(f == kl_ana_mw_warm ? mw : e->channels, e->stream)) != hipSuccess)
 			return fail("melpe_engine: codec kernel scratch could not be reserved", er);
+	if (e->d_hb && (er = (hipError_t) kl_dec2_warm(e->channels, e->stream)) != hipSuccess)
+		return fail("melpe_engine: codec kernel scratch could not be reserved", er);
 	if ((er = hipStreamSynchronize(e->stream)) != hipSuccess)
 		return fail("melpe_engine: codec kernel scratch could not be reserved", er);
 	return 0;
@@ -1067,6 +1100,11 @@ static int engine_reserve(melpe_engine *e)
 	if ((er = hipMalloc(&e->d_lq, sizeof(uint32_t) * kl_enc_ana_mw_lq_words(e->channels))) != hipSuccess) {
 		e->d_lq = nullptr;
 		return fail("melpe_engine_create: multi-wave score rows", er);
+	}
+	if (e->channels <= DEC2_MAX_CHANNELS &&
+	    (er = hipMalloc(&e->d_hb, sizeof(uint32_t) * kl_decode2_hb_words(e->channels))) != hipSuccess) {
+		e->d_hb = nullptr;
+		return fail("melpe_engine_create: two-wave decoder hand-over buffers", er);
 	}
 	const int mw = e->channels < MW_MAX_CHANNELS ? e->channels : MW_MAX_CHANNELS;
 	/* The runtime keeps a queue's scratch between dispatches only below its
@@ -1094,6 +1132,8 @@ static int engine_reserve(melpe_engine *e)
 		size_t need = per_wave * waves;
 		if (mw_wave * mw_waves > need)
 			need = mw_wave * mw_waves;
+		if (e->d_hb && kl_dec2_private() * WAVE * 2 * waves > need)
+			need = kl_dec2_private() * WAVE * 2 * waves;
 		if (ww * WAVE * resident > need)
 			need = ww * WAVE * resident;
 		size_t cur = 0, mx = 0;
@@ -1215,6 +1255,18 @@ int melpe_engine_last_ana_waves(melpe_engine *e)
 	return v;
 }
 
+int melpe_engine_set_dec_waves(melpe_engine *e, int waves)
+{
+	if (!e || !(waves == 0 || waves == 1 || waves == 2))
+		return fail_msg("melpe_engine_set_dec_waves: waves must be 0 (auto), 1 or 2");
+	if (waves == 2 && !e->d_hb)
+		return fail_msg("melpe_engine_set_dec_waves: the two-wave decoder is available up to "
+				"65,536 channels per engine");
+	std::lock_guard<std::recursive_mutex> lk(e->mu);
+	e->dec_waves = waves;
+	return 0;
+}
+
 int melpe_engine_set_ana_waves(melpe_engine *e, int waves)
 {
 	if (!e || !(waves == 0 || waves == 1 || waves == 4))
@@ -1240,6 +1292,7 @@ int melpe_engine_destroy(melpe_engine *e)
 	hipFree(e->bin_enc.perm);
 	hipFree(e->bin_dec.perm);
 	hipFree(e->d_lq);
+	hipFree(e->d_hb);
 	hipFree(e->d_res);
 	for (auto &m : e->marks)
 		hipEventDestroy(m.second);
@@ -1372,8 +1425,8 @@ int melpe_npp_host(melpe_engine *e, int16_t *sp, int frames, int stride, const u
 			hipError_t er = hipMemcpyAsync(sp, d, bytes, hipMemcpyDeviceToHost, e->stream);
 			if (er == hipSuccess)
 				er = hipEventRecord(e->ev_host, e->stream);
-				if (er == hipSuccess)
-					er = hipEventSynchronize(e->ev_host);
+			if (er == hipSuccess)
+				er = hipEventSynchronize(e->ev_host);
 			if (er != hipSuccess)
 				rc = fail("npp copy back", er);
 		}

@@ -232,6 +232,38 @@ int emu_decode(emu_engine *e, int16_t *sp, const unsigned char *bits)
 	return 0;
 }
 
+#if !defined(MELPE_OPCOUNT)
+/* the two-wave decoder (decoder.h dec2_phase) as k_decode2 runs it: wave A
+ * and wave B each on a private copy of the record, phase by phase, the two
+ * hand-over buffers the only shared data; each writes back its own side */
+struct HostHb {
+	uint32_t *v;
+	uint32_t get(int k) const { return v[k]; }
+	void put(int k, uint32_t x) const { v[k] = x; }
+};
+
+int emu_decode2(emu_engine *e, int16_t *sp, const unsigned char *bits)
+{
+	static uint32_t hb[2][HB_WORDS];
+	static DecState W[2];
+	for (int c = 0; c < e->channels; c++) {
+		DecState *D = &e->dec[c];
+		memset(hb, 0x5a, sizeof hb);	/* nothing may read a word before it is written */
+		for (int r = 0; r < 2; r++)
+			W[r] = *D;
+		memcpy(W[0].chbuf, bits + c * 11, 11);
+		memset(W[1].chbuf, 0xa5, 11);	/* B never reads the channel */
+		int16_t *out = sp + (size_t) c * BLOCK;
+		for (int p = 0; p < DEC2_PHASES; p++)
+			for (int r = 0; r < 2; r++)
+				dec2_phase(&W[r], out, HostHb{hb[0]}, HostHb{hb[1]}, r, p);
+		memcpy(D, &W[0], DEC_B_BEG);
+		memcpy((char *) D + DEC_B_BEG, (const char *) &W[1] + DEC_B_BEG, sizeof(DecState) - DEC_B_BEG);
+	}
+	return 0;
+}
+#endif
+
 /* per-superframe debug view of channel c: melp_par (3 x 30 int16) and
  * quant_par (30 int16), in the layout oracle/ref_tool.c dumps */
 int emu_enc_params(emu_engine *e, int c, int16_t *out)

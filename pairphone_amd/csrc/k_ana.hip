@@ -35,7 +35,7 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 		const int L = *nlive;
 		if (!gate.open(L))
 			return;
-		gate.mark(c == 0, 1);
+		gate.mark(c == 0 && L > 0, 1);	/* no live channel: the tag stays 0 */
 		if (c >= L)
 			return;
 		c = perm[c];

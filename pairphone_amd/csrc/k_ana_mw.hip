@@ -85,7 +85,7 @@ __global__ __launch_bounds__(WAVE * NW, MELPE_MW_WAVES) void k_enc_ana_mw(EncSta
 	 * live count: uniform per launch, so every wave leaves before a barrier */
 	if (perm && !gate.open(count))
 		return;
-	gate.mark(blockIdx.x == 0 && threadIdx.x == 0, NW);
+	gate.mark(blockIdx.x == 0 && threadIdx.x == 0 && count > 0, NW);	/* 0 live: tag stays 0 */
 	for (int grp = blockIdx.x; grp * WAVE < count; grp += gridDim.x) {
 	int c = grp * WAVE + t;
 	bool live;

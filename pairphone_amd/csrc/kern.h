@@ -49,7 +49,9 @@ using namespace mlp;
  * member is this guard; callee frames sit above the kernel frame, so no
  * private object the codec touches starts below FLAT_GUARD_BYTES.
  */
+#ifndef FLAT_GUARD_BYTES
 #define FLAT_GUARD_BYTES 4608
+#endif
 
 /* keep the guard alive: the compiler may not drop or shrink the object */
 #define PIN_FRAME(obj) __asm__ volatile("" : : "v"(&(obj)) : "memory")

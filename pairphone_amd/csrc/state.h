@@ -194,24 +194,16 @@ static_assert(offsetof(EncState, a) % 16 == 0 && sizeof(EncState) % 16 == 0, "16
 #define DISP_ORD 64
 
 struct alignas(16) DecState {	/* 16-byte aligned: moved with dwordx4 (k_dec.hip) */
+	/* ---- the excitation side: the channel read, the parameter
+	 * interpolation and harm_syn_pitch (wave A of the two-wave decoder,
+	 * decoder.h melp_syn_a) ---- */
 	MelpParam par[NF];	/* melp_par: error paths read last superframe's */
 	QuantParam qpar;	/* quant_par: ditto (uv_flag, indices) */
 	/* melpe/melp_syn.c */
 	MelpParam prev_par;
-	int16_t sigsave[PITCHMAX];
 	int16_t syn_begin, erase;
 	int16_t syn_started, noise_gain, prev_lpc_gain, prev_tilt;
-	int16_t lpc_del[LPC_ORD], ase_del[LPC_ORD], tilt_del[1];
 	int16_t prev_pcof[MIX_ORD + 1], prev_ncof[MIX_ORD + 1];
-	int16_t disp_del[DISP_ORD];
-	/* melpe/melp_sub.c scale_adj */
-	int16_t prev_scale;
-	/* melpe/postfilt.c */
-	int16_t pf_hpm, pf_gain;
-	int16_t pf_mem1[LPC_ORD], pf_mem2[LPC_ORD];
-	int16_t pf_aFIR[LPC_ORD], pf_aIIR[LPC_ORD];
-	int16_t hpf_din[2], hpf_dhi[2], hpf_dlo[2];
-	int16_t lpf_din[2], lpf_dhi[2], lpf_dlo[2];
 	/* melpe/melp_chn.c low_rate_chn_read */
 	int16_t rd_started, rd_prev_uv;
 	int16_t rd_prev_fsmag[NUM_HARM], rd_qplsp[LPC_ORD];
@@ -221,13 +213,33 @@ struct alignas(16) DecState {	/* 16-byte aligned: moved with dwordx4 (k_dec.hip)
 	uint32_t seed;
 	/* 2400 bps path: melpe/melp_sub.c q_gain_dec prev_gain, prev_gain_err */
 	int16_t qgd_prev_gain, qgd_prev_err;
+	/* ---- the filter side, from a 16-byte boundary to the end: the
+	 * synthesis filters, scale_adj, the dispersion FIR, the postfilter
+	 * (wave B, decoder.h melp_syn_b) ---- */
+	/* melpe/melp_syn.c */
+	alignas(16) int16_t sigsave[PITCHMAX];
+	int16_t lpc_del[LPC_ORD], ase_del[LPC_ORD], tilt_del[1];
+	int16_t disp_del[DISP_ORD];
+	/* melpe/melp_sub.c scale_adj */
+	int16_t prev_scale;
+	/* melpe/postfilt.c */
+	int16_t pf_hpm, pf_gain;
+	int16_t pf_mem1[LPC_ORD], pf_mem2[LPC_ORD];
+	int16_t pf_aFIR[LPC_ORD], pf_aIIR[LPC_ORD];
+	int16_t hpf_din[2], hpf_dhi[2], hpf_dlo[2];
+	int16_t lpf_din[2], lpf_dhi[2], lpf_dlo[2];
+	uint32_t fmt_pad_;	/* the tag in the record's last 4 bytes (16-byte size) */
 	uint32_t fmt;	/* record format tag, as EncState's */
 };
+/* the two sides' byte ranges of the record (the two-wave decoder writes each
+ * back from the wave that owns it) */
+#define DEC_B_BEG offsetof(DecState, sigsave)
+static_assert(DEC_B_BEG % 16 == 0, "the filter side starts on a 16-byte boundary");
 static_assert(offsetof(DecState, fmt) + 4 == sizeof(DecState), "DecState's tag ends the record");
 
 /* Layout version of the records (bump on any change to EncState /
  * DecState); the tag also folds in the record size. */
-#define MELPE_REC_LAYOUT 5u
+#define MELPE_REC_LAYOUT 6u
 #define ENC_REC_FMT (0x4d450000u ^ (MELPE_REC_LAYOUT << 24) ^ (uint32_t) sizeof(EncState))
 #define DEC_REC_FMT (0x4d440000u ^ (MELPE_REC_LAYOUT << 24) ^ (uint32_t) sizeof(DecState))
 

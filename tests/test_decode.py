@@ -47,14 +47,15 @@ def decode_all(decode, bits, nsf):
     return pcm
 
 
-def emu_decoder(ch):
+def emu_decoder(ch, fn="emu_decode"):
     lib = emu()
-    lib.emu_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    f = getattr(lib, fn)
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     e = lib.emu_create(ch)
 
     def dec(b):
         sp = np.zeros((ch, 540), np.int16)
-        lib.emu_decode(e, sp.ctypes.data, b.ctypes.data)
+        f(e, sp.ctypes.data, b.ctypes.data)
         return sp
     return lib, e, dec
 
@@ -80,6 +81,30 @@ def test_decode_hostemu_random_bitstreams_match_golden():
     assert pcm[0, :540].tolist() == g["pcm0_first_sf"]
     for c in range(ch):
         assert sha(pcm[c]) == g["pcm_sha256"][c], "channel %d" % c
+
+
+def test_decode2_hostemu_matches_goldens():
+    """The two-wave decoder's phase program (decoder.h dec2_phase: wave A the
+    channel read and the excitation, wave B the filters, dispersion and
+    postfilter one frame behind, each on its own copy of the record, the
+    hand-over buffers pattern-filled) against the decode goldens and the
+    random-bitstream fuzz set."""
+    g, ge = gold("dec_1024.json"), enc_golden()
+    ch, nsf = 4, g["superframes"]
+    bits = np.stack([np.frombuffer(bytes.fromhex(ge["bits_hex"][c]), np.uint8) for c in range(ch)])
+    lib, e, dec = emu_decoder(ch, "emu_decode2")
+    pcm = decode_all(dec, bits, nsf)
+    lib.emu_destroy(e)
+    for c in range(ch):
+        assert sha(pcm[c]) == g["pcm_sha256"][c], "channel %d" % c
+    g = gold("dec_fuzz.json")
+    ch, nsf = 8, g["superframes"]
+    bits = fuzz_bits(g["seed"], g["channels"], nsf)[:ch]
+    lib, e, dec = emu_decoder(ch, "emu_decode2")
+    pcm = decode_all(dec, bits, nsf)
+    lib.emu_destroy(e)
+    for c in range(ch):
+        assert sha(pcm[c]) == g["pcm_sha256"][c], "fuzz channel %d" % c
 
 
 def test_duplex_sharing_hostemu_matches_reference(tmp_path, ref_tool):
@@ -115,6 +140,37 @@ def test_duplex_sharing_hostemu_matches_reference(tmp_path, ref_tool):
     lib.emu_destroy(e)
     np.testing.assert_array_equal(np.concatenate(tx), want_tx)
     np.testing.assert_array_equal(np.concatenate(y), want_y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("waves", [1, 2])
+def test_decode_gpu_mappings_match_golden_and_fuzz(waves):
+    """Both decoder mappings forced on every superframe: one lane per
+    channel (k_decode, the 262,144-channel headline's) and the two-wave
+    decoder (k_decode2, the default up to 65,536 channels), against the
+    1,024-channel goldens and the random-bitstream fuzz set."""
+    from pairphone_amd import MelpeEngine
+    g, ge = gold("dec_1024.json"), enc_golden()
+    C, nsf = g["channels"], g["superframes"]
+    eng = MelpeEngine(C)
+    eng.set_dec_waves(waves)
+    x = signals(g["seed"], C, nsf)
+    enc = MelpeEngine(C)
+    bits, _ = run_superframes(enc.encode, x, nsf)
+    enc.close()
+    assert [c for c in range(C) if sha(bits[c]) != ge["bits_sha256"][c]] == []
+    pcm = decode_all(eng.decode, bits, nsf)
+    eng.close()
+    bad = [c for c in range(C) if sha(pcm[c]) != g["pcm_sha256"][c]]
+    assert not bad, "decoder mismatch on %d channels, first %s" % (len(bad), bad[:8])
+    gf = gold("dec_fuzz.json")
+    fb = fuzz_bits(gf["seed"], gf["channels"], gf["superframes"])
+    eng = MelpeEngine(gf["channels"])
+    eng.set_dec_waves(waves)
+    pcm = decode_all(eng.decode, fb, gf["superframes"])
+    eng.close()
+    bad = [c for c in range(gf["channels"]) if sha(pcm[c]) != gf["pcm_sha256"][c]]
+    assert not bad, "fuzz mismatch on %d channels, first %s" % (len(bad), bad[:8])
 
 
 @pytest.mark.gpu

@@ -116,6 +116,26 @@ def test_encode_gpu_1024_channels_match_golden():
 
 
 @pytest.mark.gpu
+def test_encode_gpu_lane_kernel_alone_1024_channels_match_golden():
+    """The headline's lane-per-channel analysis (k_enc_ana -> k_enc_harm ->
+    k_enc_tail) forced on every superframe (set_ana_waves(1)): at 1,024
+    channels the automatic choice would run the four-wave kernel instead."""
+    from pairphone_amd import MelpeEngine
+    g = golden()
+    C, nsf = g["channels"], g["superframes"]
+    x = signals(g["seed"], C, nsf)
+    eng = MelpeEngine(C)
+    eng.set_ana_waves(1)
+    bits, npp = run_superframes(eng.encode, x, nsf)
+    assert eng.last_ana_waves() == 1
+    eng.close()
+    bad = [c for c in range(C) if sha(bits[c]) != g["bits_sha256"][c]]
+    badn = [c for c in range(C) if sha(npp[c]) != g["npp_sha256"][c]]
+    assert not bad, "bitstream mismatch on %d channels, first %s" % (len(bad), bad[:8])
+    assert not badn, "NPP output mismatch on %d channels, first %s" % (len(badn), badn[:8])
+
+
+@pytest.mark.gpu
 def test_encode_host_two_threads_one_engine():
     """Two host threads calling melpe_encode_host on one engine at once,
     each on its own half of the channels (disjoint masks): every call holds

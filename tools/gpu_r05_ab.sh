@@ -4,7 +4,7 @@
 # product build) or the name of build/var/<name>.so.
 #   bash tools/gpu_r05_ab.sh <tag> <channels> cur cur:MELPE_BIN=0 ko_analysis ...
 cd $GRAFT_REPO_ROOT && T=$1 && C=$2 && shift 2 && O=gpurun_out/$T && mkdir -p $O && export TMPDIR=/tmp &&
-B="bench.py --no-cpu-baseline --no-host-leg --no-duplex --no-side-legs --total-channels 0 --tx-channels 0 --channels $C --steps 6 --warmup 2" &&
+B="bench.py --no-cpu-baseline --no-host-leg --no-duplex --no-side-legs --total-channels 0 --tx-channels 0 --rt-channels 0 --channels $C --steps 6 --warmup 2" &&
 i=0 &&
 for v in "$@"; do
   i=$((i+1))
