@@ -80,6 +80,7 @@ REF_TOOL = os.path.join(ROOT, "oracle", "_ref", "ref_tool")
 ANALYSIS_LANE = ("k_enc_ana<1>", "k_enc_harm", "k_enc_tail")
 ANALYSIS_MW = ("k_enc_ana_mw<4>",)
 MW_MAX_CHANNELS = 32768
+DEC2_MAX_CHANNELS = 65536    # engine.hip: the two-wave decoder up to here
 
 
 def parse(argv=None):
@@ -698,7 +699,9 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
             w_dec, _ = w_over(oc, "W_dec", W, W + K)
             dec["W_per_channel_superframe"] = w_dec
             dec["roofline_frac"] = w_dec * C / (dec["kernel_ms"] / 1e3) / 1e12 / PEAK_VALU_TOPS
-            dec["traffic"], _ = pmc_traffic("k_decode", C)
+            # the engine runs the two-wave decoder up to DEC2_MAX_CHANNELS
+            dec["kernel"] = "k_decode2" if C <= DEC2_MAX_CHANNELS else "k_decode"
+            dec["traffic"], _ = pmc_traffic(dec["kernel"], C)
         if side.get("vad") and oc.get("W_vad_per_sf"):
             v = side["vad"]
             vach = oc["W_vad_per_sf"] * C / (v["kernel_ms"] / 1e3) / 1e12

@@ -747,10 +747,34 @@ MN Word16 L_divider2(Word32 num, Word32 den, int16_t nsh, int16_t dsh)
 	return neg ? negate(q) : q;
 }
 
+/* The fixed-point math tables (log10_fxp, L_log10_fxp, pow10_fxp) from an
+ * LDS copy (MELPE_MATH_LDS, the NPP kernels: their per-bin log / pow
+ * lookups gather at per-lane indices, from constant memory a global-memory
+ * round trip each), else from the table blob */
+#define MOFF_pow10_q_table 0
+#define MOFF_pow10_tens_table (MOFF_pow10_q_table + TLEN_pow10_q_table)
+#define MOFF_log_table (MOFF_pow10_tens_table + TLEN_pow10_tens_table)
+#define MOFF_pow10_table (MOFF_log_table + TLEN_log_table)
+#define MTAB_WORDS (MOFF_pow10_table + TLEN_pow10_table)	/* 526 */
+#if defined(MELPE_MATH_LDS) && defined(__HIP__)
+extern __shared__ int16_t s_mtab[];
+#define TBM(name) ((const int16_t *) (s_mtab + MOFF_##name))
+#else
+#define TBM(name) TB(name)
+#endif
+/* word i of the packed copy: the four tables end to end */
+MD int mtab_src(int i)
+{
+	return i < MOFF_pow10_tens_table ? TOFF_pow10_q_table + i
+	       : i < MOFF_log_table	 ? TOFF_pow10_tens_table + (i - MOFF_pow10_tens_table)
+	       : i < MOFF_pow10_table	 ? TOFF_log_table + (i - MOFF_log_table)
+					 : TOFF_pow10_table + (i - MOFF_pow10_table);
+}
+
 /* log10_fxp :169 */
 MN Word16 log10_fxp(Word16 x, Word16 Q)
 {
-	const int16_t *lt = TB(log_table);
+	const int16_t *lt = TBM(log_table);
 	Word16 sh = sub(7, Q);
 	if (!x)
 		return (Word16) -SW_MAX_;
@@ -771,7 +795,7 @@ MN Word16 log10_fxp(Word16 x, Word16 Q)
 /* L_log10_fxp :242 */
 MN Word16 L_log10_fxp(Word32 x, Word16 Q)
 {
-	const int16_t *lt = TB(log_table);
+	const int16_t *lt = TBM(log_table);
 	Word16 sh = sub(23, Q);
 	if (!x)
 		return (Word16) -SW_MAX_;
@@ -792,9 +816,9 @@ MN Word16 L_log10_fxp(Word32 x, Word16 Q)
 /* pow10_fxp :308 */
 MN Word16 pow10_fxp(Word16 x, Word16 Q)
 {
-	const int16_t *tab = TB(pow10_table);
-	const int16_t *tens = TB(pow10_tens_table);
-	const int16_t *qt = TB(pow10_q_table);
+	const int16_t *tab = TBM(pow10_table);
+	const int16_t *tens = TBM(pow10_tens_table);
+	const int16_t *qt = TBM(pow10_q_table);
 	Word16 tm = shr(x, 12);
 	if (tm < -4)
 		return 0;

@@ -48,9 +48,17 @@ using namespace mlp;
  * calls into the codec therefore owns exactly one private object whose first
  * member is this guard; callee frames sit above the kernel frame, so no
  * private object the codec touches starts below FLAT_GUARD_BYTES.
+ * Since round 4 the build itself fails on any FLAT instruction in a codec
+ * kernel (build.py check_no_flat: the codec TUs inline their whole call
+ * tree, so every private access is a scratch_ instruction), which removes
+ * the hazard the guard covered.  The guard was 4,608 bytes (31% of the lane
+ * analysis' frame); the A/B at 262,144 channels measured it time-neutral
+ * (profiles/r06_c_flat_guard_ab_262k.txt) and it only inflated every
+ * queue's scratch reservation, so it is 16 bytes now (the frame layouts
+ * keep their 16-byte alignment).
  */
 #ifndef FLAT_GUARD_BYTES
-#define FLAT_GUARD_BYTES 4608
+#define FLAT_GUARD_BYTES 16
 #endif
 
 /* keep the guard alive: the compiler may not drop or shrink the object */

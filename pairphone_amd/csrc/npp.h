@@ -72,6 +72,20 @@ struct NppScratch {
 	int16_t ybuf[2 * NPP_WIN + 2];
 };
 
+/* The wave form's scratch (npp_wave.h): vk, noisespect2 and alpha_var are
+ * written and read back for the same bin within one pass over the bins, so
+ * there they are the lane's registers (the per-bin functions take them as
+ * parameters); only what crosses bins or passes stays in LDS. */
+struct NppScratchW {
+	int16_t YY[NPP_NB], YY_shift[NPP_NB];
+	int16_t var_rel[NPP_NB];
+	/* the first (NPP_WIN + 2) dwords double as wv_enh_init's temp_yy
+	 * (npp_wave.h NppWave), which runs while ybuf is live: ybuf after it */
+	int16_t pad_[2 * (NPP_WIN + 2) - 3 * NPP_NB];
+	int16_t ybuf[2 * NPP_WIN + 2];
+};
+static_assert(offsetof(NppScratchW, ybuf) == 4 * (NPP_WIN + 2), "ybuf clear of wv_enh_init's temp_yy");
+
 MD void npp_reset(NppState *s)
 {
 	int16_t *p = (int16_t *) s;
@@ -123,7 +137,7 @@ MD Word32 npp_spec_sum(const int16_t *v, const int16_t *vs, Word16 maxs)
 }
 
 /* gain_mod :211 -- speech-presence-uncertainty modification of the gain */
-MD void npp_gain_mod_bin(const NppState *s, const NppScratch *w, const int16_t *qk,
+MD void npp_gain_mod_bin(const NppState *s, Word16 vk, Word16 vk_shift, const int16_t *qk,
 			 int16_t *GainD, int i)
 {
 	{
@@ -137,8 +151,8 @@ MD void npp_gain_mod_bin(const NppState *s, const NppScratch *w, const int16_t *
 		sh = norm_l(L);
 		Word16 t2 = extract_h(L_shl(L, sh));
 		Word16 t2sh = sub(shl(tsh, 1), sh);
-		L = L_mult(w->vk[i], -23637);
-		sh = add(w->vk_shift[i], 1);
+		L = L_mult(vk, -23637);
+		sh = add(vk_shift, 1);
 		L = L_shr(L, sub(15, sh));
 		sh = sub(s->ksi_shift[i], tsh);
 		Word16 t3, t4;
@@ -180,7 +194,7 @@ MN void npp_gain_mod(const NppState *s, const NppScratch *w, const int16_t *qk,
 		     int16_t *GainD, int m)
 {
 	for (int i = 0; i < m; i++)
-		npp_gain_mod_bin(s, w, qk, GainD, i);
+		npp_gain_mod_bin(s, w->vk[i], w->vk_shift[i], qk, GainD, i);
 }
 
 /* compute_qk :289 -- a-priori speech absence probability */
@@ -205,8 +219,8 @@ MN void npp_compute_qk(NppState *s, int16_t *qk, const int16_t *gk, const int16_
 }
 
 /* gain_log_mmse :319 */
-MD void npp_gain_log_mmse_bin(NppState *s, NppScratch *w, const int16_t *qk, int16_t *Gain,
-			      const int16_t *gk, const int16_t *gks, int i)
+MD void npp_gain_log_mmse_bin(NppState *s, int16_t &vk, int16_t &vk_shift, const int16_t *qk,
+			      int16_t *Gain, const int16_t *gk, const int16_t *gks, int i)
 {
 	{
 		Word16 t1 = sub(SW_MAX_, qk[i]);
@@ -224,26 +238,26 @@ MD void npp_gain_log_mmse_bin(NppState *s, NppScratch *w, const int16_t *qk, int
 		Word16 kv = divide_s(t2, t1);
 		Word32 L = L_mult(kv, gk[i]);
 		sh = norm_l(L);
-		w->vk[i] = extract_h(L_shl(L, sh));
-		w->vk_shift[i] = sub(gks[i], sh);
-		if (cmp_shift(w->vk[i], w->vk_shift[i], 32767, -52) < 0) {
-			w->vk[i] = 32767;
-			w->vk_shift[i] = -52;
+		vk = extract_h(L_shl(L, sh));
+		vk_shift = sub(gks[i], sh);
+		if (cmp_shift(vk, vk_shift, 32767, -52) < 0) {
+			vk = 32767;
+			vk_shift = -52;
 		}
-		if (cmp_shift(w->vk[i], w->vk_shift[i], 26214, -3) < 0) {
-			t1 = log10_fxp(w->vk[i], 15);
+		if (cmp_shift(vk, vk_shift, 26214, -3) < 0) {
+			t1 = log10_fxp(vk, 15);
 			L = L_shl(L_deposit_l(t1), 14);
-			L = L_add(L, L_shl(L_mult(w->vk_shift[i], 9864), 10));
+			L = L_add(L, L_shl(L_mult(vk_shift, 9864), 10));
 			L = L_mpy_ls(L, -18923);
 			L = L_sub(L, 10066330L);
-		} else if (cmp_shift(w->vk[i], w->vk_shift[i], 25600, 8) > 0) {
+		} else if (cmp_shift(vk, vk_shift, 25600, 8) > 0) {
 			L = 1;
-			w->vk[i] = 25600;
-			w->vk_shift[i] = 8;
-		} else if (cmp_shift(w->vk[i], w->vk_shift[i], 32767, 0) > 0) {
-			L = L_mult(w->vk[i], -17039);
-			L = L_sub(L, L_shr(L_deposit_h(8520), w->vk_shift[i]));
-			L = L_shr(L, sub(14, w->vk_shift[i]));
+			vk = 25600;
+			vk_shift = 8;
+		} else if (cmp_shift(vk, vk_shift, 32767, 0) > 0) {
+			L = L_mult(vk, -17039);
+			L = L_sub(L, L_shr(L_deposit_h(8520), vk_shift));
+			L = L_shr(L, sub(14, vk_shift));
 			L = L_mpy_ls(L, 27213);
 			sh = extract_h(L_shl(L, 1));
 			t1 = (Word16) (extract_l(L) & 0x7fff);
@@ -252,9 +266,9 @@ MD void npp_gain_log_mmse_bin(NppState *s, NppScratch *w, const int16_t *qk, int
 			L = L_shl(L_deposit_l(t1), 10);
 			L = L_shl(L, sh);
 		} else {
-			t1 = w->vk[i];
-			if (w->vk_shift[i] != 0)
-				t1 = shl(t1, w->vk_shift[i]);
+			t1 = vk;
+			if (vk_shift != 0)
+				t1 = shl(t1, vk_shift);
 			t1 = log10_fxp(t1, 15);
 			L = L_shl(L_deposit_l(t1), 13);
 			L = L_mpy_ls(L, -25297);
@@ -283,7 +297,7 @@ MN void npp_gain_log_mmse(NppState *s, NppScratch *w, const int16_t *qk, int16_t
 			  const int16_t *gk, const int16_t *gks, int m)
 {
 	for (int i = 0; i < m; i++)
-		npp_gain_log_mmse_bin(s, w, qk, Gain, gk, gks, i);
+		npp_gain_log_mmse_bin(s, w->vk[i], w->vk_shift[i], qk, Gain, gk, gks, i);
 }
 
 /* ksi_min_adapt :428 */
@@ -387,7 +401,9 @@ MD Word16 npp_sm_period_scalars(NppState *s, Word16 maxs, Word32 L, Word16 YY_av
 }
 
 /* per-bin part of smoothed_periodogram */
-MD void npp_sm_period_bin(NppState *s, NppScratch *w, Word16 anum, Word16 amin, int i)
+template <class SC>
+MD void npp_sm_period_bin(NppState *s, SC *w, Word16 anum, Word16 amin, int i, int16_t &ns2, int16_t &ns2_shift,
+			  int16_t &alpha_var)
 {
 	Word16 ns = s->noisespect[i];
 	Word32 Lt, L;
@@ -408,8 +424,8 @@ MD void npp_sm_period_bin(NppState *s, NppScratch *w, Word16 anum, Word16 amin, 
 	Word16 nsh = norm_l(L);
 	ns = extract_h(L_shl(L, nsh));
 	Word16 nssh = sub(shl(s->noise_shift[i], 1), nsh);
-	w->noisespect2[i] = ns;
-	w->noise2_shift[i] = nssh;
+	ns2 = ns;
+	ns2_shift = nssh;
 	if (t == SW_MIN_)
 		L = 0x7fffffff;
 	else
@@ -430,7 +446,7 @@ MD void npp_sm_period_bin(NppState *s, NppScratch *w, Word16 anum, Word16 amin, 
 	if (ta < amin)
 		ta = amin;
 	t = sub(SW_MAX_, ta);
-	w->alpha_var[i] = ta;
+	alpha_var = ta;
 	Word16 ds = sub(w->YY_shift[i], s->sm_shift[i]);
 	if (ds > 0) {
 		L = L_shr(L_mult(ta, s->smoothedspect[i]), ds);
@@ -457,14 +473,15 @@ MN void npp_smoothed_periodogram(NppState *s, NppScratch *w, Word16 YY_av, Word1
 	Word16 amin;
 	Word16 anum = npp_sm_period_scalars(s, maxs, L, YY_av, yy_shift, &amin);
 	for (int i = 0; i < NPP_NB; i++)
-		npp_sm_period_bin(s, w, anum, amin, i);
+		npp_sm_period_bin(s, w, anum, amin, i, w->noisespect2[i], w->noise2_shift[i], w->alpha_var[i]);
 }
 
 /* bias_compensation :695, first per-bin pass: the variance estimates and
  * the relative variance var_rel[i] (0..16384) */
-MD void npp_bias1_bin(NppState *s, NppScratch *w, int i)
+template <class SC>
+MD void npp_bias1_bin(NppState *s, SC *w, int i, Word16 alpha_var, Word16 ns2, Word16 ns2_shift)
 {
-	Word16 beta = mult(w->alpha_var[i], w->alpha_var[i]);
+	Word16 beta = mult(alpha_var, alpha_var);
 	if (beta > 26214)
 		beta = 26214;
 	Word32 L = L_mult(sub(SW_MAX_, beta), s->smoothedspect[i]);
@@ -508,8 +525,8 @@ MD void npp_bias1_bin(NppState *s, NppScratch *w, int i)
 	}
 	s1 = sub(norm_l(L), 1);
 	Word16 t1 = extract_h(L_shl(L, s1));
-	Word16 t = sub(sub(s4, s1), w->noise2_shift[i]);
-	w->var_rel[i] = divide_s(t1, w->noisespect2[i]);
+	Word16 t = sub(sub(s4, s1), ns2_shift);
+	w->var_rel[i] = divide_s(t1, ns2);
 	if (cmp_shift(w->var_rel[i], t, 16384, 0) > 0)
 		w->var_rel[i] = 16384;
 	else
@@ -521,7 +538,8 @@ MD void npp_bias1_bin(NppState *s, NppScratch *w, int i)
 /* the scalar middle of bias_compensation: vsum = sum of var_rel over the
  * bins (each 0..16384, so the reference's L_add chain never saturates and
  * any order gives the same sum); returns vsq, sets f1/f2 */
-MD Word16 npp_bias_scalars(NppState *s, const NppScratch *w, Word32 vsum, Word16 *f1, Word16 *f2)
+template <class SC>
+MD Word16 npp_bias_scalars(NppState *s, const SC *w, Word32 vsum, Word16 *f1, Word16 *f2)
 {
 	vsum = L_shl(vsum, 1);
 	vsum = L_sub(vsum, L_deposit_l(w->var_rel[0]));
@@ -537,7 +555,8 @@ MD Word16 npp_bias_scalars(NppState *s, const NppScratch *w, Word32 vsum, Word16
 }
 
 /* second per-bin pass: the bias-compensated spectra for the minimum search */
-MD void npp_bias2_bin(const NppState *s, const NppScratch *w, int16_t &bsp, int16_t &bsh,
+template <class SC>
+MD void npp_bias2_bin(const NppState *s, const SC *w, int16_t &bsp, int16_t &bsh,
 		      int16_t &bsub, int16_t &bsubsh, Word16 vsq, Word16 f1, Word16 f2, int i)
 {
 	Word32 L3 = L_mult(vsq, s->smoothedspect[i]);
@@ -568,7 +587,7 @@ MN void npp_bias_compensation(NppState *s, NppScratch *w, int16_t *bsp, int16_t 
 {
 	Word32 vsum = 0;
 	for (int i = 0; i < NPP_NB; i++) {
-		npp_bias1_bin(s, w, i);
+		npp_bias1_bin(s, w, i, w->alpha_var[i], w->noisespect2[i], w->noise2_shift[i]);
 		vsum = L_add(vsum, L_deposit_l(w->var_rel[i]));
 	}
 	Word16 f1, f2;

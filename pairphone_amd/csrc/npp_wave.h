@@ -23,7 +23,7 @@
  *    fixed-point sum over a prefix max of the exponents, the arg-max as a
  *    scan in reference order over the few bins that can win (wv_gain_scan).
  * Scalars of the state are computed redundantly by all lanes and written by
- * all lanes with identical values.  wsync() (a one-wave workgroup barrier)
+ * all lanes with identical values.  wsync() (the wave's own LDS ordering)
  * separates phases whose LDS data crosses lanes.
  */
 #ifndef MELPE_NPP_WAVE_H
@@ -53,7 +53,16 @@ namespace wv {
 	}
 __device__ __forceinline__ void wsync()
 {
+#if defined(MELPE_NPP_WG_WAVES) && MELPE_NPP_WG_WAVES > 1
+	/* several channels' waves per workgroup, each on its own LDS image: the
+	 * LDS serves one wave's instructions in order, so the wave's own
+	 * accesses need only be kept in program order by the compiler */
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
 	__syncthreads();
+#endif
 }
 
 /* wave reductions, result uniform in every lane: DPP within each row of 16
@@ -139,7 +148,7 @@ __device__ __forceinline__ int bin_at(int r0, int r1, int r2, int i)
 /* LDS image of one channel's NPP */
 struct NppWave {
 	union {
-		NppScratch w;	/* YY.., ybuf */
+		NppScratchW w;	/* YY.., ybuf */
 		/* wv_enh_init's temp_yy (the scratch is dead there); may_alias
 		 * dwords, like the record copies */
 		u32_alias ty_init[NPP_WIN + 2];
@@ -637,7 +646,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 {
 	PROF_SCOPE(34);
 	NppState *s = wv_S(W);
-	NppScratch *w = &W->w;
+	NppScratchW *w = &W->w;
 	int16_t *yb = w->ybuf;
 	int16_t *GainD = W->GainD, *gk = W->gk, *gks = W->gks;
 	Word16 sh, t, t1, t2, t3, t4;
@@ -664,6 +673,9 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 		s->enh_i = (int16_t) (s->enh_i + 1);
 
 	int16_t *analy = W->buf;
+	Word16 g, Ysh, YYavs;
+	{
+	PROF_SCOPE(60);
 	int mx = 0;
 #pragma unroll
 	LANE_LOOP(i, NPP_WIN) {
@@ -678,10 +690,17 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 		yb[2 * i + 1] = 0;
 	}
 	wsync();
-	Word16 g = wv_fft_npp(yb, 1, kc, lane);
-	Word16 Ysh = add(ash, g);
-	Word16 YYavs = shl(Ysh, 1);
+	g = wv_fft_npp(yb, 1, kc, lane);
+	Ysh = add(ash, g);
+	YYavs = shl(Ysh, 1);
+	}
 	int maxs = SW_MIN_;
+	int part = 0;
+	/* |Y| of the lane's bins lane + 64 t: read back only by the same lane,
+	 * so it stays in registers (BIN_LOOP) */
+	int16_t ymag[3] = {0, 0, 0}, ymag_sh[3] = {0, 0, 0};
+	{
+	PROF_SCOPE(53);
 	BIN_PASSES(t, i, {
 		Word32 v;
 		if (i == 0)
@@ -698,10 +717,6 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 		maxs = max(maxs, (int) w->YY_shift[i]);
 	})
 	maxs = wmax(maxs);
-	int part = 0;
-	/* |Y| of the lane's bins lane + 64 t: read back only by the same lane,
-	 * so it stays in registers (BIN_LOOP) */
-	int16_t ymag[3] = {0, 0, 0}, ymag_sh[3] = {0, 0, 0};
 	BIN_PASSES(t, i, {
 		Word16 y = w->YY[i], ys = w->YY_shift[i];
 		if (ys & 1) {
@@ -716,6 +731,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 		part += st;
 	})
 	L = wsum(part);
+	}
 	if (L == 0)
 		L = 1;
 	t1 = norm_l(L);
@@ -737,16 +753,22 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	Word16 amin;
 	Word16 anum = npp_sm_period_scalars(s, (Word16) maxs, L, YY_av, YY_av_shift, &amin);
 	part = 0;
+	{
+	PROF_SCOPE(54);
 	BIN_PASSES(t, i, {
-		npp_sm_period_bin(s, w, anum, amin, i);
-		npp_bias1_bin(s, w, i);
+		int16_t ns2, ns2sh, av;	/* bin i's, this lane's only */
+		npp_sm_period_bin(s, w, anum, amin, i, ns2, ns2sh, av);
+		npp_bias1_bin(s, w, i, av, ns2, ns2sh);
 		part += w->var_rel[i];
 	})
+	}
 	Word32 vsum = wsum(part);
 	wsync();
 	Word16 f1, f2;
 	Word16 vsq = npp_bias_scalars(s, w, vsum, &f1, &f2);
 	Word16 slope = npp_noise_slope(s);
+	{
+	PROF_SCOPE(55);
 	BIN_PASSES(t, i, {
 		int16_t bsp, bsh, bsub, bsubsh;	/* bin i's, this lane's only */
 		npp_bias2_bin(s, w, bsp, bsh, bsub, bsubsh, vsq, f1, f2, i);
@@ -754,6 +776,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 		gk[i] = divide_s(shr(w->YY[i], 1), s->lambdaD[i]);
 		gks[i] = sub(add(w->YY_shift[i], 1), s->lambdaD_shift[i]);
 	})
+	}
 	wsync();
 	npp_min_search_post(s);
 	}
@@ -782,7 +805,10 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 			s->agal_shift[i] = sub(ymag_sh[t], n);
 		}
 	} else {
+		{
+		PROF_SCOPE(56);
 		BIN_PASSES(t, i, { npp_ksi_bin(s, gk, gks, i); })
+		}
 		t1 = mult(29491, s->Ksi_min_var);
 		t2 = mult(3277, npp_ksi_min_adapt(nflag, GM_MIN, s->SN_LT, s->SN_LT_shift));
 		Word16 kmv = add(t1, t2);
@@ -842,6 +868,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 				s->SN_LT0_shift = sns;
 			}
 			bool first = !s->qk_started;
+			PROF_SCOPE(57);
 			BIN_PASSES(t, i, {
 				npp_compute_qk_bin(s, s->qk, gk, gks, 19273, first, i);
 				if (s->qk[i] > ENH_QK_MAX)
@@ -851,10 +878,12 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 			})
 			s->qk_started = 1;
 		}
+		PROF_SCOPE(58);
 		BIN_PASSES(t, i, {
-			npp_gain_log_mmse_bin(s, w, s->qk, s->Gain, gk, gks, i);
+			int16_t vk, vksh;	/* bin i's, this lane's only */
+			npp_gain_log_mmse_bin(s, vk, vksh, s->qk, s->Gain, gk, gks, i);
 			GainD[i] = s->Gain[i];
-			npp_gain_mod_bin(s, w, s->qk, GainD, i);
+			npp_gain_mod_bin(s, vk, vksh, s->qk, GainD, i);
 			Word32 v = L_mult(GainD[i], ymag[t]);
 			Word16 n = norm_l(v);
 			s->agal[i] = extract_h(L_shl(v, n));
@@ -863,6 +892,8 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 	}
 	}
 	wsync();
+	{
+	PROF_SCOPE(59);
 	int lm = 0;
 	Word32 tyr[5];	/* temp_yy of samples lane + 64 t, in registers */
 #pragma unroll
@@ -893,6 +924,7 @@ MD void wv_process_frame(NppWave *W, NppState *m, const int16_t *in, int16_t *ou
 #pragma unroll
 	LANE_LOOP(i, NPP_WIN)
 		out[i] = mult(shl(yb[2 * i], osh), kc->win[i >> 6]);
+	}
 	/* noise power for the next frame (npp.c:1621-1635) */
 	maxs = SW_MIN_;
 	BIN_PASSES(t, i, { maxs = max(maxs, (int) s->lambdaD_shift[i]); })
