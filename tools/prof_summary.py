@@ -114,7 +114,7 @@ def main():
         with open(os.path.join(prof, tag + "_pmc.txt"), "w") as f:
             f.write("# rocprofv3 --pmc passes (%s): mean counter value per dispatch\n" % tag)
             for k in sorted(pm):
-                if not k.startswith("k_enc") and k != "k_decode":
+                if not k.startswith("k_enc") and k not in ("k_decode", "k_decode2"):
                     continue
                 f.write("[%s]\n" % k)
                 for cn in sorted(pm[k]):
