@@ -239,6 +239,16 @@ class EngineWorkload:
         self.eng.encode_ana_dev(self.bits[s].data_ptr(), self.pcm[s].data_ptr(), None,
                                 self.rig.sptr)
 
+    def pipe(self, s, nxt):
+        """superframe s's analysis beside superframe nxt's NPP (None: none)"""
+        self.eng.encode_pipe_dev(self.bits[s].data_ptr(), self.pcm[s].data_ptr(),
+                                 None if nxt is None else self.pcm[nxt].data_ptr(), stream=self.rig.sptr)
+
+    def restart(self):
+        """fresh-process state and the raw input again (melpe_engine_reset)"""
+        self.eng.reset()
+        self.regen_pcm()
+
     def dec(self, s):
         if self.out is None:
             self.out = self.rig.torch.empty_like(self.pcm)
@@ -384,6 +394,37 @@ def encode_leg(rig, wl, K, W):
     return timed(rig, [wl.npp, wl.ana], K, W)
 
 
+def pipe_leg(rig, wl, K, W):
+    """The headline step pipelined (melpe_encode_pipe_dev): superframe k's
+    analysis on the engine stream beside superframe k + 1's NPP on the
+    engine's second stream, whose waves take the SIMD slots the analysis'
+    waves free as they finish (the launch's tail: profiles/
+    r06_i_wave_times.jsonl).  W warm-up steps serialised, then a timed
+    region holding exactly K NPPs and K analyses: the NPP of superframe W,
+    then K pipelined steps, the last without a next NPP.  HIP events on the
+    caller's stream bracket each step.  Returns (wall seconds, max over
+    ranks; mean ms per step by events)."""
+    for s in range(W):
+        wl.npp(s)
+        wl.ana(s)
+    rig.sync()
+    rig.barrier()
+    rig.sync()
+    ev = [rig.event() for _ in range(K + 1)]
+    t0 = time.perf_counter()
+    wl.npp(W)
+    rig.record(ev[0])
+    for i in range(K):
+        wl.pipe(W + i, W + i + 1 if i + 1 < K else None)
+        rig.record(ev[i + 1])
+    rig.sync()
+    rig.barrier()
+    rig.sync()
+    dt = time.perf_counter() - t0
+    ems = float(np.mean([rig.elapsed_ms(ev[i], ev[i + 1]) for i in range(K)]))
+    return rig.max_over_ranks(dt), ems
+
+
 def host_leg(rig, C, first, K, W, dev_bits, world):
     """The host-fed form of the headline (melpe/melpe.c:91-99's contract:
     the caller hands host buffers): the same channels and synthetic input,
@@ -494,11 +535,35 @@ def round_trip_leg(rig, args, rank, world):
     synthetic channels), on rank 0."""
     C, K, W = args.rt_channels, args.steps, args.warmup
     wl = EngineWorkload(rig, C, rank * C, W + K)
-    dt, (npp_kms, ana_kms, dec_kms) = timed(rig, [wl.npp, wl.ana, wl.dec], K, W)
+    # serialised, each launch timed alone; then from fresh state the same
+    # work with the encode pipelined (pipe_leg), decode after each step
+    ser, (npp_kms, ana_kms, dec_kms) = timed(rig, [wl.npp, wl.ana, wl.dec], K, W)
+    ser_bits, ser_out = wl.bits.clone(), wl.out.clone()
+    wl.restart()
+    for s in range(W):
+        wl.npp(s)
+        wl.ana(s)
+        wl.dec(s)
+    rig.sync()
+    rig.barrier()
+    rig.sync()
+    t0 = time.perf_counter()
+    wl.npp(W)
+    for i in range(K):
+        wl.pipe(W + i, W + i + 1 if i + 1 < K else None)
+        wl.dec(W + i)
+    rig.sync()
+    rig.barrier()
+    rig.sync()
+    dt = rig.max_over_ranks(time.perf_counter() - t0)
+    same = bool((ser_bits == wl.bits).all()) and bool((ser_out == wl.out).all())
+    del ser_bits, ser_out
     res = {"workload": "config 3: %d channels per GPU, melpe_a + melpe_s (with postfilter) "
                        "per superframe on one engine" % C,
            "channels_per_gpu": C, "value": world * C * K * SF_SECONDS / dt,
            "unit": "channel-s/s (encoded and decoded)", "ms_per_step": 1e3 * dt / K,
+           "step": "encode pipelined (superframe k's analysis beside k+1's NPP), then decode of k",
+           "ms_per_step_serialised": 1e3 * ser / K, "bits_pcm_equal_serialised": same,
            "kernels_ms": {"k_enc_npp": npp_kms, "k_enc_ana": ana_kms, "k_decode": dec_kms}}
     oc = opcount()
     if oc:
@@ -606,14 +671,27 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
     wl = Workload(rig, C, rank * C, W + K)
     log("rank %d: %d channels x %d superframes of input resident" % (rank, C, W + K))
     # one step = melpe_a on every channel = k_enc_npp then k_enc_ana
-    enc_s, (npp_kms, ana_kms) = encode_leg(rig, wl, K, W)
+    # the serialised step: each launch alone, HIP events around each (the
+    # kernels' own durations, for the roofline)
+    ser_s, (npp_kms, ana_kms) = encode_leg(rig, wl, K, W)
     enc_kms = npp_kms + ana_kms
-    log("encode: %.1f ms/step (k_enc_npp %.1f ms + k_enc_ana %.1f ms)"
-        % (1e3 * enc_s / K, npp_kms, ana_kms))
+    log("encode, serialised: %.1f ms/step (k_enc_npp %.1f ms + k_enc_ana %.1f ms)"
+        % (1e3 * ser_s / K, npp_kms, ana_kms))
+    # the headline step: the same work pipelined, from fresh state on the
+    # same input; its bits must equal the serialised run's
+    ser_bits = wl.bits.clone()
+    wl.restart()
+    enc_s, pipe_ems = pipe_leg(rig, wl, K, W)
+    pipe_equal = bool((ser_bits == wl.bits).all())
+    del ser_bits
+    log("encode, pipelined: %.1f ms/step, bits equal to the serialised run: %s"
+        % (1e3 * enc_s / K, pipe_equal))
     hostfed = None
     if not args.no_host_leg and workload_cls is None:
         hostfed = host_leg(rig, C, rank * C, K, W, wl.bits, world)
-        hostfed["frac_of_device_resident"] = hostfed["value"] / (world * C * K * SF_SECONDS / enc_s)
+        # against the serialised device-resident step: the host-fed call is
+        # melpe_a's NPP + analysis of one superframe, not the pipelined pair
+        hostfed["frac_of_device_resident"] = hostfed["value"] / (world * C * K * SF_SECONDS / ser_s)
         log("host-fed encode: %.1f ms/step (%.0f%% of device-resident), bits equal: %s"
             % (hostfed["ms_per_step"], 100 * hostfed["frac_of_device_resident"],
                hostfed["bits_equal_device_resident"]))
@@ -647,13 +725,17 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
     if args.total_channels:
         lo, hi = channel_range(rank, world, args.total_channels)
         if hi - lo == C:
-            strong = {"ms_per_step": 1e3 * enc_s / K, "kernel_ms": enc_kms}
+            strong = {"ms_per_step": 1e3 * enc_s / K, "kernel_ms": enc_kms,
+                      "ms_per_step_serialised": 1e3 * ser_s / K}
         else:
             sw = Workload(rig, hi - lo, lo, W + K)
-            st_s, (snpp, sana) = encode_leg(rig, sw, K, W)
+            sser_s, (snpp, sana) = encode_leg(rig, sw, K, W)
+            sw.restart()
+            st_s, _ = pipe_leg(rig, sw, K, W)
             sw.close()
             strong = {"ms_per_step": 1e3 * st_s / K, "kernel_ms": snpp + sana,
-                      "k_enc_npp_ms": snpp, "k_enc_ana_ms": sana}
+                      "k_enc_npp_ms": snpp, "k_enc_ana_ms": sana,
+                      "ms_per_step_serialised": 1e3 * sser_s / K}
         strong.update({"total_channels": args.total_channels,
                        "channels_per_gpu_max": -(-args.total_channels // world),
                        "value": args.total_channels * K * SF_SECONDS / (strong["ms_per_step"] / 1e3 * K),
@@ -716,6 +798,11 @@ def run(args, rank, world, local, backend="nccl", rig_cls=None, workload_cls=Non
         "metric": "MELPe-1200 channel-seconds encoded/sec (node)",
         "value": value, "unit": "channel-s/s", "n_gpus": world, "steps": K, "warmup": W,
         "ms_per_step": 1e3 * enc_s / K, "higher_is_better": True, "scaling": "weak",
+        "step": {"form": "pipelined: superframe k's analysis beside superframe k+1's NPP "
+                         "(melpe_encode_pipe_dev); the timed region holds K NPPs and K analyses",
+                 "ms_per_step_events": pipe_ems,
+                 "ms_per_step_serialised": 1e3 * ser_s / K,
+                 "bits_equal_serialised": pipe_equal},
         "vs_baseline": None, "dtype": "int16/int32 saturating fixed point",
         "data": "synthetic (integer speech-like generator csrc/synth.h, run seed %d)" % RUN_SEED,
         "config": {"workload": "config 4: %d channels per GPU, melpe_a per superframe "

@@ -163,6 +163,19 @@ int melpe_encode_npp_dev(melpe_engine *e, void *d_sp, const void *d_active, void
 int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const void *d_active,
 			 void *hip_stream);
 
+/* Pipelined encode of a sequence of superframes: the analysis + packing of
+ * superframe k (d_sp: its PCM, already through the NPP, as
+ * melpe_encode_npp_dev leaves it; d_bits out) and, concurrently, the NPP of
+ * superframe k + 1 (d_sp_next, in place; NULL = none), on a second internal
+ * stream.  The two touch disjoint parts of every channel's state, so a
+ * sequence npp(0), pipe(0, 1), pipe(1, 2), ..., pipe(K-1, NULL) gives the
+ * bits and NPP output of K melpe_encode_dev calls; the next superframe's
+ * NPP runs in the SIMD slots the analysis leaves as its waves finish.
+ * d_sp_next must be another buffer than d_sp.  Ordered on hip_stream like
+ * the other *_dev calls (after its earlier work, before its later work). */
+int melpe_encode_pipe_dev(melpe_engine *e, void *d_bits, const void *d_sp, const void *d_active,
+			  void *d_sp_next, const void *d_active_next, void *hip_stream);
+
 /* melpe_s on every active channel: bits (C x 11, in), sp (C x 540, out) */
 int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
 		      const uint8_t *active);

@@ -60,6 +60,7 @@ def load_library(path=None):
         "melpe_encode_dev": (i32, [vp, vp, vp, vp, vp]),
         "melpe_encode_npp_dev": (i32, [vp, vp, vp, vp]),
         "melpe_encode_ana_dev": (i32, [vp, vp, vp, vp, vp]),
+        "melpe_encode_pipe_dev": (i32, [vp, vp, vp, vp, vp, vp, vp]),
         "melpe_decode_host": (i32, [vp, vp, vp, vp]),
         "melpe_decode_dev": (i32, [vp, vp, vp, vp, vp]),
         "melpe_npp_host": (i32, [vp, vp, i32, i32, vp]),
@@ -355,6 +356,12 @@ class MelpeEngine:
 
     def encode_npp_dev(self, d_sp, d_active=None, stream=None):
         _check(self.lib.melpe_encode_npp_dev(self.h, d_sp, d_active, stream))
+
+    def encode_pipe_dev(self, d_bits, d_sp, d_sp_next, d_active=None, d_active_next=None, stream=None):
+        """analysis of superframe k (d_sp already through the NPP) beside
+        the NPP of superframe k + 1 (d_sp_next, or None)"""
+        _check(self.lib.melpe_encode_pipe_dev(self.h, d_bits, d_sp, d_active, d_sp_next, d_active_next,
+                                              stream))
 
     def encode_ana_dev(self, d_bits, d_sp, d_active=None, stream=None):
         _check(self.lib.melpe_encode_ana_dev(self.h, d_bits, d_sp, d_active, stream))

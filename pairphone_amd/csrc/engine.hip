@@ -724,6 +724,7 @@ struct melpe_engine {
 	hipEvent_t ev0 = nullptr, ev1 = nullptr;
 	hipEvent_t ev_in = nullptr, ev_out = nullptr;	/* EngineCall's hops to and from the engine stream */
 	hipEvent_t ev_host = nullptr;	/* host_finish: the end of a host call's own work */
+	hipEvent_t ev_pin = nullptr, ev_npp = nullptr;	/* melpe_encode_pipe_dev's hops to / from the NPP stream */
 	EncState *d_enc = nullptr;
 	DecState *d_dec = nullptr;
 	synth_state *d_syn = nullptr;
@@ -808,8 +809,12 @@ static bool harm_split(void)
 	return v != 0;
 }
 
+/* after_sort: recorded on s between the lane-order sort and the analysis
+ * kernels (melpe_encode_pipe_dev starts the next superframe's NPP there, so
+ * that the analysis' waves are dispatched first and the NPP's fill the
+ * slots they free) */
 static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, const uint8_t *d_act,
-		      hipStream_t s)
+		      hipStream_t s, hipEvent_t after_sort = nullptr)
 {
 	BinBuf &b = e->bin_enc;
 	bool on;
@@ -818,6 +823,8 @@ static int ana_launch(melpe_engine *e, const int16_t *d_sp, uint8_t *d_bits, con
 				   (int) (offsetof(EncState, a) + offsetof(EncAna, qpar) + offsetof(QuantParam, uv_flag)),
 				   d_act, e->channels, s, &on);
 	if (er != hipSuccess)
+		return (int) er;
+	if (after_sort && (er = hipEventRecord(after_sort, s)) != hipSuccess)
 		return (int) er;
 	const int *perm = on ? b.perm : nullptr;
 	const int *nlive = on ? (const int *) (b.ctl + 2 * NBIN) : nullptr;
@@ -930,6 +937,7 @@ static int ensure_device_tables(int dev)
 			return fail("table upload", (hipError_t) rc);
 	if (hipError_t er = hipStreamCreateWithFlags(&g_dev_stream[dev], hipStreamNonBlocking))
 		return fail("engine stream", er);
+
 	g_dev_ready[dev] = true;
 	return 0;
 }
@@ -1083,6 +1091,7 @@ static int engine_warm(melpe_engine *e)
 			return fail("melpe_engine: codec kernel scratch could not be reserved", er);
 	if (e->d_hb && (er = (hipError_t) kl_dec2_warm(e->channels, e->stream)) != hipSuccess)
 		return fail("melpe_engine: codec kernel scratch could not be reserved", er);
+
 	if ((er = hipStreamSynchronize(e->stream)) != hipSuccess)
 		return fail("melpe_engine: codec kernel scratch could not be reserved", er);
 	return 0;
@@ -1174,6 +1183,8 @@ int melpe_engine_create(melpe_engine **out, int device, int channels)
 	CREATE_STEP(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
 	CREATE_STEP(hipEventCreateWithFlags(&e->ev_out, hipEventDisableTiming));
 	CREATE_STEP(hipEventCreateWithFlags(&e->ev_host, hipEventDisableTiming));
+	CREATE_STEP(hipEventCreateWithFlags(&e->ev_pin, hipEventDisableTiming));
+	CREATE_STEP(hipEventCreateWithFlags(&e->ev_npp, hipEventDisableTiming));
 	CREATE_STEP(hipMalloc(&e->d_enc, sizeof(EncState) * (size_t) channels));
 	CREATE_STEP(hipMalloc(&e->d_dec, sizeof(DecState) * (size_t) channels));
 	CREATE_STEP(hipMalloc(&e->d_syn, sizeof(synth_state) * (size_t) channels));
@@ -1310,6 +1321,10 @@ int melpe_engine_destroy(melpe_engine *e)
 		hipEventDestroy(e->ev_out);
 	if (e->ev_host)
 		hipEventDestroy(e->ev_host);
+	if (e->ev_pin)
+		hipEventDestroy(e->ev_pin);
+	if (e->ev_npp)
+		hipEventDestroy(e->ev_npp);
 	for (auto &sl : e->slot) {
 		hipFree(sl.pcm);
 		hipFree(sl.bits);
@@ -1480,6 +1495,43 @@ int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const 
 	return _call.finish();
 }
 
+static int side_streams(melpe_engine *e);
+
+int melpe_encode_pipe_dev(melpe_engine *e, void *d_bits, const void *d_sp, const void *d_active,
+			  void *d_sp_next, const void *d_active_next, void *hip_stream)
+{
+	if (!e || !d_bits || !d_sp)
+		return fail_msg("melpe_encode_pipe_dev: null argument");
+	if (d_sp_next == d_sp)
+		return fail_msg("melpe_encode_pipe_dev: the next superframe's PCM must be another buffer");
+	DEVGUARD(e->device);
+	if (d_sp_next)
+		if (int rc = side_streams(e))
+			return rc;
+	hipStream_t s = (hipStream_t) hip_stream;
+	ENGINE_CALL(e, s);
+	/* the analysis on the engine stream; the next superframe's NPP on the
+	 * engine's cin stream once the analysis' lane-order sort is done (after the
+	 * caller's work, too, which the engine stream waited for).  The NPP
+	 * touches only the records' NppState and d_sp_next, the analysis only
+	 * their EncAna and d_sp. */
+	ev_begin(e, s);
+	HIPCHK((hipError_t) ana_launch(e, (const int16_t *) d_sp, (uint8_t *) d_bits, (const uint8_t *) d_active,
+				       s, d_sp_next ? e->ev_pin : nullptr));
+	ev_end(e, s, false);
+	if (d_sp_next) {
+		const hipStream_t ns = e->cin;
+		HIPCHK(hipStreamWaitEvent(ns, e->ev_pin, 0));
+		HIPCHK((hipError_t) kl_enc_npp(e->d_enc, (int16_t *) d_sp_next, (const uint8_t *) d_active_next,
+					       e->channels, ns));
+		HIPCHK(hipEventRecord(e->ev_npp, ns));
+	}
+	/* the hop back to the caller covers the NPP too */
+	if (d_sp_next)
+		HIPCHK(hipStreamWaitEvent(s, e->ev_npp, 0));
+	return _call.finish();
+}
+
 int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const uint8_t *active)
 {
 	if (!e || !bits || !sp)
@@ -1505,10 +1557,27 @@ int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const u
 	return 0;
 }
 
-/* the host-fed pipeline's buffers and streams, made at its first call */
-static int async_setup(melpe_engine *e)
+/* The engine's two side streams, made at the first call that needs them
+ * (the host-fed pipeline's copies; the pipelined encode's NPP runs on cin).
+ * The runtime spreads streams over the process's hardware queues in the
+ * order they are made, so they are made in one place, cout then cin.  The
+ * NPP kernel's scratch is reserved on cin's queue here (only that kernel
+ * runs there besides copies). */
+static int side_streams(melpe_engine *e)
 {
 	if (e->cin)
+		return 0;
+	HIPCHK(hipStreamCreateWithFlags(&e->cout, hipStreamNonBlocking));
+	HIPCHK(hipStreamCreateWithFlags(&e->cin, hipStreamNonBlocking));
+	HIPCHK((hipError_t) kl_npp_warm(e->channels, e->cin));
+	HIPCHK(hipStreamSynchronize(e->cin));
+	return 0;
+}
+
+/* the host-fed pipeline's buffers, made at its first call */
+static int async_setup(melpe_engine *e)
+{
+	if (e->slot[0].pcm)
 		return 0;
 	const size_t pb = sizeof(int16_t) * BLOCK * (size_t) e->channels, bb = (size_t) 11 * e->channels;
 	for (auto &sl : e->slot) {
@@ -1518,9 +1587,7 @@ static int async_setup(melpe_engine *e)
 		for (hipEvent_t *ev : {&sl.loaded, &sl.done, &sl.freed})
 			HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
 	}
-	HIPCHK(hipStreamCreateWithFlags(&e->cout, hipStreamNonBlocking));
-	HIPCHK(hipStreamCreateWithFlags(&e->cin, hipStreamNonBlocking));
-	return 0;
+	return side_streams(e);
 }
 
 int melpe_encode_host_async(melpe_engine *e, unsigned char *bits, int16_t *sp, const uint8_t *active)

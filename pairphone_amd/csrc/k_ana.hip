@@ -21,6 +21,27 @@ struct AnaLane {
  * MODE 1: the split form (encoder.h analysis_a): the windowed residuals to
  *         res (NF x LPC_FRAME per channel), the Fourier magnitudes and the
  *         packing in k_harm.hip. */
+#if defined(MELPE_WAVE_TIMES)
+/* diagnostics (tools/wave_times.py): each wave's start and end on the
+ * chip-wide 100 MHz counter, to see how the launch's waves finish */
+__device__ unsigned long long g_wave_t[2 * 16384];
+extern "C" int kl_wave_times(unsigned long long *out, int n)
+{
+	return (int) hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), sizeof(unsigned long long) * n);
+}
+#define WT_START() const unsigned long long wt0_ = __builtin_amdgcn_s_memrealtime()
+#define WT_END()                                                                         \
+	do {                                                                             \
+		if (threadIdx.x == 0 && blockIdx.x < 16384) {                            \
+			g_wave_t[2 * blockIdx.x] = wt0_;                                 \
+			g_wave_t[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime(); \
+		}                                                                        \
+	} while (0)
+#else
+#define WT_START() (void) 0
+#define WT_END() (void) 0
+#endif
+
 template <int MODE>
 __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits,
 						  const uint8_t *active, int n, const int *perm,
@@ -30,6 +51,7 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 	 * by pitch class (engine.hip, MELPE_BIN), else channel g under the mask;
 	 * the whole launch stands down unless the live count is the gate's
 	 * (engine.hip ana_launch enqueues this and the four-wave kernel) */
+	WT_START();
 	int c = blockIdx.x * WAVE + threadIdx.x;
 	if (perm) {
 		const int L = *nlive;
@@ -58,6 +80,7 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 	if (MODE == 0)
 		for (int k = 0; k < 11; k++)
 			bits[(size_t) c * 11 + k] = L.S.chbuf[k];
+	WT_END();
 }
 
 /* debug aid: analysis cut after `upto` stages (0 = nothing) */

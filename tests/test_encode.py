@@ -136,6 +136,40 @@ def test_encode_gpu_lane_kernel_alone_1024_channels_match_golden():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("waves", [0, 1])
+def test_encode_pipe_dev_matches_golden(waves):
+    """The pipelined encode (melpe_encode_pipe_dev: superframe k's analysis
+    beside superframe k+1's NPP on the engine's second stream) over the
+    1,024-channel goldens x 149 superframes: the bits and the NPP output
+    melpe_a leaves in the buffer, channel by channel -- with the automatic
+    mapping (the four-wave analysis at this size) and the lane kernel."""
+    import torch
+    from pairphone_amd import MelpeEngine
+    g = golden()
+    C, nsf = g["channels"], g["superframes"]
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    x = torch.from_numpy(np.ascontiguousarray(
+        signals(g["seed"], C, nsf).reshape(C, nsf, 540).transpose(1, 0, 2))).to(dev)
+    bits = torch.zeros((nsf, C, 11), dtype=torch.uint8, device=dev)
+    eng = MelpeEngine(C)
+    if waves:
+        eng.set_ana_waves(waves)
+    eng.encode_npp_dev(x[0].data_ptr(), None, s)
+    for k in range(nsf):
+        eng.encode_pipe_dev(bits[k].data_ptr(), x[k].data_ptr(),
+                            x[k + 1].data_ptr() if k + 1 < nsf else None, stream=s)
+    torch.cuda.synchronize(dev)
+    eng.close()
+    b = bits.cpu().numpy().transpose(1, 0, 2).reshape(C, nsf * 11)
+    n = x.cpu().numpy().transpose(1, 0, 2).reshape(C, nsf * 540)
+    bad = [c for c in range(C) if sha(b[c]) != g["bits_sha256"][c]]
+    badn = [c for c in range(C) if sha(n[c]) != g["npp_sha256"][c]]
+    assert not bad, "bitstream mismatch on %d channels, first %s" % (len(bad), bad[:8])
+    assert not badn, "NPP output mismatch on %d channels, first %s" % (len(badn), badn[:8])
+
+
+@pytest.mark.gpu
 def test_encode_host_two_threads_one_engine():
     """Two host threads calling melpe_encode_host on one engine at once,
     each on its own half of the channels (disjoint masks): every call holds

@@ -132,6 +132,14 @@ class FakeWorkload:
         g = torch.arange(self.first, self.first + self.C, dtype=torch.int64)
         self.bits[s] = ((g[:, None] * 31 + s * 7 + torch.arange(11)) % 251).to(torch.uint8)
 
+    def pipe(self, s, nxt):
+        self.ana(s)
+        if nxt is not None:
+            self.npp(nxt)
+
+    def restart(self):
+        self.bits.zero_()
+
     def dec(self, s):
         pass
 

@@ -1,69 +1,70 @@
-"""Superframe pipeline experiment (diagnostics): NPP of superframe s+1 on a
-second stream beside the analysis of superframe s, against the sequential
-NPP -> analysis step, on the product library (or MELPE_AMD_LIB).
+#!/usr/bin/env python3
+"""Diagnostics: the encode step serialised (melpe_encode_npp_dev then
+melpe_encode_ana_dev, the bench's encode leg) against the pipelined form
+(melpe_encode_pipe_dev: superframe k's analysis beside superframe k+1's NPP
+on the engine's second stream), same channels and input, wall-clock per
+step; and whether the bits agree.
 
-    python tools/pipe_exp.py [channels] [steps]
-
-Prints one JSON line: sequential and pipelined ms per superframe step, and
-whether the pipelined bitstreams equal the sequential ones.
+  python tools/pipe_exp.py [channels] [steps] [warmup]
 """
 import json
 import os
 import sys
 import time
 
-import torch
-
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from pairphone_amd import MelpeEngine  # noqa: E402
-
-SF, NB = 540, 11
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
-def main():
-    C = int(sys.argv[1]) if len(sys.argv) > 1 else 262144
-    K = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+def main(C=262144, K=10, W=2):
+    import torch
+    import bench
+    from pairphone_amd import MelpeEngine
     dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
-    s1 = torch.cuda.current_stream(dev)
-    s2 = torch.cuda.Stream(dev)
-    out = {"channels": C, "steps": K}
+    s = torch.cuda.current_stream(dev).cuda_stream
+    res = {}
     bits = {}
-    for mode in ("seq", "pipe"):
-        eng = MelpeEngine(C, device=0)
-        pcm = torch.empty((K + 1, C, SF), dtype=torch.int16, device=dev)
-        b = torch.zeros((K + 1, C, NB), dtype=torch.uint8, device=dev)
-        eng.synth_seed(2026, first_channel=0)
-        for s in range(K + 1):
-            eng.synth_dev(pcm[s].data_ptr(), SF, s1.cuda_stream)
-        # superframe 0 outside the timed region
-        eng.encode_npp_dev(pcm[0].data_ptr(), None, s1.cuda_stream)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        if mode == "seq":
-            for s in range(K):
-                eng.encode_ana_dev(b[s].data_ptr(), pcm[s].data_ptr(), None, s1.cuda_stream)
-                eng.encode_npp_dev(pcm[s + 1].data_ptr(), None, s1.cuda_stream)
+    for mode in ("serial", "pipe", "serial2", "pipe2"):
+        eng = MelpeEngine(C)
+        n = W + K
+        pcm = torch.empty((n, C, 540), dtype=torch.int16, device=dev)
+        b = torch.zeros((n, C, 11), dtype=torch.uint8, device=dev)
+        eng.synth_seed(bench.RUN_SEED)
+        for k in range(n):
+            eng.synth_dev(pcm[k].data_ptr(), 540, s)
+        torch.cuda.synchronize(dev)
+
+        def serial(k):
+            eng.encode_npp_dev(pcm[k].data_ptr(), None, s)
+            eng.encode_ana_dev(b[k].data_ptr(), pcm[k].data_ptr(), None, s)
+        if mode.startswith("serial"):
+            for k in range(W):
+                serial(k)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for k in range(W, n):
+                serial(k)
+            torch.cuda.synchronize(dev)
         else:
-            ev = [torch.cuda.Event() for _ in range(K + 1)]
-            ev[0].record(s1)
-            s2.wait_event(ev[0])
-            for s in range(K):
-                eng.encode_npp_dev(pcm[s + 1].data_ptr(), None, s2.cuda_stream)
-                ev[s + 1].record(s2)
-                eng.encode_ana_dev(b[s].data_ptr(), pcm[s].data_ptr(), None, s1.cuda_stream)
-                s1.wait_event(ev[s + 1])
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        out[mode + "_ms_per_step"] = 1e3 * dt / K
-        bits[mode] = b[:K].cpu()
+            for k in range(W):
+                serial(k)
+            torch.cuda.synchronize(dev)
+            # the timed region holds the same K NPPs and K analyses
+            t0 = time.perf_counter()
+            eng.encode_npp_dev(pcm[W].data_ptr(), None, s)
+            for k in range(W, n):
+                nxt = pcm[k + 1].data_ptr() if k + 1 < n else None
+                eng.encode_pipe_dev(b[k].data_ptr(), pcm[k].data_ptr(), nxt, stream=s)
+            torch.cuda.synchronize(dev)
+        res[mode] = 1e3 * (time.perf_counter() - t0) / K
+        bits[mode] = b.cpu()
         eng.close()
         del pcm, b
-        torch.cuda.empty_cache()
-    out["bit_exact"] = bool(torch.equal(bits["seq"], bits["pipe"]))
-    out["lib"] = os.environ.get("MELPE_AMD_LIB", "product")
-    print(json.dumps(out), flush=True)
+    res["bits_equal"] = bool(torch.equal(bits["serial"], bits["pipe"]))
+    res["channels"] = C
+    print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":
-    main()
+    a = sys.argv[1:]
+    main(*(int(x) for x in a))
