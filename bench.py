@@ -394,19 +394,31 @@ def encode_leg(rig, wl, K, W):
     return timed(rig, [wl.npp, wl.ana], K, W)
 
 
+def pipe_warmup(wl, W, dec=False):
+    """W warm-up steps in the pipelined form (the engine makes and warms its
+    side stream at the first pipelined call, outside the timed region):
+    npp(0), pipe(0, 1), ..., pipe(W-1, none) -- superframe W is left for
+    the timed region's first NPP"""
+    if W <= 0:
+        return
+    wl.npp(0)
+    for s in range(W):
+        wl.pipe(s, s + 1 if s + 1 < W else None)
+        if dec:
+            wl.dec(s)
+
+
 def pipe_leg(rig, wl, K, W):
     """The headline step pipelined (melpe_encode_pipe_dev): superframe k's
     analysis on the engine stream beside superframe k + 1's NPP on the
     engine's second stream, whose waves take the SIMD slots the analysis'
     waves free as they finish (the launch's tail: profiles/
-    r06_i_wave_times.jsonl).  W warm-up steps serialised, then a timed
+    r06_i_wave_times.jsonl).  W warm-up steps pipelined, then a timed
     region holding exactly K NPPs and K analyses: the NPP of superframe W,
     then K pipelined steps, the last without a next NPP.  HIP events on the
     caller's stream bracket each step.  Returns (wall seconds, max over
     ranks; mean ms per step by events)."""
-    for s in range(W):
-        wl.npp(s)
-        wl.ana(s)
+    pipe_warmup(wl, W)
     rig.sync()
     rig.barrier()
     rig.sync()
@@ -540,10 +552,7 @@ def round_trip_leg(rig, args, rank, world):
     ser, (npp_kms, ana_kms, dec_kms) = timed(rig, [wl.npp, wl.ana, wl.dec], K, W)
     ser_bits, ser_out = wl.bits.clone(), wl.out.clone()
     wl.restart()
-    for s in range(W):
-        wl.npp(s)
-        wl.ana(s)
-        wl.dec(s)
+    pipe_warmup(wl, W, dec=True)
     rig.sync()
     rig.barrier()
     rig.sync()
