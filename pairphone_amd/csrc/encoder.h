@@ -452,6 +452,12 @@ MN void sc_ana(EncAna *E, MelpParam *par)
 	(void) t2;
 }
 
+/* a progress checkpoint of the lane analysis kernel (k_ana.hip may set the
+ * wave's issue priority there); a no-op everywhere else */
+#ifndef ANA_CKPT
+#define ANA_CKPT(j) ((void) 0)
+#endif
+
 /* analysis :119 -- 540 NPP-processed samples -> quantised params + chbuf */
 /* analysis() in the two parts the GPU runs as separate kernels:
  * analysis_frame: dc removal and melp_ana of frame i (melp_ana.c:140-160);
@@ -541,6 +547,7 @@ MN void analysis_a2(EncAna *E, int16_t *res)
 #if !defined(MELPE_KO_LSFVQ)
 	lsf_vq(E, par);
 #endif
+	ANA_CKPT(4);
 	pitch_vq(E, par);
 	gain_vq(E, par);
 	for (int i = 0; i < NF; i++)
@@ -567,8 +574,10 @@ MN void analysis_a(EncAna *E, const int16_t *sp_in, int16_t *res)
 #if defined(MELPE_KO_ANALYSIS)
 	return;
 #endif
-	for (int i = 0; i < NF; i++)
+	for (int i = 0; i < NF; i++) {
 		analysis_frame(E, sp_in, i);
+		ANA_CKPT(i + 1);
+	}
 	analysis_a2(E, res);
 }
 

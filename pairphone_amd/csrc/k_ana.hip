@@ -5,6 +5,39 @@
  * NPP output k_enc_npp left in the caller's PCM.
  */
 #include <stdlib.h>
+#include <hip/hip_runtime.h>
+
+/* progress-driven issue priority (MELPE_ANA_PRIO 6, experiment): every wave
+ * counts its checkpoints (encoder.h ANA_CKPT: after each frame and after
+ * lsf_vq) on one counter, and a wave behind the average takes a higher
+ * priority, one ahead a lower */
+struct AnaProg {
+	unsigned cnt;
+	int mode;
+};
+__device__ AnaProg g_ana_prog;
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void ana_ckpt(int j)
+{
+	if (g_ana_prog.mode != 6)
+		return;
+	unsigned before = 0;
+	if (__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x)
+		before = atomicAdd(&g_ana_prog.cnt, 1u);
+	before = __builtin_amdgcn_readfirstlane(before);
+	const int avg4 = (int) ((4ull * before) / gridDim.x);	/* checkpoints passed per wave, x4 */
+	const int d = 4 * (j - 1) - avg4;			/* > 0: ahead of the average */
+	if (d < -2)
+		__builtin_amdgcn_s_setprio(3);
+	else if (d < 0)
+		__builtin_amdgcn_s_setprio(2);
+	else if (d < 2)
+		__builtin_amdgcn_s_setprio(1);
+	else
+		__builtin_amdgcn_s_setprio(0);
+}
+#define ANA_CKPT(j) ana_ckpt(j)
+#endif
 #include "kern.h"
 
 MELPE_TU(ana)
@@ -25,9 +58,15 @@ struct AnaLane {
 /* diagnostics (tools/wave_times.py): each wave's start and end on the
  * chip-wide 100 MHz counter, to see how the launch's waves finish */
 __device__ unsigned long long g_wave_t[2 * 16384];
+/* the wave's placement: HW_ID (wave, SIMD, CU, SH, SE) and XCC_ID */
+__device__ unsigned g_wave_hw[2 * 16384];
 extern "C" int kl_wave_times(unsigned long long *out, int n)
 {
 	return (int) hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), sizeof(unsigned long long) * n);
+}
+extern "C" int kl_wave_hw(unsigned *out, int n)
+{
+	return (int) hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_hw), sizeof(unsigned) * n);
 }
 #define WT_START() const unsigned long long wt0_ = __builtin_amdgcn_s_memrealtime()
 #define WT_END()                                                                         \
@@ -35,6 +74,8 @@ extern "C" int kl_wave_times(unsigned long long *out, int n)
 		if (threadIdx.x == 0 && blockIdx.x < 16384) {                            \
 			g_wave_t[2 * blockIdx.x] = wt0_;                                 \
 			g_wave_t[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime(); \
+			g_wave_hw[2 * blockIdx.x] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  \
+			g_wave_hw[2 * blockIdx.x + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20); \
 		}                                                                        \
 	} while (0)
 #else
@@ -42,10 +83,52 @@ extern "C" int kl_wave_times(unsigned long long *out, int n)
 #define WT_END() (void) 0
 #endif
 
+/* The wave's issue priority from its place in the lane order.  The order
+ * runs from the lightest classes to the heaviest (voiced, long pitch), and
+ * with every wave resident from the first cycle the launch lasts as long as
+ * its heaviest waves: measured per wave at 262,144 channels
+ * (profiles/r06_m_wave_place.txt), the first 1/32 of the order takes 19.4 ms,
+ * the last 24.6 ms, and each SIMD holds four waves from across the order.
+ * Mode 1: quartile q of the order runs at priority q; mode 2: the lower half
+ * at 1, the upper at 3 (priority 0 is then left to the next superframe's NPP
+ * waves in the pipelined step). */
+__device__ __forceinline__ void ana_wave_prio(int mode, int w, int nw)
+{
+	if (mode <= 0)
+		return;
+	const int q = (4 * w) / nw;	/* 0..3, wave-uniform */
+	if (mode == 3) {
+		if (q >= 2)
+			__builtin_amdgcn_s_setprio(1);
+	} else if (mode == 4) {
+		if (q == 3)
+			__builtin_amdgcn_s_setprio(1);
+	} else if (mode == 5) {
+		if (q == 1 || q == 2)
+			__builtin_amdgcn_s_setprio(1);
+		else if (q == 3)
+			__builtin_amdgcn_s_setprio(2);
+	} else if (mode == 6) {
+		__builtin_amdgcn_s_setprio(1);
+	} else if (mode == 1) {
+		if (q == 1)
+			__builtin_amdgcn_s_setprio(1);
+		else if (q == 2)
+			__builtin_amdgcn_s_setprio(2);
+		else if (q >= 3)
+			__builtin_amdgcn_s_setprio(3);
+	} else {
+		if (q >= 2)
+			__builtin_amdgcn_s_setprio(3);
+		else
+			__builtin_amdgcn_s_setprio(1);
+	}
+}
+
 template <int MODE>
 __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits,
 						  const uint8_t *active, int n, const int *perm,
-						  const int *nlive, int16_t *res, AnaGate gate)
+						  const int *nlive, int16_t *res, AnaGate gate, int prio)
 {
 	/* lane g runs channel perm[g] when the engine ordered the live channels
 	 * by pitch class (engine.hip, MELPE_BIN), else channel g under the mask;
@@ -60,6 +143,7 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 		gate.mark(c == 0 && L > 0, 1);	/* no live channel: the tag stays 0 */
 		if (c >= L)
 			return;
+		ana_wave_prio(prio, blockIdx.x, (L + WAVE - 1) / WAVE);
 		c = perm[c];
 	} else {
 		gate.mark(c == 0, 1);
@@ -109,15 +193,34 @@ static unsigned ana_lds_bytes(void)
 	return (unsigned) v;
 }
 
+/* MELPE_ANA_PRIO: the waves' issue priority by lane order (ana_wave_prio) */
+static int ana_prio_mode(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("MELPE_ANA_PRIO");
+		v = e ? atoi(e) : 0;
+	}
+	return v;
+}
+
 extern "C" int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const uint8_t *active,
 			  int n, const int *perm, const int *nlive, int16_t *res, AnaGate gate, hipStream_t s)
 {
+	const int pm = ana_prio_mode();
+	if (pm == 6) {	/* the progress counter restarts with each launch */
+		static const AnaProg z = {0u, 6};
+		hipError_t er = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ana_prog), &z, sizeof(z), 0,
+						       hipMemcpyHostToDevice, s);
+		if (er != hipSuccess)
+			return (int) er;
+	}
 	if (res)
 		k_enc_ana<1><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res,
-									 gate);
+									 gate, pm);
 	else
 		k_enc_ana<0><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res,
-									 gate);
+									 gate, pm);
 	return (int) hipGetLastError();
 }
 
@@ -142,6 +245,6 @@ extern "C" size_t kl_ana_private(void)
 extern "C" int kl_ana_warm(int n, hipStream_t s)
 {
 	k_enc_ana<1><<<grid_for(n), WAVE, 0, s>>>(nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
-						 AnaGate{});
+						 AnaGate{}, 0);
 	return (int) hipGetLastError();
 }

@@ -103,8 +103,15 @@ struct ProfScope {
 	__device__ ~ProfScope()
 	{
 		unsigned long long dt = __builtin_amdgcn_s_memtime() - t0;
+#if defined(MELPE_PROF_QUART)
+		/* per quarter of the grid (the lane order: light -> heavy classes) */
+		const int q = k < 64 ? (int) ((4 * blockIdx.x) / gridDim.x) : 0;
+		if (__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x)
+			atomicAdd(&g_prof[k + 64 * q], dt);
+#else
 		if (__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x)
 			atomicAdd(&g_prof[k], dt);
+#endif
 	}
 };
 #define PROF_SCOPE(k) ProfScope PROF_CAT(prof_scope_, __LINE__)(k)

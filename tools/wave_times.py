@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main(C=262144, nsf=6):
+def main(C=262144, nsf=6, dump=None):
     import torch
     import bench
     from pairphone_amd import MelpeEngine, load_library
@@ -55,9 +55,14 @@ def main(C=262144, nsf=6):
                     "end_ms_pct": {p: float(np.percentile(ends, p)) for p in (10, 25, 50, 75, 90, 99, 100)},
                     "wave_ms_mean": float(dur.mean()), "slot_utilisation": util})
         print(json.dumps(out[-1]), flush=True)
+        if dump and k == nsf - 1:
+            hw = np.zeros(2 * W, np.uint32)
+            lib.kl_wave_hw.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            lib.kl_wave_hw(hw.ctypes.data, 2 * W)
+            np.savez(dump, start=starts, end=ends, hwid=hw[0::2], xcc=hw[1::2])
     eng.close()
 
 
 if __name__ == "__main__":
     a = sys.argv[1:]
-    main(int(a[0]) if a else 262144, int(a[1]) if len(a) > 1 else 6)
+    main(int(a[0]) if a else 262144, int(a[1]) if len(a) > 1 else 6, a[2] if len(a) > 2 else None)
