@@ -1814,6 +1814,11 @@ MD void dec2_phase(DecState *D, int16_t *out, Hb hb0, Hb hb1, int role, int p)
 #endif
 
 /* synthesis :110 -- melpe_s: D->chbuf (11 bytes) -> 540 samples */
+/* a progress checkpoint of the lane decoder (progprio.h); a no-op elsewhere */
+#ifndef DEC_CKPT
+#define DEC_CKPT(j) ((void) 0)
+#endif
+
 MN void decode_superframe(DecState *D, int16_t *out)
 {
 	PROF_SCOPE(22);
@@ -1826,6 +1831,7 @@ MN void decode_superframe(DecState *D, int16_t *out)
 		melp_syn<false>(D, &D->par[i], &out[i * FRAME]);
 		if (D->syn_begin > 0 && i < NF - 1)
 			v_copy(&out[(i + 1) * FRAME], D->sigsave, D->syn_begin);
+		DEC_CKPT(i + 1);
 	}
 }
 

@@ -452,8 +452,8 @@ MN void sc_ana(EncAna *E, MelpParam *par)
 	(void) t2;
 }
 
-/* a progress checkpoint of the lane analysis kernel (k_ana.hip may set the
- * wave's issue priority there); a no-op everywhere else */
+/* a progress checkpoint of the lane analysis kernel (progprio.h); a no-op
+ * everywhere else */
 #ifndef ANA_CKPT
 #define ANA_CKPT(j) ((void) 0)
 #endif

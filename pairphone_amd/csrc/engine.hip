@@ -534,7 +534,8 @@ struct BinBuf {
 	uint16_t *key = nullptr;	/* [C] class of each channel (NOT_LIVE: not live) */
 	/* [0, NBIN) counts, [NBIN, 2 NBIN) next slot of each class, [2 NBIN]
 	 * the live count, [2 NBIN + 1] the mapping the last analysis launch ran
-	 * (AnaGate tag: 1 lane, 4 four-wave; 0 none yet) */
+	 * (AnaGate tag: 1 lane, 4 four-wave; 0 none yet), [2 NBIN + 2] the
+	 * launch's progress counter (k_ana.hip ana_ckpt) */
 	unsigned *ctl = nullptr;
 	/* The buffers are one per engine and direction, but *_dev calls may
 	 * come on different streams: the sort of a call waits for the kernel
@@ -632,6 +633,7 @@ __global__ void k_bin_scan(BinBuf b)
 		}
 		b.ctl[2 * NBIN] = acc;
 		b.ctl[2 * NBIN + 1] = 0;	/* the mapping tag: the launch that runs sets it */
+		b.ctl[2 * NBIN + 2] = 0;	/* the lane kernels' progress counter (k_ana.hip ana_ckpt) */
 	}
 }
 

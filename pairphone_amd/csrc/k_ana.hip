@@ -5,39 +5,7 @@
  * NPP output k_enc_npp left in the caller's PCM.
  */
 #include <stdlib.h>
-#include <hip/hip_runtime.h>
-
-/* progress-driven issue priority (MELPE_ANA_PRIO 6, experiment): every wave
- * counts its checkpoints (encoder.h ANA_CKPT: after each frame and after
- * lsf_vq) on one counter, and a wave behind the average takes a higher
- * priority, one ahead a lower */
-struct AnaProg {
-	unsigned cnt;
-	int mode;
-};
-__device__ AnaProg g_ana_prog;
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ void ana_ckpt(int j)
-{
-	if (g_ana_prog.mode != 6)
-		return;
-	unsigned before = 0;
-	if (__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x)
-		before = atomicAdd(&g_ana_prog.cnt, 1u);
-	before = __builtin_amdgcn_readfirstlane(before);
-	const int avg4 = (int) ((4ull * before) / gridDim.x);	/* checkpoints passed per wave, x4 */
-	const int d = 4 * (j - 1) - avg4;			/* > 0: ahead of the average */
-	if (d < -2)
-		__builtin_amdgcn_s_setprio(3);
-	else if (d < 0)
-		__builtin_amdgcn_s_setprio(2);
-	else if (d < 2)
-		__builtin_amdgcn_s_setprio(1);
-	else
-		__builtin_amdgcn_s_setprio(0);
-}
-#define ANA_CKPT(j) ana_ckpt(j)
-#endif
+#define MELPE_PROG_PRIO	/* progprio.h: ANA_CKPT */
 #include "kern.h"
 
 MELPE_TU(ana)
@@ -83,48 +51,6 @@ extern "C" int kl_wave_hw(unsigned *out, int n)
 #define WT_END() (void) 0
 #endif
 
-/* The wave's issue priority from its place in the lane order.  The order
- * runs from the lightest classes to the heaviest (voiced, long pitch), and
- * with every wave resident from the first cycle the launch lasts as long as
- * its heaviest waves: measured per wave at 262,144 channels
- * (profiles/r06_m_wave_place.txt), the first 1/32 of the order takes 19.4 ms,
- * the last 24.6 ms, and each SIMD holds four waves from across the order.
- * Mode 1: quartile q of the order runs at priority q; mode 2: the lower half
- * at 1, the upper at 3 (priority 0 is then left to the next superframe's NPP
- * waves in the pipelined step). */
-__device__ __forceinline__ void ana_wave_prio(int mode, int w, int nw)
-{
-	if (mode <= 0)
-		return;
-	const int q = (4 * w) / nw;	/* 0..3, wave-uniform */
-	if (mode == 3) {
-		if (q >= 2)
-			__builtin_amdgcn_s_setprio(1);
-	} else if (mode == 4) {
-		if (q == 3)
-			__builtin_amdgcn_s_setprio(1);
-	} else if (mode == 5) {
-		if (q == 1 || q == 2)
-			__builtin_amdgcn_s_setprio(1);
-		else if (q == 3)
-			__builtin_amdgcn_s_setprio(2);
-	} else if (mode == 6) {
-		__builtin_amdgcn_s_setprio(1);
-	} else if (mode == 1) {
-		if (q == 1)
-			__builtin_amdgcn_s_setprio(1);
-		else if (q == 2)
-			__builtin_amdgcn_s_setprio(2);
-		else if (q >= 3)
-			__builtin_amdgcn_s_setprio(3);
-	} else {
-		if (q >= 2)
-			__builtin_amdgcn_s_setprio(3);
-		else
-			__builtin_amdgcn_s_setprio(1);
-	}
-}
-
 template <int MODE>
 __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits,
 						  const uint8_t *active, int n, const int *perm,
@@ -143,9 +69,11 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 		gate.mark(c == 0 && L > 0, 1);	/* no live channel: the tag stays 0 */
 		if (c >= L)
 			return;
-		ana_wave_prio(prio, blockIdx.x, (L + WAVE - 1) / WAVE);
+		/* progprio.h: the counter is the sort's control word nlive[2] */
+		PP_BEGIN(prio ? (unsigned *) (nlive + 2) : nullptr, (L + WAVE - 1) / WAVE);
 		c = perm[c];
 	} else {
+		PP_BEGIN(nullptr, 1);
 		gate.mark(c == 0, 1);
 		if (c >= n || (active && !active[c]))
 			return;
@@ -171,6 +99,7 @@ __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana(EncState *enc
 __global__ __launch_bounds__(WAVE, MELPE_ENC_WAVES) void k_enc_ana_dbg(EncState *enc, const int16_t *sp, int n, int upto)
 {
 	int c = blockIdx.x * WAVE + threadIdx.x;
+	PP_BEGIN(nullptr, 1);
 	if (c >= n || upto <= 0)
 		return;
 	AnaLane L;
@@ -193,13 +122,13 @@ static unsigned ana_lds_bytes(void)
 	return (unsigned) v;
 }
 
-/* MELPE_ANA_PRIO: the waves' issue priority by lane order (ana_wave_prio) */
+/* MELPE_ANA_PRIO=0: no progress-driven priority (progprio.h), for A/Bs */
 static int ana_prio_mode(void)
 {
 	static int v = -1;
 	if (v < 0) {
 		const char *e = getenv("MELPE_ANA_PRIO");
-		v = e ? atoi(e) : 0;
+		v = e ? (atoi(e) != 0) : 1;
 	}
 	return v;
 }
@@ -208,13 +137,6 @@ extern "C" int kl_enc_ana(EncState *enc, const int16_t *sp, uint8_t *bits, const
 			  int n, const int *perm, const int *nlive, int16_t *res, AnaGate gate, hipStream_t s)
 {
 	const int pm = ana_prio_mode();
-	if (pm == 6) {	/* the progress counter restarts with each launch */
-		static const AnaProg z = {0u, 6};
-		hipError_t er = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ana_prog), &z, sizeof(z), 0,
-						       hipMemcpyHostToDevice, s);
-		if (er != hipSuccess)
-			return (int) er;
-	}
 	if (res)
 		k_enc_ana<1><<<grid_for(n), WAVE, ana_lds_bytes(), s>>>(enc, sp, bits, active, n, perm, nlive, res,
 									 gate, pm);

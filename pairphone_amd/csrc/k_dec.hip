@@ -3,6 +3,8 @@
  * postfilter of one superframe per active channel, one lane per channel.
  */
 #define MELPE_IDFT_LDS	/* realIDFT's table from LDS (decoder.h) */
+#define MELPE_PROG_PRIO	/* progprio.h: DEC_CKPT in k_decode */
+#include <stdlib.h>
 #include "kern.h"
 
 MELPE_TU(dec)
@@ -19,11 +21,16 @@ struct DecLane {
 
 __global__ __launch_bounds__(DEC_BLOCK, MELPE_DEC_WAVES) void k_decode(DecState *dec, int16_t *sp,
 						      const uint8_t *bits, const uint8_t *active, int n,
-						      const int *perm, const int *nlive)
+						      const int *perm, const int *nlive, int prio)
 {
 	for (int len = 1; len <= PITCHMAX; len++)
 		for (int i = threadIdx.x; i < len; i += blockDim.x)
 			s_idft_cos[((len - 1) * len) / 2 + i] = g_der.idft_cos[len][i];
+	/* progprio.h: the counter is the sort's control word nlive[2] */
+	if (perm)
+		PP_BEGIN(prio ? (unsigned *) (nlive + 2) : nullptr, (*nlive + WAVE - 1) / WAVE);
+	else
+		PP_BEGIN(nullptr, 1);
 	__syncthreads();
 	/* lane g decodes channel perm[g] when the engine ordered the live
 	 * channels by pitch class (engine.hip, MELPE_BIN) */
@@ -46,13 +53,25 @@ __global__ __launch_bounds__(DEC_BLOCK, MELPE_DEC_WAVES) void k_decode(DecState 
 	lane_copy(sp + (size_t) c * BLOCK, L.out, sizeof(int16_t) * BLOCK);
 }
 
+/* MELPE_DEC_PRIO=0: no progress-driven priority (progprio.h), for A/Bs */
+static int dec_prio_mode(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("MELPE_DEC_PRIO");
+		v = e ? (atoi(e) != 0) : 1;
+	}
+	return v;
+}
+
 extern "C" int kl_decode(DecState *dec, int16_t *sp, const uint8_t *bits, const uint8_t *active,
 			 int n, const int *perm, const int *nlive, hipStream_t s)
 {
 	int b = DEC_BLOCK;
 	while (b > WAVE && (n + b - 1) / b < 1024)
 		b /= 2;
-	k_decode<<<(n + b - 1) / b, b, IDFT_LDS_WORDS * sizeof(int16_t), s>>>(dec, sp, bits, active, n, perm, nlive);
+	k_decode<<<(n + b - 1) / b, b, IDFT_LDS_WORDS * sizeof(int16_t), s>>>(dec, sp, bits, active, n, perm, nlive,
+									     dec_prio_mode());
 	return (int) hipGetLastError();
 }
 
@@ -94,6 +113,7 @@ __global__ __launch_bounds__(DEC2_BLOCK, MELPE_DEC_WAVES) void k_decode2(DecStat
 	for (int len = 1; len <= PITCHMAX; len++)
 		for (int i = threadIdx.x; i < len; i += blockDim.x)
 			s_idft_cos[((len - 1) * len) / 2 + i] = g_der.idft_cos[len][i];
+	PP_BEGIN(nullptr, 1);	/* no checkpoint is on its path; kept off all the same */
 	__syncthreads();
 	const int w = threadIdx.x / WAVE, t = threadIdx.x % WAVE;
 	const int grp = blockIdx.x * DEC2_GROUPS + (w >> 1), role = w & 1;
@@ -178,6 +198,6 @@ extern "C" int kl_dec_warm(int n, hipStream_t s)
 	while (b > WAVE && (n + b - 1) / b < 1024)
 		b /= 2;
 	k_decode<<<(n + b - 1) / b, b, IDFT_LDS_WORDS * sizeof(int16_t), s>>>(nullptr, nullptr, nullptr, nullptr,
-									     0, nullptr, nullptr);
+									     0, nullptr, nullptr, 0);
 	return (int) hipGetLastError();
 }

@@ -24,6 +24,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include "progprio.h"	/* before the codec: its checkpoint hooks */
 #include "codec.h"
 
 using namespace mlp;
