@@ -244,6 +244,16 @@ class EngineWorkload:
         self.eng.encode_pipe_dev(self.bits[s].data_ptr(), self.pcm[s].data_ptr(),
                                  None if nxt is None else self.pcm[nxt].data_ptr(), stream=self.rig.sptr)
 
+    def duplex(self, s, nxt, d):
+        """pipe(s, nxt) plus the decode of superframe d (None: none) on the
+        engine's decoder stream, beside it (melpe_duplex_pipe_dev)"""
+        if self.out is None:
+            self.out = self.rig.torch.empty_like(self.pcm)
+        self.eng.duplex_pipe_dev(self.bits[s].data_ptr(), self.pcm[s].data_ptr(),
+                                 None if nxt is None else self.pcm[nxt].data_ptr(),
+                                 None if d is None else self.out[d].data_ptr(),
+                                 None if d is None else self.bits[d].data_ptr(), stream=self.rig.sptr)
+
     def restart(self):
         """fresh-process state and the raw input again (melpe_engine_reset)"""
         self.eng.reset()
@@ -541,37 +551,51 @@ def round_trip_leg(rig, args, rank, world):
     """BASELINE config 3: the encode + decode round trip (melpe_a then melpe_s
     with the postfilter, melpe/melpe.c:91-107) of --rt-channels channels per
     GPU on one engine; one step = k_enc_npp + the analysis + k_decode of one
-    superframe of every channel, each launch timed with HIP events.  After the
-    timed region the bits and the decoded PCM of sampled channels are checked
+    superframe of every channel.  Timed serialised (each launch alone, HIP
+    events), then from fresh state as the engine runs it: superframe k's
+    analysis, k+1's NPP and the decode of k-1's bits on three queues
+    (melpe_duplex_pipe_dev), whose bits and PCM must equal the serialised
+    run's.  After the timed region the bits and the decoded PCM of sampled channels are checked
     against the reference (oracle/_ref/ref_tool encgen + decgen on the same
     synthetic channels), on rank 0."""
     C, K, W = args.rt_channels, args.steps, args.warmup
     wl = EngineWorkload(rig, C, rank * C, W + K)
     # serialised, each launch timed alone; then from fresh state the same
-    # work with the encode pipelined (pipe_leg), decode after each step
+    # work on the engine's three queues
     ser, (npp_kms, ana_kms, dec_kms) = timed(rig, [wl.npp, wl.ana, wl.dec], K, W)
     ser_bits, ser_out = wl.bits.clone(), wl.out.clone()
     wl.restart()
-    pipe_warmup(wl, W, dec=True)
+    # warm-up in the same form (the engine makes and warms its side streams
+    # at the first call): npp(0), duplex(0, 1, -), duplex(1, 2, 0), ...,
+    # duplex(W-1, -, W-2); the timed region then holds exactly K NPPs, K
+    # analyses and K decodes: npp(W), duplex(W+i, W+i+1, W+i-1) for i < K
+    # (the decode of W+K-1 follows it)
+    if W > 0:
+        wl.npp(0)
+        for s in range(W):
+            wl.duplex(s, s + 1 if s + 1 < W else None, s - 1 if s > 0 else None)
     rig.sync()
     rig.barrier()
     rig.sync()
     t0 = time.perf_counter()
     wl.npp(W)
     for i in range(K):
-        wl.pipe(W + i, W + i + 1 if i + 1 < K else None)
-        wl.dec(W + i)
+        s = W + i
+        wl.duplex(s, s + 1 if i + 1 < K else None, s - 1 if s > 0 else None)
     rig.sync()
     rig.barrier()
     rig.sync()
     dt = rig.max_over_ranks(time.perf_counter() - t0)
+    wl.dec(W + K - 1)
+    rig.sync()
     same = bool((ser_bits == wl.bits).all()) and bool((ser_out == wl.out).all())
     del ser_bits, ser_out
     res = {"workload": "config 3: %d channels per GPU, melpe_a + melpe_s (with postfilter) "
                        "per superframe on one engine" % C,
            "channels_per_gpu": C, "value": world * C * K * SF_SECONDS / dt,
            "unit": "channel-s/s (encoded and decoded)", "ms_per_step": 1e3 * dt / K,
-           "step": "encode pipelined (superframe k's analysis beside k+1's NPP), then decode of k",
+           "step": "melpe_duplex_pipe_dev: superframe k's analysis, k+1's NPP and the decode of "
+                   "k-1's bits on three queues of one engine",
            "ms_per_step_serialised": 1e3 * ser / K, "bits_pcm_equal_serialised": same,
            "kernels_ms": {"k_enc_npp": npp_kms, "k_enc_ana": ana_kms, "k_decode": dec_kms}}
     oc = opcount()

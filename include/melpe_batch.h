@@ -176,6 +176,19 @@ int melpe_encode_ana_dev(melpe_engine *e, void *d_bits, const void *d_sp, const 
 int melpe_encode_pipe_dev(melpe_engine *e, void *d_bits, const void *d_sp, const void *d_active,
 			  void *d_sp_next, const void *d_active_next, void *hip_stream);
 
+/* melpe_encode_pipe_dev plus a decode (melpe_decode_dev: d_dec_bits in,
+ * C x 11; d_dec_sp out, C x 540; NULL d_dec_bits = no decode) on a third
+ * internal stream, concurrently with the encode's analysis and next NPP --
+ * a round trip or a duplex link, e.g. decoding the bits the previous call
+ * encoded (BASELINE config 3).  The decoder touches only the channels'
+ * decoder state, so the results are those of the same calls serialised.
+ * d_dec_bits must not be d_bits and d_dec_sp none of d_sp, d_sp_next.
+ * Ordered on hip_stream like the other *_dev calls: all three parts start
+ * after its earlier work and its later work waits for all three. */
+int melpe_duplex_pipe_dev(melpe_engine *e, void *d_bits, const void *d_sp, const void *d_active,
+			  void *d_sp_next, const void *d_active_next, void *d_dec_sp,
+			  const void *d_dec_bits, const void *d_dec_active, void *hip_stream);
+
 /* melpe_s on every active channel: bits (C x 11, in), sp (C x 540, out) */
 int melpe_decode_host(melpe_engine *e, int16_t *sp, const unsigned char *bits,
 		      const uint8_t *active);

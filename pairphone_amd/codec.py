@@ -61,6 +61,7 @@ def load_library(path=None):
         "melpe_encode_npp_dev": (i32, [vp, vp, vp, vp]),
         "melpe_encode_ana_dev": (i32, [vp, vp, vp, vp, vp]),
         "melpe_encode_pipe_dev": (i32, [vp, vp, vp, vp, vp, vp, vp]),
+        "melpe_duplex_pipe_dev": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "melpe_decode_host": (i32, [vp, vp, vp, vp]),
         "melpe_decode_dev": (i32, [vp, vp, vp, vp, vp]),
         "melpe_npp_host": (i32, [vp, vp, i32, i32, vp]),
@@ -362,6 +363,13 @@ class MelpeEngine:
         the NPP of superframe k + 1 (d_sp_next, or None)"""
         _check(self.lib.melpe_encode_pipe_dev(self.h, d_bits, d_sp, d_active, d_sp_next, d_active_next,
                                               stream))
+
+    def duplex_pipe_dev(self, d_bits, d_sp, d_sp_next, d_dec_sp, d_dec_bits, d_active=None,
+                        d_active_next=None, d_dec_active=None, stream=None):
+        """encode_pipe_dev plus a decode (d_dec_bits -> d_dec_sp, or None)
+        on the engine's decoder stream, beside the encode"""
+        _check(self.lib.melpe_duplex_pipe_dev(self.h, d_bits, d_sp, d_active, d_sp_next, d_active_next,
+                                              d_dec_sp, d_dec_bits, d_dec_active, stream))
 
     def encode_ana_dev(self, d_bits, d_sp, d_active=None, stream=None):
         _check(self.lib.melpe_encode_ana_dev(self.h, d_bits, d_sp, d_active, stream))

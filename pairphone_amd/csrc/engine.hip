@@ -764,6 +764,9 @@ struct melpe_engine {
 		bool used = false;
 	} slot[2];
 	hipStream_t cin = nullptr, cout = nullptr;
+	/* melpe_duplex_pipe_dev's decoder stream and its hops */
+	hipStream_t cdec = nullptr;
+	hipEvent_t ev_dec = nullptr;
 	long async_calls = 0;
 	hipStream_t own = nullptr;	/* melpe_engine_set_own_stream */
 };
@@ -1341,6 +1344,10 @@ int melpe_engine_destroy(melpe_engine *e)
 		hipStreamDestroy(e->cin);
 	if (e->cout)
 		hipStreamDestroy(e->cout);
+	if (e->cdec)
+		hipStreamDestroy(e->cdec);
+	if (e->ev_dec)
+		hipEventDestroy(e->ev_dec);
 	delete e;
 	return 0;
 }
@@ -1534,6 +1541,53 @@ int melpe_encode_pipe_dev(melpe_engine *e, void *d_bits, const void *d_sp, const
 	return _call.finish();
 }
 
+static int dec_queue(melpe_engine *e);
+
+int melpe_duplex_pipe_dev(melpe_engine *e, void *d_bits, const void *d_sp, const void *d_active,
+			  void *d_sp_next, const void *d_active_next, void *d_dec_sp,
+			  const void *d_dec_bits, const void *d_dec_active, void *hip_stream)
+{
+	if (!e || !d_bits || !d_sp || (d_dec_bits && !d_dec_sp))
+		return fail_msg("melpe_duplex_pipe_dev: null argument");
+	if (d_sp_next == d_sp)
+		return fail_msg("melpe_duplex_pipe_dev: the next superframe's PCM must be another buffer");
+	if (d_dec_bits && (d_dec_bits == d_bits || d_dec_sp == d_sp || d_dec_sp == d_sp_next))
+		return fail_msg("melpe_duplex_pipe_dev: the decode's buffers must differ from the encode's");
+	DEVGUARD(e->device);
+	if (d_sp_next || d_dec_bits)
+		if (int rc = d_dec_bits ? dec_queue(e) : side_streams(e))
+			return rc;
+	hipStream_t s = (hipStream_t) hip_stream;
+	ENGINE_CALL(e, s);
+	/* three queues: the analysis of this superframe on the engine stream, and
+	 * once its lane-order sort is done (so that the analysis' waves, the
+	 * longest, are dispatched first) the next superframe's NPP on cin
+	 * (melpe_encode_pipe_dev) and the decode on cdec.  The encoder and
+	 * decoder halves of a record and their lane-order buffers (bin_enc,
+	 * bin_dec) are disjoint. */
+	ev_begin(e, s);
+	HIPCHK((hipError_t) ana_launch(e, (const int16_t *) d_sp, (uint8_t *) d_bits, (const uint8_t *) d_active,
+				       s, (d_sp_next || d_dec_bits) ? e->ev_pin : nullptr));
+	ev_end(e, s, false);
+	if (d_dec_bits) {
+		HIPCHK(hipStreamWaitEvent(e->cdec, e->ev_pin, 0));
+		HIPCHK((hipError_t) dec_launch(e, (int16_t *) d_dec_sp, (const uint8_t *) d_dec_bits,
+					       (const uint8_t *) d_dec_active, e->cdec));
+		HIPCHK(hipEventRecord(e->ev_dec, e->cdec));
+	}
+	if (d_sp_next) {
+		HIPCHK(hipStreamWaitEvent(e->cin, e->ev_pin, 0));
+		HIPCHK((hipError_t) kl_enc_npp(e->d_enc, (int16_t *) d_sp_next, (const uint8_t *) d_active_next,
+					       e->channels, e->cin));
+		HIPCHK(hipEventRecord(e->ev_npp, e->cin));
+		HIPCHK(hipStreamWaitEvent(s, e->ev_npp, 0));
+	}
+	/* the hop back to the caller covers the decode too */
+	if (d_dec_bits)
+		HIPCHK(hipStreamWaitEvent(s, e->ev_dec, 0));
+	return _call.finish();
+}
+
 int melpe_encode_host(melpe_engine *e, unsigned char *bits, int16_t *sp, const uint8_t *active)
 {
 	if (!e || !bits || !sp)
@@ -1573,6 +1627,26 @@ static int side_streams(melpe_engine *e)
 	HIPCHK(hipStreamCreateWithFlags(&e->cin, hipStreamNonBlocking));
 	HIPCHK((hipError_t) kl_npp_warm(e->channels, e->cin));
 	HIPCHK(hipStreamSynchronize(e->cin));
+	return 0;
+}
+
+/* melpe_duplex_pipe_dev's decoder stream, made after the two side streams
+ * (so the three land on hardware queues in a fixed order), with the
+ * decoder kernels' scratch reserved on its queue as engine_warm does on the
+ * engine stream's */
+static int dec_queue(melpe_engine *e)
+{
+	if (e->cdec)
+		return 0;
+	if (int rc = side_streams(e))
+		return rc;
+	if (!e->ev_dec)
+		HIPCHK(hipEventCreateWithFlags(&e->ev_dec, hipEventDisableTiming));
+	HIPCHK(hipStreamCreateWithFlags(&e->cdec, hipStreamNonBlocking));
+	HIPCHK((hipError_t) kl_dec_warm(e->channels, e->cdec));
+	if (e->d_hb)
+		HIPCHK((hipError_t) kl_dec2_warm(e->channels, e->cdec));
+	HIPCHK(hipStreamSynchronize(e->cdec));
 	return 0;
 }
 

@@ -294,3 +294,40 @@ def test_duplex_encoder_decoder_on_own_streams_match_goldens():
     assert [c for c in range(C) if sha(b[c]) != ge["bits_sha256"][c]] == []
     assert [c for c in range(C) if sha(n[c]) != ge["npp_sha256"][c]] == []
     assert [c for c in range(C) if sha(p[c]) != gd["pcm_sha256"][c]] == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("waves", [1, 2])
+def test_duplex_pipe_dev_matches_goldens(waves):
+    """melpe_duplex_pipe_dev on one engine: superframe k's analysis, k+1's
+    NPP and the decode of superframe k-1's bits on three internal streams
+    (the config-3 round trip as bench.py times it), both decoder mappings:
+    the bits, the NPP output and the decoded PCM match the 1,024-channel
+    goldens, as the same calls serialised do."""
+    import torch
+    from pairphone_amd import MelpeEngine
+    ge, gd = enc_golden(), gold("dec_1024.json")
+    C, nsf = ge["channels"], ge["superframes"]
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    x = torch.from_numpy(np.ascontiguousarray(
+        signals(ge["seed"], C, nsf).reshape(C, nsf, 540).transpose(1, 0, 2))).to(dev)
+    bits = torch.zeros((nsf, C, 11), dtype=torch.uint8, device=dev)
+    pcm = torch.zeros((nsf, C, 540), dtype=torch.int16, device=dev)
+    eng = MelpeEngine(C)
+    eng.set_dec_waves(waves)
+    eng.encode_npp_dev(x[0].data_ptr(), None, s)
+    for k in range(nsf):
+        eng.duplex_pipe_dev(bits[k].data_ptr(), x[k].data_ptr(),
+                            x[k + 1].data_ptr() if k + 1 < nsf else None,
+                            pcm[k - 1].data_ptr() if k > 0 else None,
+                            bits[k - 1].data_ptr() if k > 0 else None, stream=s)
+    eng.decode_dev(pcm[nsf - 1].data_ptr(), bits[nsf - 1].data_ptr(), None, s)
+    torch.cuda.synchronize(dev)
+    eng.close()
+    b = bits.cpu().numpy().transpose(1, 0, 2).reshape(C, nsf * 11)
+    n = x.cpu().numpy().transpose(1, 0, 2).reshape(C, nsf * 540)
+    p = pcm.cpu().numpy().transpose(1, 0, 2).reshape(C, nsf * 540)
+    assert [c for c in range(C) if sha(b[c]) != ge["bits_sha256"][c]] == []
+    assert [c for c in range(C) if sha(n[c]) != ge["npp_sha256"][c]] == []
+    assert [c for c in range(C) if sha(p[c]) != gd["pcm_sha256"][c]] == []
