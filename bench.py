@@ -664,23 +664,62 @@ def tx_leg(rig, args, rank, world):
     votes = torch.zeros((nsf, C), dtype=torch.uint8, device=rig.dev)
     gate = torch.zeros((nsf, C), dtype=torch.uint8, device=rig.dev)
     vst = torch.zeros(C * lib.melpe_vad_state_bytes(), dtype=torch.uint8, device=rig.dev)
-    if lib.melpe_vad_reset_dev(vst.data_ptr(), C, None, rig.sptr):
-        raise RuntimeError(lib.melpe_last_error().decode())
-    rig.sync()
+
+    def fresh():
+        """fresh codec and VAD state, the raw input again"""
+        eng.reset()
+        eng.synth_seed(RUN_SEED, first_channel=lo)
+        for s in range(nsf):
+            eng.synth_dev(pcm[s].data_ptr(), SF_SAMPLES, rig.sptr)
+        if lib.melpe_vad_reset_dev(vst.data_ptr(), C, None, rig.sptr):
+            raise RuntimeError(lib.melpe_last_error().decode())
+        for t in (bits, votes, gate):
+            t.zero_()
+        rig.sync()
 
     def step(s):
         if s < nsf:
             eng.tx_dev(vst.data_ptr(), bits[s].data_ptr(), pcm[s].data_ptr(), votes[s].data_ptr(),
                        gate[s].data_ptr(), act[s].data_ptr(), rig.sptr)
+
+    def pstep(s):
+        """the pipelined form: superframe s's analysis beside s+1's VAD and NPP"""
+        if s == 0:
+            eng.tx_npp_dev(vst.data_ptr(), pcm[0].data_ptr(), votes[0].data_ptr(), gate[0].data_ptr(),
+                           act[0].data_ptr(), rig.sptr)
+        if s < nsf:
+            nx = s + 1 < nsf
+            eng.tx_pipe_dev(vst.data_ptr(), bits[s].data_ptr(), pcm[s].data_ptr(), gate[s].data_ptr(),
+                            pcm[s + 1].data_ptr() if nx else None, votes[s + 1].data_ptr() if nx else None,
+                            gate[s + 1].data_ptr() if nx else None, act[s + 1].data_ptr() if nx else None,
+                            stream=rig.sptr)
     # every rank runs the job's step count (its own streams may end sooner)
     steps = int(rig.max_over_ranks(float(nsf)))
-    dt, (kms,) = timed(rig, [step], steps, 0)
+    fresh()
+    ser_dt, (ser_kms,) = timed(rig, [step], steps, 0)
+    ser = (bits.clone(), votes.clone(), gate.clone())
+    fresh()
+    # the engine makes and warms its side stream at its first pipelined call:
+    # one call with every mask zero (no channel's state moves) before timing
+    z = torch.zeros((2, C), dtype=torch.uint8, device=rig.dev)
+    zp = torch.zeros((2, C, SF_SAMPLES), dtype=torch.int16, device=rig.dev)
+    zb = torch.zeros((C, SF_BYTES), dtype=torch.uint8, device=rig.dev)
+    eng.tx_pipe_dev(vst.data_ptr(), zb.data_ptr(), zp[0].data_ptr(), z[0].data_ptr(), zp[1].data_ptr(),
+                    zb.data_ptr(), z[1].data_ptr(), z[0].data_ptr(), stream=rig.sptr)
+    rig.sync()
+    del z, zp, zb
+    dt, (kms,) = timed(rig, [pstep], steps, 0)
+    same = all(bool(torch.equal(a, b)) for a, b in zip(ser, (bits, votes, gate)))
+    del ser
     chs = float(lengths_all.sum()) * SF_SECONDS
     res = {"workload": "config 5: %d streams (%d per GPU on average), ragged lengths uniform in "
                        "[1 s, 20 s] (seed %d), VAD2 gate + melpe_a on the opened superframes"
                        % (len(lengths_all), args.tx_channels, RUN_SEED + 5),
            "value": chs / dt, "unit": "channel-s/s (whole streams)",
            "wall_s": dt, "steps": steps, "mean_step_ms": kms,
+           "step": "melpe_tx_pipe_dev: superframe k's analysis beside k+1's VAD gate and NPP",
+           "value_serialised": chs / ser_dt, "mean_step_ms_serialised": ser_kms,
+           "bits_votes_gates_equal_serialised": same,
            "channel_seconds": chs,
            "gated_open_fraction": float(gate.float().sum().item() / act.float().sum().item()),
            "sharding": "shard.superframe_range: contiguous channel ranges balanced by total "

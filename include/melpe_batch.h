@@ -276,6 +276,21 @@ int melpe_vad_host(unsigned char *state, const int16_t *sp, uint8_t *votes, int 
  * all channels (ragged streams pass their mask). */
 int melpe_tx_dev(melpe_engine *e, void *d_vad_state, void *d_bits, void *d_sp, void *d_votes,
 		 void *d_gate, const void *d_active, void *hip_stream);
+/* melpe_tx_dev in two halves, for the pipelined form: melpe_tx_npp_dev is
+ * the VAD gate and the NPP of the channels it opens; melpe_tx_pipe_dev is
+ * the analysis of superframe k under its gate (d_gate, written by the
+ * previous call) and, concurrently on a second internal stream once the
+ * analysis' lane-order sort is done, the VAD of superframe k + 1
+ * (d_votes_next, d_gate_next out; d_active_next its mask) and the NPP of
+ * the channels that gate opens (d_sp_next NULL = none).  A sequence
+ * tx_npp(0), tx_pipe(0, 1), ..., tx_pipe(K-1, NULL) gives the bits, votes,
+ * gates and NPP output of K melpe_tx_dev calls.  The next superframe's
+ * buffers must be other buffers than this one's. */
+int melpe_tx_npp_dev(melpe_engine *e, void *d_vad_state, void *d_sp, void *d_votes, void *d_gate,
+		     const void *d_active, void *hip_stream);
+int melpe_tx_pipe_dev(melpe_engine *e, void *d_vad_state, void *d_bits, const void *d_sp,
+		      const void *d_gate, void *d_sp_next, void *d_votes_next, void *d_gate_next,
+		      const void *d_active_next, void *hip_stream);
 /* The VAD-framed stream format of melpe_enc.c:55-72 / melpe_dec.c:33-49
  * (host functions, no GPU).  Per superframe a silent channel writes 1 byte,
  * its carried txbuf[0] with bit 1 set; a voiced channel writes its 11 bytes

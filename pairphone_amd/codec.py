@@ -80,6 +80,8 @@ def load_library(path=None):
         "melpe_vad_dev": (i32, [vp, vp, vp, i32, vp, vp]),
         "melpe_vad_host": (i32, [vp, vp, vp, i32, vp]),
         "melpe_tx_dev": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "melpe_tx_npp_dev": (i32, [vp, vp, vp, vp, vp, vp, vp]),
+        "melpe_tx_pipe_dev": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "melpe_stream_pack": (i32, [vp, vp, vp, vp, vp, i32, vp]),
         "melpe_stream_unpack": (ctypes.c_long, [vp, ctypes.c_long, vp, vp, ctypes.c_long]),
         "melpe_encode2400_dev": (i32, [vp, vp, vp, vp, vp]),
@@ -378,6 +380,17 @@ class MelpeEngine:
         """VAD gate + melpe_a on the channels it opens (tx.c:232-245)"""
         _check(self.lib.melpe_tx_dev(self.h, d_vad_state, d_bits, d_sp, d_votes, d_gate,
                                      d_active, stream))
+
+    def tx_npp_dev(self, d_vad_state, d_sp, d_votes, d_gate, d_active=None, stream=None):
+        """the first half of tx_dev: VAD gate + the NPP of the opened channels"""
+        _check(self.lib.melpe_tx_npp_dev(self.h, d_vad_state, d_sp, d_votes, d_gate, d_active, stream))
+
+    def tx_pipe_dev(self, d_vad_state, d_bits, d_sp, d_gate, d_sp_next, d_votes_next, d_gate_next,
+                    d_active_next=None, stream=None):
+        """superframe k's analysis under its gate beside superframe k+1's
+        VAD and NPP (d_sp_next None: none)"""
+        _check(self.lib.melpe_tx_pipe_dev(self.h, d_vad_state, d_bits, d_sp, d_gate, d_sp_next,
+                                          d_votes_next, d_gate_next, d_active_next, stream))
 
     def decode_dev(self, d_sp, d_bits, d_active=None, stream=None):
         _check(self.lib.melpe_decode_dev(self.h, d_sp, d_bits, d_active, stream))

@@ -2343,6 +2343,67 @@ int melpe_tx_dev(melpe_engine *e, void *d_vad_state, void *d_bits, void *d_sp, v
 	return melpe_encode_dev(e, d_bits, d_sp, d_gate, hip_stream);
 }
 
+/* the first half of melpe_tx_dev: the VAD gate and the NPP of the channels
+ * it opens (the analysis follows in melpe_tx_pipe_dev or
+ * melpe_encode_ana_dev with the gate as the mask) */
+int melpe_tx_npp_dev(melpe_engine *e, void *d_vad_state, void *d_sp, void *d_votes, void *d_gate,
+		     const void *d_active, void *hip_stream)
+{
+	if (!e || !d_vad_state || !d_sp || !d_votes || !d_gate)
+		return fail_msg("melpe_tx_npp_dev: bad arguments");
+	if ((uintptr_t) d_vad_state & 3)
+		return fail_msg("melpe_tx_npp_dev: state must be 4-byte aligned");
+	DEVGUARD(e->device);
+	k_vad<<<grid_for(e->channels), WAVE, 0, (hipStream_t) hip_stream>>>(
+		(VadState *) d_vad_state, (const int16_t *) d_sp, (uint8_t *) d_votes,
+		(uint8_t *) d_gate, (const uint8_t *) d_active, e->channels);
+	HIPCHK(hipGetLastError());
+	return melpe_encode_npp_dev(e, d_sp, d_gate, hip_stream);
+}
+
+/* the TX front end pipelined like melpe_encode_pipe_dev: superframe k's
+ * analysis on the engine stream (gated by d_gate, which melpe_tx_npp_dev or
+ * the previous call wrote), and once its lane-order sort is done, on cin,
+ * superframe k + 1's VAD (votes and gate out) and the NPP of the channels
+ * it opens.  The VAD state is the VAD's alone, so a sequence tx_npp(0),
+ * tx_pipe(0, 1), ..., tx_pipe(K-1, NULL) gives the bits, votes, gates and
+ * NPP output of K melpe_tx_dev calls. */
+int melpe_tx_pipe_dev(melpe_engine *e, void *d_vad_state, void *d_bits, const void *d_sp, const void *d_gate,
+		      void *d_sp_next, void *d_votes_next, void *d_gate_next, const void *d_active_next,
+		      void *hip_stream)
+{
+	if (!e || !d_vad_state || !d_bits || !d_sp || !d_gate ||
+	    (d_sp_next && (!d_votes_next || !d_gate_next)))
+		return fail_msg("melpe_tx_pipe_dev: bad arguments");
+	if ((uintptr_t) d_vad_state & 3)
+		return fail_msg("melpe_tx_pipe_dev: state must be 4-byte aligned");
+	if (d_sp_next == d_sp || (d_sp_next && d_gate_next == d_gate))
+		return fail_msg("melpe_tx_pipe_dev: the next superframe's buffers must be other buffers");
+	DEVGUARD(e->device);
+	if (d_sp_next)
+		if (int rc = side_streams(e))
+			return rc;
+	hipStream_t s = (hipStream_t) hip_stream;
+	ENGINE_CALL(e, s);
+	ev_begin(e, s);
+	HIPCHK((hipError_t) ana_launch(e, (const int16_t *) d_sp, (uint8_t *) d_bits, (const uint8_t *) d_gate, s,
+				       d_sp_next ? e->ev_pin : nullptr));
+	ev_end(e, s, false);
+	if (d_sp_next) {
+		const hipStream_t ns = e->cin;
+		HIPCHK(hipStreamWaitEvent(ns, e->ev_pin, 0));
+		k_vad<<<grid_for(e->channels), WAVE, 0, ns>>>((VadState *) d_vad_state, (const int16_t *) d_sp_next,
+							      (uint8_t *) d_votes_next, (uint8_t *) d_gate_next,
+							      (const uint8_t *) d_active_next, e->channels);
+		HIPCHK(hipGetLastError());
+		HIPCHK((hipError_t) kl_enc_npp(e->d_enc, (int16_t *) d_sp_next, (const uint8_t *) d_gate_next,
+					       e->channels, ns));
+		HIPCHK(hipEventRecord(e->ev_npp, ns));
+		HIPCHK(hipStreamWaitEvent(s, e->ev_npp, 0));
+	}
+	return _call.finish();
+}
+
 
 int melpe_stream_pack(const unsigned char *bits, const uint8_t *votes, uint8_t *last,
 		      unsigned char *out, uint8_t *lens, int channels, const uint8_t *active)

@@ -147,27 +147,41 @@ def test_gpu_tx_front_end_vad_gated_ragged_matches_reference(tmp_path, ref_tool)
 
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream().cuda_stream
-    eng = MelpeEngine(C)
-    st = torch.zeros(C * lib.melpe_vad_state_bytes(), dtype=torch.uint8, device=dev)
-    assert lib.melpe_vad_reset_dev(st.data_ptr(), C, None, s) == 0
-    d_x = torch.from_numpy(np.ascontiguousarray(x.transpose(1, 0, 2))).to(dev)   # nsf x C x 540
-    bits = torch.zeros((nsf, C, 11), dtype=torch.uint8, device=dev)
-    votes = torch.zeros((nsf, C), dtype=torch.uint8, device=dev)
-    gate = torch.zeros((nsf, C), dtype=torch.uint8, device=dev)
-    for k in range(nsf):
-        act = torch.from_numpy((lengths > k).astype(np.uint8)).to(dev)
-        eng.tx_dev(st.data_ptr(), bits[k].data_ptr(), d_x[k].data_ptr(), votes[k].data_ptr(),
-                   gate[k].data_ptr(), act.data_ptr(), s)
-    torch.cuda.synchronize()
-    got_votes = votes.cpu().numpy().T
-    got_gate = gate.cpu().numpy().T
-    got_bits = bits.cpu().numpy().transpose(1, 0, 2)
-    closed = 0
-    for c in range(C):
-        L = lengths[c]
-        assert np.array_equal(got_votes[c, :L], want_votes[c, :L]), c
-        assert np.array_equal(got_gate[c], (np.arange(nsf) < L) & (want_votes[c] > 0)), c
-        assert np.array_equal(got_bits[c, :L], want_bits[c]), c
-        assert not got_bits[c, L:].any()
-        closed += int((want_votes[c, :L] == 0).sum())
-    assert closed > 0      # the gate did close somewhere
+    acts = torch.from_numpy(np.stack([(lengths > k).astype(np.uint8) for k in range(nsf)])).to(dev)
+    # melpe_tx_dev per superframe, then the pipelined form (melpe_tx_npp_dev,
+    # melpe_tx_pipe_dev: superframe k's analysis beside k+1's VAD and NPP)
+    for pipe in (False, True):
+        eng = MelpeEngine(C)
+        st = torch.zeros(C * lib.melpe_vad_state_bytes(), dtype=torch.uint8, device=dev)
+        assert lib.melpe_vad_reset_dev(st.data_ptr(), C, None, s) == 0
+        d_x = torch.from_numpy(np.ascontiguousarray(x.transpose(1, 0, 2))).to(dev)   # nsf x C x 540
+        bits = torch.zeros((nsf, C, 11), dtype=torch.uint8, device=dev)
+        votes = torch.zeros((nsf, C), dtype=torch.uint8, device=dev)
+        gate = torch.zeros((nsf, C), dtype=torch.uint8, device=dev)
+        if pipe:
+            eng.tx_npp_dev(st.data_ptr(), d_x[0].data_ptr(), votes[0].data_ptr(), gate[0].data_ptr(),
+                           acts[0].data_ptr(), s)
+        for k in range(nsf):
+            if not pipe:
+                eng.tx_dev(st.data_ptr(), bits[k].data_ptr(), d_x[k].data_ptr(), votes[k].data_ptr(),
+                           gate[k].data_ptr(), acts[k].data_ptr(), s)
+                continue
+            nx = k + 1 < nsf
+            eng.tx_pipe_dev(st.data_ptr(), bits[k].data_ptr(), d_x[k].data_ptr(), gate[k].data_ptr(),
+                            d_x[k + 1].data_ptr() if nx else None, votes[k + 1].data_ptr() if nx else None,
+                            gate[k + 1].data_ptr() if nx else None, acts[k + 1].data_ptr() if nx else None,
+                            stream=s)
+        torch.cuda.synchronize()
+        eng.close()
+        got_votes = votes.cpu().numpy().T
+        got_gate = gate.cpu().numpy().T
+        got_bits = bits.cpu().numpy().transpose(1, 0, 2)
+        closed = 0
+        for c in range(C):
+            L = lengths[c]
+            assert np.array_equal(got_votes[c, :L], want_votes[c, :L]), (pipe, c)
+            assert np.array_equal(got_gate[c], (np.arange(nsf) < L) & (want_votes[c] > 0)), (pipe, c)
+            assert np.array_equal(got_bits[c, :L], want_bits[c]), (pipe, c)
+            assert not got_bits[c, L:].any()
+            closed += int((want_votes[c, :L] == 0).sum())
+        assert closed > 0      # the gate did close somewhere
