@@ -31,7 +31,9 @@
  * stream, and later work on that stream after it.  Its kernels run on the
  * device's engine stream (two event hops), so the *_dev calls of all engines
  * on a device execute in the order they were made, whatever streams they
- * name.  The
+ * name (the pipelined calls, melpe_encode_pipe_dev, melpe_duplex_pipe_dev
+ * and melpe_tx_pipe_dev, also run parts on the engine's own side streams,
+ * still inside that order).  The
  * *_host calls, melpe_engine_reset and the state export/import first wait
  * for every *_dev call of the same engine already enqueued, on any stream
  * (the engine records an event on each stream it is given), and for nothing
