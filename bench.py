@@ -497,12 +497,14 @@ def host_leg(rig, C, first, K, W, dev_bits, world):
 def duplex_leg(rig, wl, C, K, W):
     """A duplex link's two directions on one GPU: an encoder engine and a
     decoder engine of C channels, superframe k encoded on one caller stream
-    while superframe k - 1's bits are decoded on another.  Timed twice,
-    fresh engines each time: with both engines on the device's shared engine
-    stream (the default: one hardware queue, the kernels serialise) and
-    with each on a stream of its own (melpe_engine_set_own_stream: the
-    kernels may overlap).  ms per duplex step either way, and whether the
-    two runs' bits agree."""
+    while superframe k - 1's bits are decoded on another.  Timed with fresh
+    engines each time: with both engines on the device's shared engine
+    stream (the default: one hardware queue, the kernels serialise), with
+    each on a stream of its own (melpe_engine_set_own_stream: the kernels
+    may overlap), and with one engine doing both directions
+    (melpe_duplex_pipe_dev: the analysis, the next NPP and the decode on the
+    engine's three streams).  ms per duplex step each way, and whether the
+    runs' bits agree."""
     import torch
     from pairphone_amd import MelpeEngine
     out = {}
@@ -539,11 +541,37 @@ def duplex_leg(rig, wl, C, K, W):
         enc.close()
         dec.close()
         del bits, pcm
+    # one engine, both directions: melpe_duplex_pipe_dev (superframe k's
+    # analysis, k+1's NPP, the decode of k-1 on the engine's three streams)
+    wl.regen_pcm()
+    eng = MelpeEngine(C, device=rig.dev.index)
+    bits = torch.zeros((W + K, C, SF_BYTES), dtype=torch.uint8, device=rig.dev)
+    pcm = torch.empty((C, SF_SAMPLES), dtype=torch.int16, device=rig.dev)
+    s0 = rig.sptr
+
+    def dstep(s):
+        nx = s + 1 < W + K
+        eng.duplex_pipe_dev(bits[s].data_ptr(), wl.pcm[s].data_ptr(), wl.pcm[s + 1].data_ptr() if nx else None,
+                            pcm.data_ptr() if s > 0 else None, bits[s - 1].data_ptr() if s > 0 else None,
+                            stream=s0)
+    eng.encode_npp_dev(wl.pcm[0].data_ptr(), None, s0)
+    for s in range(W):
+        dstep(s)
+    rig.sync()
+    t0 = time.perf_counter()
+    for s in range(W, W + K):
+        dstep(s)
+    rig.sync()
+    out["pipe"] = 1e3 * (time.perf_counter() - t0) / K
+    out["pipe_bits_equal"] = bool(torch.equal(ref_bits, bits.cpu()))
+    eng.close()
+    del bits, pcm
     res = {"ms_per_step_shared_stream": out["shared"], "ms_per_step_own_streams": out["own"],
-           "bits_equal": out["bits_equal"], "channels": C,
+           "ms_per_step_one_engine_duplex_pipe": out["pipe"],
+           "bits_equal": out["bits_equal"] and out["pipe_bits_equal"], "channels": C,
            "step": "encode superframe k (caller stream A) + decode superframe k - 1 (caller stream B)"}
-    log("duplex: %.1f ms/step on the shared engine stream, %.1f ms/step on own streams"
-        % (out["shared"], out["own"]))
+    log("duplex: %.1f ms/step on the shared engine stream, %.1f ms/step on own streams, "
+        "%.1f ms/step on one engine (melpe_duplex_pipe_dev)" % (out["shared"], out["own"], out["pipe"]))
     return res
 
 

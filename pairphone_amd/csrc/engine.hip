@@ -1443,8 +1443,9 @@ int melpe_npp_host(melpe_engine *e, int16_t *sp, int frames, int stride, const u
 	int rc;
 	const uint8_t *m = stage_mask(e, active, &rc);
 	if (!rc) {
-		hipMemcpyAsync(d, sp, bytes, hipMemcpyHostToDevice, e->stream);
-		rc = npp_launch(e, d, frames, stride, m, e->stream, true, 1);
+		hipError_t ec = hipMemcpyAsync(d, sp, bytes, hipMemcpyHostToDevice, e->stream);
+		rc = ec == hipSuccess ? npp_launch(e, d, frames, stride, m, e->stream, true, 1)
+				      : fail("npp copy in", ec);
 		if (!rc) {
 			hipError_t er = hipMemcpyAsync(sp, d, bytes, hipMemcpyDeviceToHost, e->stream);
 			if (er == hipSuccess)
