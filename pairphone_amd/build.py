@@ -20,6 +20,8 @@ LIB = os.path.join(ROOT, "pairphone_amd", "libmelpe_amd.so")
 EMU = os.path.join(ROOT, "build", "libmelpe_hostemu.so")
 REF = "/root/reference/melpe"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# the offload target (MELPE_ARCH for A/B builds, e.g. gfx950:xnack-)
+ARCH = os.environ.get("MELPE_ARCH", "gfx950")
 
 
 def _run(cmd, **kw):
@@ -76,7 +78,7 @@ def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=
     tag = os.path.splitext(os.path.basename(out))[0]
     objdir = os.path.join(ROOT, "build", "obj", tag)
     os.makedirs(objdir, exist_ok=True)
-    common = [HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-c",
+    common = [HIPCC, "-O3", "--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-c",
               "-Wno-unused-result", "-Wno-unused-value", '-DMELPE_TABLES_BIN="%s"' % blob] \
         + (["-DMELPE_PROF"] if prof else []) + ["-D" + d for d in defs] \
         + os.environ.get("MELPE_EXTRA_FLAGS", "").split()
@@ -97,7 +99,7 @@ def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=
         raise RuntimeError("hipcc failed for " + ", ".join(bad))
     check_no_flat(objdir)
     tmp = out + ".tmp"
-    _run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", tmp])
+    _run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + ["-o", tmp])
     os.replace(tmp, out)
     return out
 
@@ -105,16 +107,22 @@ def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=
 LLVM_BIN = "/opt/rocm/lib/llvm/bin"
 
 
-def device_disassembly(obj):
+def device_disassembly(obj, arch=None):
     """gfx950 disassembly of one hipcc object (its offload bundle), as
     {kernel symbol: [instruction lines]}"""
+    arch = arch or ARCH
     import tempfile
     with tempfile.TemporaryDirectory() as tmp:
         fat, elf = os.path.join(tmp, "fat.bin"), os.path.join(tmp, "dev.elf")
         subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=" + fat, obj], check=True)
-        subprocess.run([os.path.join(LLVM_BIN, "clang-offload-bundler"), "--unbundle", "--type=o",
-                        "--input=" + fat, "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
-                        "--output=" + elf], check=True)
+        for a in dict.fromkeys((arch, "gfx950")):	# an A/B build may mix targets
+            r = subprocess.run([os.path.join(LLVM_BIN, "clang-offload-bundler"), "--unbundle", "--type=o",
+                                "--input=" + fat, "--targets=hipv4-amdgcn-amd-amdhsa--" + a,
+                                "--output=" + elf], capture_output=True)
+            if r.returncode == 0 and os.path.getsize(elf) > 0:
+                break
+        else:
+            raise RuntimeError("no gfx950 code object in " + obj)
         txt = subprocess.run([os.path.join(LLVM_BIN, "llvm-objdump"), "-d", "--no-show-raw-insn",
                               elf], check=True, capture_output=True, text=True).stdout
     out, cur = {}, None
