@@ -63,6 +63,11 @@ TUS = ("engine", "k_npp", "k_ana", "k_ana_mw", "k_harm", "k_dec", "k_r24")
 # instead of a generic FLAT access; this is what costs compile
 # time, hence one TU per kernel, compiled in parallel
 HOT_TUS = ("k_npp", "k_ana", "k_ana_mw", "k_harm", "k_dec", "k_r24")
+# per-TU code-generation options, each kept by an A/B on MI355X: the lane
+# analysis without the scheduler's unclustered high-register-pressure
+# rescheduling stage, 25.54-25.56 -> 25.38-25.40 ms at 262,144 channels
+# (profiles/r06_sch_flags_ab.txt)
+TU_FLAGS = {"k_ana": ["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"]}
 
 
 def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=HOT_TUS, only=None):
@@ -88,7 +93,7 @@ def build_engine(force=False, prof=False, defs=(), out=None, tus_defs=None, hot=
         objs.append(o)
         if only is not None and tu not in only and os.path.exists(o):
             continue
-        extra = ["-DMELPE_INLINE_ALL"] if tu in hot else []
+        extra = (["-DMELPE_INLINE_ALL"] if tu in hot else []) + TU_FLAGS.get(tu, [])
         if tus_defs and tu in tus_defs:
             extra += ["-D" + d for d in tus_defs[tu]]
         cmd = common + extra + [os.path.join(CSRC, tu + ".hip"), "-o", o]
