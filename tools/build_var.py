@@ -20,6 +20,7 @@ from pairphone_amd import build  # noqa: E402
 
 def main(name, tus, defs):
     out = os.path.join(ROOT, "build", "var", name + ".so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     objdir = os.path.join(ROOT, "build", "obj", name)
     os.makedirs(objdir, exist_ok=True)
     for o in glob.glob(os.path.join(ROOT, "build", "obj", "libmelpe_amd", "*.o")):
